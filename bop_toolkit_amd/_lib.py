@@ -1,0 +1,167 @@
+"""ctypes binding of libbopx.so (the C-ABI declared in include/bopx.h).
+
+There is no CPU fallback anywhere in bop_toolkit_amd: if the HIP library is
+missing or no GPU is visible, load()/Context() raise. (The CPU restatement in
+oracle/ is test infrastructure and is never imported from here.)
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("BOPX_LIB", os.path.join(_HERE, "lib", "libbopx.so"))
+
+OK, E_INVALID, E_NOT_FOUND, E_HIP, E_OOM, E_UNSUPPORTED = 0, 1, 2, 3, 4, 5
+COST_STEP, COST_TLINEAR = 0, 1
+VISIB_BOP18, VISIB_BOP19 = 0, 1
+DELTA_F64 = 1
+MAX_TAUS = 16
+
+_d = ctypes.POINTER(ctypes.c_double)
+_f = ctypes.POINTER(ctypes.c_float)
+_u8 = ctypes.POINTER(ctypes.c_uint8)
+_u32 = ctypes.POINTER(ctypes.c_uint32)
+_i32 = ctypes.POINTER(ctypes.c_int32)
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_D = ctypes.c_double
+_P = ctypes.c_void_p
+_CTX = ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/bopx.h one to one.
+SIGNATURES = {
+    "bopx_version": (_I, []),
+    "bopx_device_count": (_I, [ctypes.POINTER(_I)]),
+    "bopx_create": (_I, [_I, ctypes.POINTER(_CTX)]),
+    "bopx_destroy": (None, [_CTX]),
+    "bopx_last_error": (ctypes.c_char_p, [_CTX]),
+    "bopx_synchronize": (_I, [_CTX]),
+    "bopx_stream": (_P, [_CTX]),
+    "bopx_add_object": (_I, [_CTX, _I, _d, _I64, _u32, _I64]),
+    "bopx_remove_object": (_I, [_CTX, _I]),
+    "bopx_set_symmetries": (_I, [_CTX, _I, _d, _I64]),
+    "bopx_object_slot": (_I, [_CTX, _I, ctypes.POINTER(_I)]),
+    "bopx_mssd_batch": (_I, [_CTX, _I64, _i32, _d, _d, _d]),
+    "bopx_mspd_batch": (_I, [_CTX, _I64, _i32, _d, _d, _d, _d]),
+    "bopx_add_batch": (_I, [_CTX, _I64, _i32, _d, _d, _d]),
+    "bopx_adi_batch": (_I, [_CTX, _I64, _i32, _d, _d, _d]),
+    "bopx_proj_batch": (_I, [_CTX, _I64, _i32, _d, _d, _d, _d]),
+    "bopx_vsd_batch": (_I, [_CTX, _I64, _i32, _d, _d, _i32, _f, _I64, _I, _I, _d, _D, _I, _d,
+                            _I, _I, _d, _I, _d]),
+    "bopx_vsd_from_depths": (_I, [_CTX, _I, _I, _f, _f, _f, _D, _D, _D, _D, _D, _I, _d, _I, _I,
+                                  _D, _I, _d]),
+    "bopx_render_depth": (_I, [_CTX, _I, _d, _d, _D, _D, _D, _D, _I, _I, _f]),
+    "bopx_dist_im": (_I, [_CTX, _I, _I, _f, _D, _D, _D, _D, _d]),
+    "bopx_visib_mask": (_I, [_CTX, _I64, _d, _d, _u8, _D, _I, _I, _u8]),
+    "bopx_mssd_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _P]),
+    "bopx_mspd_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _P, _P]),
+    "bopx_add_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _P]),
+    "bopx_adi_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _P]),
+    "bopx_vsd_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _P, _I, _I, _P, _D, _I, _d, _I, _I,
+                                _P, _I, _P, _P]),
+    "bopx_depth_clear_dev": (_I, [_CTX, _P, _I64, _P]),
+    "bopx_render_depth_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _P, _I, _I, _P]),
+    "bopx_depth_finish_dev": (_I, [_CTX, _P, _I64, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class BopxError(RuntimeError):
+  pass
+
+
+def load():
+  """Load libbopx.so (raises ImportError if it has not been built)."""
+  global _lib
+  with _lock:
+    if _lib is None:
+      if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "libbopx.so not found at %s: build it with `python -c 'import __graft_entry__ as g;"
+            " g.build()'` (bop_toolkit_amd has no CPU fallback)" % LIB_PATH)
+      L = ctypes.CDLL(LIB_PATH)
+      for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+      _lib = L
+  return _lib
+
+
+def ptr(a, ct):
+  return a.ctypes.data_as(ct) if a is not None else None
+
+
+def device_count():
+  n = _I(0)
+  load().bopx_device_count(ctypes.byref(n))
+  return n.value
+
+
+class Context:
+  """One libbopx context (a HIP device + stream + the resident object registry)."""
+
+  def __init__(self, device=0):
+    L = load()
+    h = _CTX()
+    rc = L.bopx_create(int(device), ctypes.byref(h))
+    if rc != OK or not h.value:
+      raise BopxError("bopx_create(device=%d) failed (rc=%d): no usable HIP device; "
+                      "bop_toolkit_amd has no CPU fallback" % (device, rc))
+    self.h = h
+    self.device = int(device)
+    self.lib = L
+
+  def close(self):
+    if self.h is not None and self.h.value:
+      self.lib.bopx_destroy(self.h)
+    self.h = None
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:
+      pass
+
+  def check(self, rc, what=""):
+    if rc == OK:
+      return
+    msg = self.lib.bopx_last_error(self.h).decode(errors="replace")
+    if rc == E_INVALID:
+      raise ValueError(msg)
+    if rc == E_NOT_FOUND:
+      raise KeyError(msg)
+    raise BopxError("%s failed (rc=%d): %s" % (what, rc, msg))
+
+  def call(self, name, *args):
+    self.check(getattr(self.lib, name)(self.h, *args), name)
+
+  def stream(self):
+    return self.lib.bopx_stream(self.h)
+
+  def slot(self, obj_id):
+    s = _I(-1)
+    rc = self.lib.bopx_object_slot(self.h, int(obj_id), ctypes.byref(s))
+    if rc != OK:
+      raise KeyError("unknown obj_id %r" % (obj_id,))
+    return s.value
+
+  # -- registry ---------------------------------------------------------------
+  def add_object(self, obj_id, pts, faces=None):
+    pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
+    if faces is None:
+      faces = np.zeros((0, 3), np.uint32)
+    faces = np.ascontiguousarray(faces, np.uint32).reshape(-1, 3)
+    self.call("bopx_add_object", int(obj_id), ptr(pts, _d), len(pts), ptr(faces, _u32),
+              len(faces))
+
+  def remove_object(self, obj_id):
+    self.call("bopx_remove_object", int(obj_id))
+
+  def set_symmetries(self, obj_id, syms12):
+    syms12 = np.ascontiguousarray(syms12, np.float64).reshape(-1, 12)
+    self.call("bopx_set_symmetries", int(obj_id), ptr(syms12, _d), len(syms12))

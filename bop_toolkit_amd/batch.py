@@ -1,0 +1,133 @@
+"""Batched, HBM-resident pose-error evaluation (the throughput path).
+
+The reference evaluates one (est, gt) tuple per Python call
+(eval_calc_errors.py:281-378). Here a whole batch of tuples lives in HBM as
+structure-of-arrays torch tensors and each error type is ONE kernel launch:
+
+  k_vsd         fused raster + VSD for every tuple      (pose_error.py:17-93)
+  k_sym_error   every (tuple, symmetry) pair, MSSD/MSPD (pose_error.py:96-144)
+  k_mean_error  ADD / PROJ                              (pose_error.py:147-161, 217-232)
+  k_adi         exact-NN ADI                            (pose_error.py:164-184)
+
+Tensor conventions (all on the evaluator's device):
+  slots     int32 [n]       object slots (BatchEvaluator.slots)
+  pose_*    float64 [n, 12] [R row-major | t]
+  K         float64 [n, 9]  full intrinsics (MSPD/PROJ)
+  frames    float32 [n_frames, H, W] test depth in mm
+  frame_idx int32 [n]       frame of each tuple
+  cam       float64 [n_frames, 4] (fx, fy, cx, cy)
+torch provides device memory and the stream; the arithmetic is all libbopx.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from .misc import symmetries_to_array
+
+
+def _stream(dev):
+  return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _p(t):
+  return t.data_ptr() if t is not None else None
+
+
+class BatchEvaluator:
+  """Registry of resident objects + batched error launches on one GPU."""
+
+  def __init__(self, device=0):
+    self.device = torch.device("cuda", int(device))
+    torch.cuda.set_device(self.device)
+    self.ctx = _lib.Context(int(device))
+    self.objects = {}
+
+  # -- registry ---------------------------------------------------------------
+  def add_object(self, obj_id, pts, faces=None, syms=None, diameter=None):
+    """Upload one object. syms: list of {'R','t'} (misc.get_symmetry_
+    transformations) or an S x 12 array; diameter: models_info 'diameter'."""
+    self.ctx.add_object(obj_id, pts, faces)
+    if syms is not None:
+      s12 = syms if isinstance(syms, np.ndarray) else symmetries_to_array(syms)
+      self.ctx.set_symmetries(obj_id, s12)
+    self.objects[obj_id] = {
+        "slot": self.ctx.slot(obj_id), "nv": len(pts),
+        "nf": 0 if faces is None else len(faces),
+        "ns": 0 if syms is None else len(syms), "diameter": diameter}
+
+  def slots(self, obj_ids):
+    """int32 device tensor of slots for a sequence of obj_ids."""
+    table = {k: v["slot"] for k, v in self.objects.items()}
+    s = np.fromiter((table[int(o)] for o in obj_ids), np.int32, count=len(obj_ids))
+    return torch.from_numpy(s).to(self.device)
+
+  # -- launches (async on the current torch stream) ---------------------------
+  def _out(self, n, cols=None):
+    shape = (n,) if cols is None else (n, cols)
+    return torch.empty(shape, dtype=torch.float64, device=self.device)
+
+  def mssd(self, slots, pose_est, pose_gt, out=None):
+    n = slots.numel()
+    out = self._out(n) if out is None else out
+    self.ctx.call("bopx_mssd_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(out),
+                  _stream(self.device))
+    return out
+
+  def mspd(self, slots, pose_est, pose_gt, K, out=None):
+    n = slots.numel()
+    out = self._out(n) if out is None else out
+    self.ctx.call("bopx_mspd_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(K),
+                  _p(out), _stream(self.device))
+    return out
+
+  def add(self, slots, pose_est, pose_gt, out=None):
+    n = slots.numel()
+    out = self._out(n) if out is None else out
+    self.ctx.call("bopx_add_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(out),
+                  _stream(self.device))
+    return out
+
+  def adi(self, slots, pose_est, pose_gt, out=None):
+    n = slots.numel()
+    out = self._out(n) if out is None else out
+    self.ctx.call("bopx_adi_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(out),
+                  _stream(self.device))
+    return out
+
+  def vsd(self, slots, pose_est, pose_gt, frame_idx, frames, cam, delta, taus, diameters,
+          normalized_by_diameter=True, cost_type="step", out=None, delta_flags=0):
+    n = slots.numel()
+    taus = np.ascontiguousarray(taus, np.float64)
+    code = {"step": _lib.COST_STEP, "tlinear": _lib.COST_TLINEAR}.get(cost_type)
+    if code is None:
+      raise ValueError("Unknown pixel matching cost.")
+    H, W = int(frames.shape[-2]), int(frames.shape[-1])
+    out = self._out(n, len(taus)) if out is None else out
+    self.ctx.call("bopx_vsd_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(frame_idx),
+                  _p(frames), W, H, _p(cam), float(delta), int(delta_flags),
+                  taus.ctypes.data_as(_lib._d), len(taus), int(bool(normalized_by_diameter)),
+                  _p(diameters), code, _p(out), _stream(self.device))
+    return out
+
+  def render(self, slots, pose, frame_idx, cam, n_frames, width, height, frames=None):
+    """Min-composite depth renders of many instances into n_frames frames
+    (instances sharing a frame occlude each other). Returns float32 frames."""
+    if frames is None:
+      frames = torch.empty((n_frames, height, width), dtype=torch.float32, device=self.device)
+    npx = frames.numel()
+    s = _stream(self.device)
+    self.ctx.call("bopx_depth_clear_dev", _p(frames), npx, s)
+    self.ctx.call("bopx_render_depth_batch_dev", slots.numel(), _p(slots), _p(pose),
+                  _p(frame_idx), _p(cam), _p(frames), width, height, s)
+    self.ctx.call("bopx_depth_finish_dev", _p(frames), npx, s)
+    return frames
+
+  def bop19(self, slots, pose_est, pose_gt, K, frame_idx, frames, cam, delta, taus, diameters,
+            out_vsd=None, out_mssd=None, out_mspd=None):
+    """The BOP19 error set of every tuple: VSD (per tau), MSSD and MSPD
+    (eval_bop19_pose.py:21-53), three launches on one stream."""
+    v = self.vsd(slots, pose_est, pose_gt, frame_idx, frames, cam, delta, taus, diameters,
+                 out=out_vsd)
+    m = self.mssd(slots, pose_est, pose_gt, out=out_mssd)
+    p = self.mspd(slots, pose_est, pose_gt, K, out=out_mspd)
+    return {"vsd": v, "mssd": m, "mspd": p}

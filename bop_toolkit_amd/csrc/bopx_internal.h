@@ -1,0 +1,82 @@
+// bopx_internal.h — device-side data layout shared by the gfx950 kernels and the
+// runtime (runtime.hip). Not part of the public C-ABI (include/bopx.h).
+//
+// HBM layout of one registered object:
+//   pts   : float64 SoA  x[nv] | y[nv] | z[nv]       (point errors, fp64 math)
+//   vtx   : float32x4    (x, y, z, 0) per vertex     (rasteriser, GL-like fp32)
+//   faces : uint32 x3 per triangle, re-ordered into meshlets of 64 triangles
+//           sorted by the Morton code of the triangle centroid
+//   mlet  : float32 x8 per meshlet: min xyz, 0, max xyz, 0 (object-space AABB
+//           of the meshlet's float32 vertices; used for conservative culling)
+//   syms  : float64 x12 per symmetry [R row-major | t]
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bopx {
+
+constexpr int kMeshletTris = 64;    // one wave lane per triangle
+constexpr int kMaxMeshlets = 1024;  // per object => <= 65,536 triangles for VSD
+constexpr int kMaxTaus = 16;
+constexpr int kTileW = 64;          // VSD screen tile (LDS-resident depth pair)
+constexpr int kTileH = 64;
+constexpr float kGuardBand = 16384.0f;  // |u|,|v| limit of a rasterised vertex (px)
+
+struct ObjDesc {
+  const double* pts;      // 3*nv, SoA
+  const float4* vtx;      // nv
+  const uint32_t* faces;  // 3*nf (meshlet order)
+  const float* mlet;      // 8*nm
+  const double* syms;     // 12*ns
+  int nv, nf, nm, ns;
+};
+
+struct VsdArgs {
+  const ObjDesc* objs;
+  const int32_t* slots;
+  const double* pose_est;
+  const double* pose_gt;
+  const int32_t* frame_idx;
+  const float* frames;
+  const double* cam;  // per frame: fx fy cx cy
+  const double* diameters;
+  double* out;
+  int64_t n;
+  int width, height;
+  float delta32;
+  int delta_f64;
+  double delta64;
+  int n_tau;
+  int normalized;
+  double taus[kMaxTaus];
+};
+
+// Launchers (kernels in kern_pose.hip / kern_vsd.hip). All return hipError_t of
+// the launch; inputs are device pointers.
+hipError_t launch_sym_error(int mode, const ObjDesc* objs, int64_t n, const int32_t* slots,
+                            const double* pe, const double* pg, const double* K, double* out,
+                            hipStream_t s);  // mode 0 = MSSD, 1 = MSPD
+hipError_t launch_mean_error(int mode, const ObjDesc* objs, int64_t n, const int32_t* slots,
+                             const double* pe, const double* pg, const double* K, double* out,
+                             hipStream_t s);  // mode 0 = ADD, 1 = PROJ
+hipError_t launch_adi(const ObjDesc* objs, int64_t n, const int32_t* slots, const double* pe,
+                      const double* pg, double* out, hipStream_t s);
+hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s);
+hipError_t launch_vsd_depths(int W, int H, const float* dt, const float* de, const float* dg,
+                             double fx, double fy, double cx, double cy, float delta32,
+                             int delta_f64, double delta64, const double* taus_host, int n_tau,
+                             int normalized, double diameter, double* partials, int n_blocks,
+                             hipStream_t s);
+int vsd_depths_blocks(int W, int H);
+hipError_t launch_dist_im(int W, int H, const float* depth, double fx, double fy, double cx,
+                          double cy, double* out, hipStream_t s);
+hipError_t launch_visib(int64_t n, const double* dt, const double* dm, const uint8_t* vg,
+                        float delta32, int delta_f64, double delta64, int mode, uint8_t* out,
+                        hipStream_t s);
+hipError_t launch_depth_fill(float* frames, int64_t n_pixels, int to_background,
+                             hipStream_t s);
+hipError_t launch_render_batch(const ObjDesc* objs, int max_nf, int64_t n, const int32_t* slots,
+                               const double* pose, const int32_t* frame_idx, const double* cam,
+                               float* frames, int W, int H, hipStream_t s);
+
+}  // namespace bopx

@@ -1,0 +1,480 @@
+// kern_vsd.hip — fused depth raster + Visible Surface Discrepancy on gfx950.
+//
+// Reference path (per tuple, pose_error.py:17-93):
+//   2 GL renders (renderer_vispy.py:433-538) -> 3 full-frame float64 distance
+//   images (misc.py:143-163) -> 2 visibility masks (visibility.py:9-75) ->
+//   inter/union counts -> per-tau step (or truncated-linear) cost.
+//
+// Here ONE launch evaluates a whole batch: one 256-thread workgroup per tuple.
+//  1. The object's meshlets (64 triangles each) are culled per pose: the 8
+//     corners of each meshlet AABB are projected (float32, same arithmetic as
+//     the vertices) into a conservative pixel rectangle kept in LDS. Their
+//     union is the tuple's region of interest (ROI): pixels outside both
+//     silhouettes cannot change VSD (masks need d_model > 0, visibility.py:37).
+//  2. The ROI is swept in 64x64 screen tiles. Per tile, both depth buffers
+//     (est, gt) live in LDS (2 x 16 KiB, +inf cleared); the meshlets whose
+//     rectangle touches the tile are listed, and each wave rasterises one
+//     meshlet per step (lane = triangle) with exact integer edge functions and
+//     an LDS atomicMin on the float bits (order-independent z-buffer).
+//  3. The tile's pixels are then evaluated in place: test depth is read from
+//     HBM (coalesced rows), the three float64 distances and the float32
+//     visibility tests follow the reference operation order exactly
+//     (-ffp-contract=off), and integer counters (union, inter, per-tau) stay
+//     in registers. Pixels covered by neither pose are skipped.
+//  4. Counters are reduced across the workgroup; one thread writes
+//     e_k = (cnt_k + comp) / union (1.0 when union == 0).
+// Results are bit-identical to the reference given identical depth maps.
+#include "raster.h"
+
+namespace bopx {
+
+constexpr int kVsdThreads = 256;
+constexpr uint32_t kInfBits = 0x7F800000u;
+
+// float64 distance of a float32 depth at pixel (pX, pY) (misc.py:158-161).
+__device__ __forceinline__ double dist_of(double pX, double pY, float depth) {
+  const double d = (double)depth;
+  const double a = pX * d, b = pY * d;
+  return sqrt((a * a + b * b) + d * d);
+}
+
+// visibility._estimate_visib_mask, bop19 (visibility.py:34-37).
+__device__ __forceinline__ bool visib19(double dt, double dm, float delta32, int delta_f64,
+                                        double delta64) {
+  const float diff = (float)dm - (float)dt;
+  const bool le = delta_f64 ? ((double)diff <= delta64) : (diff <= delta32);
+  return (le || dt == 0.0) && dm > 0.0;
+}
+
+// Conservative pixel rectangle of one meshlet AABB under a pose. Any corner with
+// Z <= 0 (or a non-finite projection) gives the whole image.
+__device__ __forceinline__ short4 meshlet_rect(const float* __restrict__ mb, const float* Rf,
+                                               const Cam32& c, int W, int H) {
+  float umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
+  bool full = false;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float x = (k & 1) ? mb[4] : mb[0];
+    const float y = (k & 2) ? mb[5] : mb[1];
+    const float z = (k & 4) ? mb[6] : mb[2];
+    const float X = ((Rf[0] * x + Rf[1] * y) + Rf[2] * z) + Rf[9];
+    const float Y = ((Rf[3] * x + Rf[4] * y) + Rf[5] * z) + Rf[10];
+    const float Z = ((Rf[6] * x + Rf[7] * y) + Rf[8] * z) + Rf[11];
+    if (!(Z > 0.0f)) {
+      full = true;
+    } else {
+      const float u = (c.fx * X) / Z + c.cx, v = (c.fy * Y) / Z + c.cy;
+      umin = fminf(umin, u);
+      umax = fmaxf(umax, u);
+      vmin = fminf(vmin, v);
+      vmax = fmaxf(vmax, v);
+    }
+  }
+  if (full || !(umin == umin) || !(vmin == vmin) || !(umax == umax) || !(vmax == vmax))
+    return make_short4(0, 0, (short)(W - 1), (short)(H - 1));
+  // pixel col is sampled at col + 0.5; one pixel of margin for rounding.
+  const float fx0 = floorf(umin - 0.5f) - 1.0f, fx1 = ceilf(umax - 0.5f) + 1.0f;
+  const float fy0 = floorf(vmin - 0.5f) - 1.0f, fy1 = ceilf(vmax - 0.5f) + 1.0f;
+  if (fx1 < 0.0f || fy1 < 0.0f || fx0 > (float)(W - 1) || fy0 > (float)(H - 1))
+    return make_short4(1, 1, 0, 0);  // empty
+  const int x0 = (int)fmaxf(fx0, 0.0f), y0 = (int)fmaxf(fy0, 0.0f);
+  const int x1 = (int)fminf(fx1, (float)(W - 1)), y1 = (int)fminf(fy1, (float)(H - 1));
+  return make_short4((short)x0, (short)y0, (short)x1, (short)y1);
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int COST>  // 0 = step, 1 = tlinear
+__global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
+  __shared__ uint32_t s_dep[2][kTileW * kTileH];
+  __shared__ short4 s_rect[2 * kMaxMeshlets];
+  __shared__ uint16_t s_list[2 * kMaxMeshlets];
+  __shared__ float s_pose[2][12];
+  __shared__ int s_roi[4];
+  __shared__ int s_nlist;
+  __shared__ uint32_t s_cnt[kVsdThreads / 64][2 + kMaxTaus];
+  __shared__ double s_lin[kVsdThreads / 64][kMaxTaus];
+
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const ObjDesc o = a.objs[a.slots[b]];
+  const int W = a.width, H = a.height, nm = o.nm, nf = o.nf;
+  const int64_t fidx = a.frame_idx[b];
+  const float* __restrict__ frame = a.frames + fidx * (int64_t)W * H;
+  const double fx = a.cam[4 * fidx + 0], fy = a.cam[4 * fidx + 1];
+  const double cx = a.cam[4 * fidx + 2], cy = a.cam[4 * fidx + 3];
+  Cam32 c32;
+  c32.fx = (float)fx;
+  c32.fy = (float)fy;
+  c32.cx = (float)cx;
+  c32.cy = (float)cy;
+  if (tid < 12) {
+    s_pose[0][tid] = (float)a.pose_est[12 * b + tid];
+    s_pose[1][tid] = (float)a.pose_gt[12 * b + tid];
+  }
+  if (tid == 0) {
+    s_roi[0] = s_roi[1] = 0x7FFFFFFF;
+    s_roi[2] = s_roi[3] = -1;
+  }
+  __syncthreads();
+
+  // 1. per-pose meshlet rectangles + ROI.
+  for (int i = tid; i < 2 * nm; i += kVsdThreads) {
+    const int r = i >= nm, m = i - r * nm;
+    const short4 rc = meshlet_rect(o.mlet + 8 * (int64_t)m, s_pose[r], c32, W, H);
+    s_rect[i] = rc;
+    if (rc.x <= rc.z && rc.y <= rc.w) {
+      atomicMin(&s_roi[0], (int)rc.x);
+      atomicMin(&s_roi[1], (int)rc.y);
+      atomicMax(&s_roi[2], (int)rc.z);
+      atomicMax(&s_roi[3], (int)rc.w);
+    }
+  }
+  __syncthreads();
+  const int rx0 = s_roi[0], ry0 = s_roi[1], rx1 = s_roi[2], ry1 = s_roi[3];
+
+  uint32_t c_union = 0, c_inter = 0;
+  uint32_t c_tau[kMaxTaus];
+  double lin[kMaxTaus];
+#pragma unroll
+  for (int k = 0; k < kMaxTaus; ++k) {
+    c_tau[k] = 0;
+    lin[k] = 0.0;
+  }
+
+  if (rx0 <= rx1 && ry0 <= ry1) {
+    const int ntx = (rx1 - rx0 + kTileW) / kTileW, nty = (ry1 - ry0 + kTileH) / kTileH;
+    for (int t = 0; t < ntx * nty; ++t) {
+      const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
+      const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
+      // 2a. clear both depth tiles, list the meshlets touching the tile.
+      uint32_t* dep_flat = &s_dep[0][0];
+      for (int i = tid; i < 2 * kTileW * kTileH; i += kVsdThreads) dep_flat[i] = kInfBits;
+      if (tid == 0) s_nlist = 0;
+      __syncthreads();
+      for (int i = tid; i < 2 * nm; i += kVsdThreads) {
+        const short4 rc = s_rect[i];
+        if (rc.x <= tx1 && rc.z >= tx0 && rc.y <= ty1 && rc.w >= ty0 && rc.x <= rc.z &&
+            rc.y <= rc.w)
+          s_list[atomicAdd(&s_nlist, 1)] = (uint16_t)i;
+      }
+      __syncthreads();
+      // 2b. rasterise: one meshlet per wave step, one triangle per lane.
+      const int nl = s_nlist;
+      for (int li = wave; li < nl; li += kVsdThreads / 64) {
+        const int e = s_list[li];
+        const int r = e >= nm, m = e - r * nm;
+        const int tri = m * kMeshletTris + lane;
+        if (tri < nf) {
+          const uint32_t i0 = o.faces[3 * (int64_t)tri], i1 = o.faces[3 * (int64_t)tri + 1],
+                         i2 = o.faces[3 * (int64_t)tri + 2];
+          const float4 v0 = o.vtx[i0], v1 = o.vtx[i1], v2 = o.vtx[i2];
+          const float* Rf = s_pose[r];
+          const RVtx A = r_vertex(Rf, c32, v0.x, v0.y, v0.z);
+          const RVtx B = r_vertex(Rf, c32, v1.x, v1.y, v1.z);
+          const RVtx C = r_vertex(Rf, c32, v2.x, v2.y, v2.z);
+          RTri T;
+          if (r_setup(A, B, C, T)) {
+            const int cc0 = max(T.c0, tx0), cc1 = min(T.c1, tx1);
+            const int rr0 = max(T.r0, ty0), rr1 = min(T.r1, ty1);
+            uint32_t* dep = s_dep[r];
+            for (int row = rr0; row <= rr1; ++row)
+              for (int col = cc0; col <= cc1; ++col) {
+                float z;
+                if (r_fragment(T, col, row, z))
+                  atomicMin(&dep[(row - ty0) * kTileW + (col - tx0)], __float_as_uint(z));
+              }
+          }
+        }
+      }
+      __syncthreads();
+      // 3. per-pixel distances, visibility masks, counters.
+      for (int p = tid; p < kTileW * kTileH; p += kVsdThreads) {
+        const int row = ty0 + p / kTileW, col = tx0 + p % kTileW;
+        if (row > ty1 || col > tx1) continue;
+        const uint32_t ue = s_dep[0][p], ug = s_dep[1][p];
+        if (ue == kInfBits && ug == kInfBits) continue;
+        const float de = ue == kInfBits ? 0.0f : __uint_as_float(ue);
+        const float dg = ug == kInfBits ? 0.0f : __uint_as_float(ug);
+        const float dtest = frame[(int64_t)row * W + col];
+        const double pX = ((double)col - cx) / fx;
+        const double pY = ((double)row - cy) / fy;
+        const double dist_t = dist_of(pX, pY, dtest);
+        const double dist_g = dist_of(pX, pY, dg);
+        const double dist_e = dist_of(pX, pY, de);
+        const bool vg = visib19(dist_t, dist_g, a.delta32, a.delta_f64, a.delta64);
+        bool ve = visib19(dist_t, dist_e, a.delta32, a.delta_f64, a.delta64);
+        ve = ve || (vg && dist_e > 0.0);  // visibility.py:74
+        c_union += (vg || ve);
+        if (vg && ve) {
+          ++c_inter;
+          double dd = fabs(dist_g - dist_e);
+          if (a.normalized) dd /= a.diameters[b];
+#pragma unroll
+          for (int k = 0; k < kMaxTaus; ++k) {
+            if (k < a.n_tau) {
+              if (COST == 0) {
+                c_tau[k] += (dd >= a.taus[k]);
+              } else {
+                const double cst = dd / a.taus[k];
+                lin[k] += cst > 1.0 ? 1.0 : cst;
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // 4. workgroup reduction (fixed order) and the error formula (pose_error.py:75-91).
+  c_union = wave_sum_u32(c_union);
+  c_inter = wave_sum_u32(c_inter);
+#pragma unroll
+  for (int k = 0; k < kMaxTaus; ++k) {
+    if (COST == 0)
+      c_tau[k] = wave_sum_u32(c_tau[k]);
+    else
+      lin[k] = wave_sum_f64(lin[k]);
+  }
+  if (lane == 0) {
+    s_cnt[wave][0] = c_union;
+    s_cnt[wave][1] = c_inter;
+#pragma unroll
+    for (int k = 0; k < kMaxTaus; ++k) {
+      s_cnt[wave][2 + k] = c_tau[k];
+      s_lin[wave][k] = lin[k];
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t un = 0, in = 0;
+    for (int w = 0; w < kVsdThreads / 64; ++w) {
+      un += s_cnt[w][0];
+      in += s_cnt[w][1];
+    }
+    double* out = a.out + b * (int64_t)a.n_tau;
+    for (int k = 0; k < a.n_tau; ++k) {
+      if (un == 0) {
+        out[k] = 1.0;
+      } else if (COST == 0) {
+        uint64_t cnt = 0;
+        for (int w = 0; w < kVsdThreads / 64; ++w) cnt += s_cnt[w][2 + k];
+        out[k] = (double)(cnt + (un - in)) / (double)un;
+      } else {
+        double sum = 0.0;
+        for (int w = 0; w < kVsdThreads / 64; ++w) sum += s_lin[w][k];
+        out[k] = (sum + (double)(un - in)) / (double)un;
+      }
+    }
+  }
+}
+
+hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s) {
+  if (a.n <= 0) return hipSuccess;
+  dim3 grid((unsigned)a.n), block(kVsdThreads);
+  if (cost_type == 0)
+    hipLaunchKernelGGL(k_vsd<0>, grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL(k_vsd<1>, grid, block, 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// VSD given three host-supplied depth maps (foreign renderer path). Each block
+// reduces 4096 pixels into one partial row [union, inter, cnt[n_tau], lin[n_tau]]
+// (float64, exact for counts); the host sums the rows in order.
+constexpr int kDepthsPix = 4096;
+
+int vsd_depths_blocks(int W, int H) {
+  return (int)(((int64_t)W * H + kDepthsPix - 1) / kDepthsPix);
+}
+
+struct TauArr {
+  double v[kMaxTaus];
+};
+
+__global__ __launch_bounds__(kVsdThreads) void k_vsd_depths(
+    int W, int H, const float* __restrict__ dt, const float* __restrict__ de,
+    const float* __restrict__ dg, double fx, double fy, double cx, double cy, float delta32,
+    int delta_f64, double delta64, TauArr taus, int n_tau, int normalized, double diameter,
+    double* __restrict__ partials) {
+  __shared__ double s_p[kVsdThreads / 64][2 + 2 * kMaxTaus];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t npx = (int64_t)W * H;
+  double acc[2 + 2 * kMaxTaus];
+#pragma unroll
+  for (int k = 0; k < 2 + 2 * kMaxTaus; ++k) acc[k] = 0.0;
+  for (int j = tid; j < kDepthsPix; j += kVsdThreads) {
+    const int64_t i = (int64_t)blockIdx.x * kDepthsPix + j;
+    if (i >= npx) break;
+    const int row = (int)(i / W), col = (int)(i % W);
+    const double pX = ((double)col - cx) / fx, pY = ((double)row - cy) / fy;
+    const double dist_t = dist_of(pX, pY, dt[i]);
+    const double dist_g = dist_of(pX, pY, dg[i]);
+    const double dist_e = dist_of(pX, pY, de[i]);
+    const bool vg = visib19(dist_t, dist_g, delta32, delta_f64, delta64);
+    bool ve = visib19(dist_t, dist_e, delta32, delta_f64, delta64);
+    ve = ve || (vg && dist_e > 0.0);
+    acc[0] += (vg || ve) ? 1.0 : 0.0;
+    if (vg && ve) {
+      acc[1] += 1.0;
+      double dd = fabs(dist_g - dist_e);
+      if (normalized) dd /= diameter;
+#pragma unroll
+      for (int k = 0; k < kMaxTaus; ++k) {
+        if (k < n_tau) {
+          acc[2 + k] += (dd >= taus.v[k]) ? 1.0 : 0.0;
+          const double cst = dd / taus.v[k];
+          acc[2 + kMaxTaus + k] += cst > 1.0 ? 1.0 : cst;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2 + 2 * kMaxTaus; ++k) acc[k] = wave_sum_f64(acc[k]);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 2 + 2 * kMaxTaus; ++k) s_p[wave][k] = acc[k];
+  __syncthreads();
+  if (tid < 2 + 2 * kMaxTaus) {
+    double v = 0.0;
+    for (int w = 0; w < kVsdThreads / 64; ++w) v += s_p[w][tid];
+    partials[(int64_t)blockIdx.x * (2 + 2 * kMaxTaus) + tid] = v;
+  }
+}
+
+hipError_t launch_vsd_depths(int W, int H, const float* dt, const float* de, const float* dg,
+                             double fx, double fy, double cx, double cy, float delta32,
+                             int delta_f64, double delta64, const double* taus_host, int n_tau,
+                             int normalized, double diameter, double* partials, int n_blocks,
+                             hipStream_t s) {
+  TauArr ta;
+  for (int k = 0; k < kMaxTaus; ++k) ta.v[k] = k < n_tau ? taus_host[k] : 1.0;
+  hipLaunchKernelGGL(k_vsd_depths, dim3(n_blocks), dim3(kVsdThreads), 0, s, W, H, dt, de, dg, fx,
+                     fy, cx, cy, delta32, delta_f64, delta64, ta, n_tau, normalized, diameter,
+                     partials);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// misc.depth_im_to_dist_im_fast (misc.py:143-163), elementwise.
+__global__ void k_dist_im(int W, int H, const float* __restrict__ depth, double fx, double fy,
+                          double cx, double cy, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)W * H) return;
+  const int row = (int)(i / W), col = (int)(i % W);
+  out[i] = dist_of(((double)col - cx) / fx, ((double)row - cy) / fy, depth[i]);
+}
+
+hipError_t launch_dist_im(int W, int H, const float* depth, double fx, double fy, double cx,
+                          double cy, double* out, hipStream_t s) {
+  const int64_t n = (int64_t)W * H;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_dist_im, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, H, depth,
+                     fx, fy, cx, cy, out);
+  return hipGetLastError();
+}
+
+// visibility._estimate_visib_mask (+ estimate_visib_mask_est's OR), elementwise.
+__global__ void k_visib(int64_t n, const double* __restrict__ dt, const double* __restrict__ dm,
+                        const uint8_t* __restrict__ vg, float delta32, int delta_f64,
+                        double delta64, int mode, uint8_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double t = dt[i], m = dm[i];
+  const float diff = (float)m - (float)t;
+  const bool le = delta_f64 ? ((double)diff <= delta64) : (diff <= delta32);
+  bool v = mode == 0 ? (le && t > 0.0 && m > 0.0) : ((le || t == 0.0) && m > 0.0);
+  if (vg) v = v || (vg[i] && m > 0.0);
+  out[i] = v ? 1 : 0;
+}
+
+hipError_t launch_visib(int64_t n, const double* dt, const double* dm, const uint8_t* vg,
+                        float delta32, int delta_f64, double delta64, int mode, uint8_t* out,
+                        hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_visib, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, dt, dm, vg,
+                     delta32, delta_f64, delta64, mode, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Batched full-frame renderer: one thread per (instance, triangle), global
+// atomicMin z-buffer. Frames are +inf-filled first and background-mapped after.
+__global__ void k_depth_fill(uint32_t* __restrict__ f, int64_t n, int to_background) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (to_background) {
+    if (f[i] == kInfBits) f[i] = 0u;
+  } else {
+    f[i] = kInfBits;
+  }
+}
+
+hipError_t launch_depth_fill(float* frames, int64_t n_pixels, int to_background,
+                             hipStream_t s) {
+  if (n_pixels <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_depth_fill, dim3((unsigned)((n_pixels + 255) / 256)), dim3(256), 0, s,
+                     (uint32_t*)frames, n_pixels, to_background);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_render_batch(const ObjDesc* __restrict__ objs,
+                                                      int64_t inst0,
+                                                      const int32_t* __restrict__ slots,
+                                                      const double* __restrict__ pose,
+                                                      const int32_t* __restrict__ frame_idx,
+                                                      const double* __restrict__ cam,
+                                                      uint32_t* __restrict__ frames, int W,
+                                                      int H) {
+  __shared__ float s_pose[12];
+  const int64_t inst = inst0 + blockIdx.y;
+  const ObjDesc o = objs[slots[inst]];
+  if (threadIdx.x < 12) s_pose[threadIdx.x] = (float)pose[12 * inst + threadIdx.x];
+  __syncthreads();
+  const int tri = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tri >= o.nf) return;
+  const int64_t f = frame_idx[inst];
+  Cam32 c;
+  c.fx = (float)cam[4 * f];
+  c.fy = (float)cam[4 * f + 1];
+  c.cx = (float)cam[4 * f + 2];
+  c.cy = (float)cam[4 * f + 3];
+  const float4 v0 = o.vtx[o.faces[3 * (int64_t)tri]], v1 = o.vtx[o.faces[3 * (int64_t)tri + 1]],
+               v2 = o.vtx[o.faces[3 * (int64_t)tri + 2]];
+  RTri T;
+  if (!r_setup(r_vertex(s_pose, c, v0.x, v0.y, v0.z), r_vertex(s_pose, c, v1.x, v1.y, v1.z),
+               r_vertex(s_pose, c, v2.x, v2.y, v2.z), T))
+    return;
+  const int c0 = max(T.c0, 0), c1 = min(T.c1, W - 1), r0 = max(T.r0, 0), r1 = min(T.r1, H - 1);
+  uint32_t* fr = frames + f * (int64_t)W * H;
+  for (int row = r0; row <= r1; ++row)
+    for (int col = c0; col <= c1; ++col) {
+      float z;
+      if (r_fragment(T, col, row, z)) atomicMin(&fr[(int64_t)row * W + col], __float_as_uint(z));
+    }
+}
+
+hipError_t launch_render_batch(const ObjDesc* objs, int max_nf, int64_t n, const int32_t* slots,
+                               const double* pose, const int32_t* frame_idx, const double* cam,
+                               float* frames, int W, int H, hipStream_t s) {
+  const unsigned gx = (unsigned)((max_nf + 255) / 256);
+  for (int64_t i0 = 0; i0 < n; i0 += 65535) {
+    const unsigned gy = (unsigned)(n - i0 < 65535 ? n - i0 : 65535);
+    hipLaunchKernelGGL(k_render_batch, dim3(gx, gy), dim3(256), 0, s, objs, i0, slots, pose,
+                       frame_idx, cam, (uint32_t*)frames, W, H);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace bopx

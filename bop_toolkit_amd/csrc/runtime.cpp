@@ -1,0 +1,754 @@
+// runtime.cpp — libbopx host runtime: contexts, the on-device object registry
+// (meshes, meshlets, symmetry tables) and the C-ABI of include/bopx.h.
+//
+// The registry is what renderer.add_object (renderer_vispy.py:291-418) and the
+// per-dataset precompute of eval_calc_errors.py:162-191 (models, symmetries)
+// amount to: every object is uploaded once and stays resident in HBM, so a
+// batch of tuples touches only its poses, its test depth and its outputs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/bopx.h"
+#include "bopx_internal.h"
+
+using bopx::ObjDesc;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+};
+
+struct Object {
+  int obj_id = -1;
+  bool live = false;
+  int64_t nv = 0, nf = 0, nm = 0, ns = 0;
+  double* d_pts = nullptr;
+  float4* d_vtx = nullptr;
+  uint32_t* d_faces = nullptr;
+  float* d_mlet = nullptr;
+  double* d_syms = nullptr;
+};
+
+}  // namespace
+
+struct bopx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::unordered_map<int, int> slot_of;
+  std::vector<Object> objs;
+  ObjDesc* d_desc = nullptr;
+  size_t desc_cap = 0;
+  int max_nf = 0;
+  DevBuf ws;  // scratch for host-buffer calls
+};
+
+namespace {
+
+int fail(bopx_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define HIPCHK(c, expr)                                                              \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    if (_e != hipSuccess)                                                           \
+      return fail((c), BOPX_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                  __FILE__, __LINE__);                                              \
+  } while (0)
+
+int set_dev(bopx_ctx* c) {
+  HIPCHK(c, hipSetDevice(c->device));
+  return BOPX_OK;
+}
+
+hipStream_t pick_stream(bopx_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+
+// Grow-only scratch; one allocation serves a whole host-buffer call.
+int ws_reserve(bopx_ctx* c, size_t bytes) {
+  if (c->ws.n >= bytes) return BOPX_OK;
+  if (c->ws.p) HIPCHK(c, hipFree(c->ws.p));
+  c->ws.p = nullptr;
+  c->ws.n = 0;
+  size_t want = std::max(bytes, (size_t)1 << 20);
+  if (hipMalloc(&c->ws.p, want) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(c, BOPX_E_OOM, "workspace allocation of %zu bytes failed", want);
+  }
+  c->ws.n = want;
+  return BOPX_OK;
+}
+
+// Bump allocator over the scratch (256-B aligned pieces).
+struct Carve {
+  char* base;
+  size_t off = 0;
+  template <class T>
+  T* take(size_t count) {
+    off = (off + 255) & ~(size_t)255;
+    T* p = (T*)(base + off);
+    off += count * sizeof(T);
+    return p;
+  }
+};
+static size_t carve_size(std::initializer_list<size_t> bytes) {
+  size_t s = 0;
+  for (size_t b : bytes) s += ((b + 255) & ~(size_t)255);
+  return s + 256;
+}
+
+int sync_desc(bopx_ctx* c) {
+  std::vector<ObjDesc> h(c->objs.size());
+  int max_nf = 0;
+  for (size_t i = 0; i < c->objs.size(); ++i) {
+    const Object& o = c->objs[i];
+    ObjDesc d{};
+    if (o.live) {
+      d.pts = o.d_pts;
+      d.vtx = o.d_vtx;
+      d.faces = o.d_faces;
+      d.mlet = o.d_mlet;
+      d.syms = o.d_syms;
+      d.nv = (int)o.nv;
+      d.nf = (int)o.nf;
+      d.nm = (int)o.nm;
+      d.ns = (int)o.ns;
+      max_nf = std::max(max_nf, (int)o.nf);
+    }
+    h[i] = d;
+  }
+  c->max_nf = max_nf;
+  if (h.size() > c->desc_cap) {
+    if (c->d_desc) HIPCHK(c, hipFree(c->d_desc));
+    size_t cap = std::max<size_t>(64, h.size() * 2);
+    HIPCHK(c, hipMalloc(&c->d_desc, cap * sizeof(ObjDesc)));
+    c->desc_cap = cap;
+  }
+  if (!h.empty())
+    HIPCHK(c, hipMemcpyAsync(c->d_desc, h.data(), h.size() * sizeof(ObjDesc),
+                             hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BOPX_OK;
+}
+
+void free_object(Object& o) {
+  if (o.d_pts) (void)hipFree(o.d_pts);
+  if (o.d_vtx) (void)hipFree(o.d_vtx);
+  if (o.d_faces) (void)hipFree(o.d_faces);
+  if (o.d_mlet) (void)hipFree(o.d_mlet);
+  if (o.d_syms) (void)hipFree(o.d_syms);
+  o = Object();
+}
+
+uint32_t spread10(uint32_t x) {
+  x &= 0x3FF;
+  x = (x | (x << 16)) & 0x30000FF;
+  x = (x | (x << 8)) & 0x300F00F;
+  x = (x | (x << 4)) & 0x30C30C3;
+  x = (x | (x << 2)) & 0x9249249;
+  return x;
+}
+
+template <class T>
+int upload(bopx_ctx* c, T** dst, const T* src, size_t count) {
+  if (count == 0) return BOPX_OK;
+  if (hipMalloc((void**)dst, count * sizeof(T)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(c, BOPX_E_OOM, "object allocation failed");
+  }
+  HIPCHK(c, hipMemcpy(*dst, src, count * sizeof(T), hipMemcpyHostToDevice));
+  return BOPX_OK;
+}
+
+int slot_checked(const bopx_ctx* c, int obj_id, int* slot) {
+  auto it = c->slot_of.find(obj_id);
+  if (it == c->slot_of.end()) return BOPX_E_NOT_FOUND;
+  *slot = it->second;
+  return BOPX_OK;
+}
+
+// Map obj_ids to slots on the host and validate the per-call requirements.
+int map_slots(bopx_ctx* c, int64_t n, const int32_t* obj_ids, std::vector<int32_t>& slots,
+              bool need_syms, bool need_faces) {
+  slots.resize((size_t)n);
+  for (int64_t i = 0; i < n; ++i) {
+    int s;
+    if (slot_checked(c, obj_ids[i], &s) != BOPX_OK)
+      return fail(c, BOPX_E_NOT_FOUND, "unknown obj_id %d", obj_ids[i]);
+    const Object& o = c->objs[s];
+    if (o.nv <= 0) return fail(c, BOPX_E_INVALID, "obj_id %d has no vertices", obj_ids[i]);
+    if (need_syms && o.ns <= 0)
+      return fail(c, BOPX_E_INVALID, "obj_id %d has no symmetry set", obj_ids[i]);
+    if (need_faces && o.nf <= 0)
+      return fail(c, BOPX_E_INVALID, "obj_id %d has no faces", obj_ids[i]);
+    if (need_faces && o.nm > bopx::kMaxMeshlets)
+      return fail(c, BOPX_E_UNSUPPORTED, "obj_id %d: %lld meshlets > %d", obj_ids[i],
+                  (long long)o.nm, bopx::kMaxMeshlets);
+    slots[i] = s;
+  }
+  return BOPX_OK;
+}
+
+int check_taus(bopx_ctx* c, const double* taus, int n_tau) {
+  if (n_tau < 1 || n_tau > BOPX_MAX_TAUS)
+    return fail(c, BOPX_E_INVALID, "n_tau = %d outside [1, %d]", n_tau, BOPX_MAX_TAUS);
+  if (!taus) return fail(c, BOPX_E_INVALID, "taus is NULL");
+  return BOPX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bopx_version(void) { return (0 << 16) | 1; }
+
+int bopx_device_count(int* n) {
+  int k = 0;
+  if (hipGetDeviceCount(&k) != hipSuccess) {
+    (void)hipGetLastError();
+    k = 0;
+  }
+  if (n) *n = k;
+  return BOPX_OK;
+}
+
+int bopx_create(int device, bopx_ctx** out) {
+  if (!out) return BOPX_E_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+    (void)hipGetLastError();
+    return BOPX_E_INVALID;
+  }
+  bopx_ctx* c = new bopx_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return BOPX_E_HIP;
+  }
+  *out = c;
+  return BOPX_OK;
+}
+
+void bopx_destroy(bopx_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (Object& o : c->objs) free_object(o);
+  if (c->d_desc) (void)hipFree(c->d_desc);
+  if (c->ws.p) (void)hipFree(c->ws.p);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* bopx_last_error(const bopx_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int bopx_synchronize(bopx_ctx* c) {
+  if (!c) return BOPX_E_INVALID;
+  if (int r = set_dev(c)) return r;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BOPX_OK;
+}
+
+void* bopx_stream(bopx_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int bopx_add_object(bopx_ctx* c, int obj_id, const double* pts, int64_t nv,
+                    const uint32_t* faces, int64_t nf) {
+  if (!c) return BOPX_E_INVALID;
+  if (nv <= 0 || !pts) return fail(c, BOPX_E_INVALID, "object %d: no vertices", obj_id);
+  if (nv > (1LL << 30) || nf > (1LL << 30))
+    return fail(c, BOPX_E_UNSUPPORTED, "object %d too large", obj_id);
+  if (nf > 0 && !faces) return fail(c, BOPX_E_INVALID, "object %d: faces is NULL", obj_id);
+  for (int64_t i = 0; i < 3 * nf; ++i)
+    if (faces[i] >= (uint64_t)nv)
+      return fail(c, BOPX_E_INVALID, "object %d: face index %u >= nv", obj_id, faces[i]);
+  if (int r = set_dev(c)) return r;
+  if (c->slot_of.count(obj_id)) bopx_remove_object(c, obj_id);
+
+  Object o;
+  o.obj_id = obj_id;
+  o.nv = nv;
+  o.nf = nf;
+  // float64 SoA points.
+  std::vector<double> soa(3 * (size_t)nv);
+  for (int64_t v = 0; v < nv; ++v)
+    for (int k = 0; k < 3; ++k) soa[k * (size_t)nv + v] = pts[3 * v + k];
+  // float32 raster vertices (GL vertex buffers are float32, renderer_vispy.py:373).
+  std::vector<float4> vtx((size_t)nv);
+  for (int64_t v = 0; v < nv; ++v)
+    vtx[v] = make_float4((float)pts[3 * v], (float)pts[3 * v + 1], (float)pts[3 * v + 2], 0.f);
+  // Meshlets: triangles sorted by the Morton code of their centroid, 64 per meshlet.
+  std::vector<uint32_t> fsorted;
+  std::vector<float> mlet;
+  if (nf > 0) {
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t v = 0; v < nv; ++v) {
+      const float p[3] = {vtx[v].x, vtx[v].y, vtx[v].z};
+      for (int k = 0; k < 3; ++k) lo[k] = std::min(lo[k], p[k]), hi[k] = std::max(hi[k], p[k]);
+    }
+    std::vector<std::pair<uint32_t, uint32_t>> key((size_t)nf);
+    for (int64_t f = 0; f < nf; ++f) {
+      uint32_t q[3];
+      for (int k = 0; k < 3; ++k) {
+        const float* p0 = &vtx[faces[3 * f]].x;
+        const float* p1 = &vtx[faces[3 * f + 1]].x;
+        const float* p2 = &vtx[faces[3 * f + 2]].x;
+        float cen = (p0[k] + p1[k] + p2[k]) / 3.0f;
+        float ext = hi[k] - lo[k];
+        float u = ext > 0 ? (cen - lo[k]) / ext : 0.f;
+        q[k] = (uint32_t)std::min(1023.0f, std::max(0.0f, u * 1023.0f));
+      }
+      key[f] = {spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2), (uint32_t)f};
+    }
+    std::stable_sort(key.begin(), key.end());
+    fsorted.resize(3 * (size_t)nf);
+    for (int64_t i = 0; i < nf; ++i)
+      for (int k = 0; k < 3; ++k) fsorted[3 * i + k] = faces[3 * (size_t)key[i].second + k];
+    o.nm = (nf + bopx::kMeshletTris - 1) / bopx::kMeshletTris;
+    mlet.assign(8 * (size_t)o.nm, 0.f);
+    for (int64_t m = 0; m < o.nm; ++m) {
+      float bl[3] = {INFINITY, INFINITY, INFINITY}, bh[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (int64_t f = m * bopx::kMeshletTris; f < std::min(nf, (m + 1) * bopx::kMeshletTris); ++f)
+        for (int j = 0; j < 3; ++j) {
+          const float* p = &vtx[fsorted[3 * f + j]].x;
+          for (int k = 0; k < 3; ++k) bl[k] = std::min(bl[k], p[k]), bh[k] = std::max(bh[k], p[k]);
+        }
+      for (int k = 0; k < 3; ++k) mlet[8 * m + k] = bl[k], mlet[8 * m + 4 + k] = bh[k];
+    }
+  }
+  int r;
+  if ((r = upload(c, &o.d_pts, soa.data(), soa.size())) ||
+      (r = upload(c, &o.d_vtx, vtx.data(), vtx.size())) ||
+      (r = upload(c, &o.d_faces, fsorted.data(), fsorted.size())) ||
+      (r = upload(c, &o.d_mlet, mlet.data(), mlet.size()))) {
+    free_object(o);
+    return r;
+  }
+  o.live = true;
+  int slot = -1;
+  for (size_t i = 0; i < c->objs.size(); ++i)
+    if (!c->objs[i].live) {
+      slot = (int)i;
+      break;
+    }
+  if (slot < 0) {
+    slot = (int)c->objs.size();
+    c->objs.push_back(Object());
+  }
+  c->objs[slot] = o;
+  c->slot_of[obj_id] = slot;
+  return sync_desc(c);
+}
+
+int bopx_remove_object(bopx_ctx* c, int obj_id) {
+  if (!c) return BOPX_E_INVALID;
+  int s;
+  if (slot_checked(c, obj_id, &s) != BOPX_OK)
+    return fail(c, BOPX_E_NOT_FOUND, "unknown obj_id %d", obj_id);
+  if (int r = set_dev(c)) return r;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  free_object(c->objs[s]);
+  c->slot_of.erase(obj_id);
+  return sync_desc(c);
+}
+
+int bopx_set_symmetries(bopx_ctx* c, int obj_id, const double* syms, int64_t ns) {
+  if (!c) return BOPX_E_INVALID;
+  int s;
+  if (slot_checked(c, obj_id, &s) != BOPX_OK)
+    return fail(c, BOPX_E_NOT_FOUND, "unknown obj_id %d", obj_id);
+  if (ns < 1 || !syms) return fail(c, BOPX_E_INVALID, "empty symmetry set");
+  if (int r = set_dev(c)) return r;
+  Object& o = c->objs[s];
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (o.d_syms) HIPCHK(c, hipFree(o.d_syms));
+  o.d_syms = nullptr;
+  o.ns = 0;
+  if (int r = upload(c, &o.d_syms, syms, 12 * (size_t)ns)) return r;
+  o.ns = ns;
+  return sync_desc(c);
+}
+
+int bopx_object_slot(const bopx_ctx* c, int obj_id, int* slot) {
+  if (!c || !slot) return BOPX_E_INVALID;
+  return slot_checked(c, obj_id, slot);
+}
+
+// ---------------------------------------------------------------- point errors
+static int point_batch(bopx_ctx* c, int kind, int64_t n, const int32_t* obj_ids,
+                       const double* pe, const double* pg, const double* K, double* out) {
+  // kind: 0 mssd, 1 mspd, 2 add, 3 adi, 4 proj
+  if (!c) return BOPX_E_INVALID;
+  if (n < 0) return fail(c, BOPX_E_INVALID, "n < 0");
+  if (n == 0) return BOPX_OK;
+  if (!obj_ids || !pe || !pg || !out) return fail(c, BOPX_E_INVALID, "NULL buffer");
+  const bool needK = kind == 1 || kind == 4;
+  if (needK && !K) return fail(c, BOPX_E_INVALID, "K is NULL");
+  if (int r = set_dev(c)) return r;
+  std::vector<int32_t> slots;
+  if (int r = map_slots(c, n, obj_ids, slots, kind <= 1, false)) return r;
+  const size_t bytes = carve_size({4 * (size_t)n, 96 * (size_t)n, 96 * (size_t)n,
+                                   needK ? 72 * (size_t)n : 0, 8 * (size_t)n});
+  if (int r = ws_reserve(c, bytes)) return r;
+  Carve cv{(char*)c->ws.p};
+  int32_t* d_s = cv.take<int32_t>(n);
+  double* d_pe = cv.take<double>(12 * n);
+  double* d_pg = cv.take<double>(12 * n);
+  double* d_K = needK ? cv.take<double>(9 * n) : nullptr;
+  double* d_out = cv.take<double>(n);
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_s, slots.data(), 4 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_pe, pe, 96 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_pg, pg, 96 * n, hipMemcpyHostToDevice, s));
+  if (needK) HIPCHK(c, hipMemcpyAsync(d_K, K, 72 * n, hipMemcpyHostToDevice, s));
+  hipError_t e;
+  if (kind <= 1)
+    e = bopx::launch_sym_error(kind, c->d_desc, n, d_s, d_pe, d_pg, d_K, d_out, s);
+  else if (kind == 3)
+    e = bopx::launch_adi(c->d_desc, n, d_s, d_pe, d_pg, d_out, s);
+  else
+    e = bopx::launch_mean_error(kind == 2 ? 0 : 1, c->d_desc, n, d_s, d_pe, d_pg, d_K, d_out, s);
+  HIPCHK(c, e);
+  HIPCHK(c, hipMemcpyAsync(out, d_out, 8 * n, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return BOPX_OK;
+}
+
+int bopx_mssd_batch(bopx_ctx* c, int64_t n, const int32_t* ids, const double* pe,
+                    const double* pg, double* out) {
+  return point_batch(c, 0, n, ids, pe, pg, nullptr, out);
+}
+int bopx_mspd_batch(bopx_ctx* c, int64_t n, const int32_t* ids, const double* pe,
+                    const double* pg, const double* K, double* out) {
+  return point_batch(c, 1, n, ids, pe, pg, K, out);
+}
+int bopx_add_batch(bopx_ctx* c, int64_t n, const int32_t* ids, const double* pe,
+                   const double* pg, double* out) {
+  return point_batch(c, 2, n, ids, pe, pg, nullptr, out);
+}
+int bopx_adi_batch(bopx_ctx* c, int64_t n, const int32_t* ids, const double* pe,
+                   const double* pg, double* out) {
+  return point_batch(c, 3, n, ids, pe, pg, nullptr, out);
+}
+int bopx_proj_batch(bopx_ctx* c, int64_t n, const int32_t* ids, const double* pe,
+                    const double* pg, const double* K, double* out) {
+  return point_batch(c, 4, n, ids, pe, pg, K, out);
+}
+
+int bopx_mssd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
+                        const double* pg, double* out, void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (int r = set_dev(c)) return r;
+  HIPCHK(c, bopx::launch_sym_error(0, c->d_desc, n, slots, pe, pg, nullptr, out,
+                                   pick_stream(c, stream)));
+  return BOPX_OK;
+}
+int bopx_mspd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
+                        const double* pg, const double* K, double* out, void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (int r = set_dev(c)) return r;
+  HIPCHK(c, bopx::launch_sym_error(1, c->d_desc, n, slots, pe, pg, K, out, pick_stream(c, stream)));
+  return BOPX_OK;
+}
+int bopx_add_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
+                       const double* pg, double* out, void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (int r = set_dev(c)) return r;
+  HIPCHK(c, bopx::launch_mean_error(0, c->d_desc, n, slots, pe, pg, nullptr, out,
+                                    pick_stream(c, stream)));
+  return BOPX_OK;
+}
+int bopx_adi_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
+                       const double* pg, double* out, void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (int r = set_dev(c)) return r;
+  HIPCHK(c, bopx::launch_adi(c->d_desc, n, slots, pe, pg, out, pick_stream(c, stream)));
+  return BOPX_OK;
+}
+
+// ------------------------------------------------------------------------ VSD
+static int fill_vsd_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height, double delta,
+                         int flags, const double* taus, int n_tau, int normalized,
+                         int cost_type) {
+  if (width <= 0 || height <= 0 || width > 32767 || height > 32767)
+    return fail(c, BOPX_E_INVALID, "bad image size %dx%d", width, height);
+  if (cost_type != BOPX_COST_STEP && cost_type != BOPX_COST_TLINEAR)
+    return fail(c, BOPX_E_INVALID, "Unknown pixel matching cost.");
+  if (int r = check_taus(c, taus, n_tau)) return r;
+  a.width = width;
+  a.height = height;
+  a.delta32 = (float)delta;
+  a.delta64 = delta;
+  a.delta_f64 = (flags & BOPX_DELTA_F64) ? 1 : 0;
+  a.n_tau = n_tau;
+  a.normalized = normalized ? 1 : 0;
+  for (int k = 0; k < bopx::kMaxTaus; ++k) a.taus[k] = k < n_tau ? taus[k] : 1.0;
+  return BOPX_OK;
+}
+
+int bopx_vsd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
+                       const double* pg, const int32_t* frame_idx, const float* frames,
+                       int width, int height, const double* cam, double delta, int flags,
+                       const double* taus, int n_tau, int normalized, const double* diameters,
+                       int cost_type, double* out, void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (int r = set_dev(c)) return r;
+  bopx::VsdArgs a{};
+  if (int r = fill_vsd_args(c, a, width, height, delta, flags, taus, n_tau, normalized,
+                            cost_type))
+    return r;
+  a.objs = c->d_desc;
+  a.slots = slots;
+  a.pose_est = pe;
+  a.pose_gt = pg;
+  a.frame_idx = frame_idx;
+  a.frames = frames;
+  a.cam = cam;
+  a.diameters = diameters;
+  a.out = out;
+  a.n = n;
+  HIPCHK(c, bopx::launch_vsd(a, cost_type, pick_stream(c, stream)));
+  return BOPX_OK;
+}
+
+int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double* pe,
+                   const double* pg, const int32_t* frame_idx, const float* frames,
+                   int64_t n_frames, int width, int height, const double* cam, double delta,
+                   int flags, const double* taus, int n_tau, int normalized,
+                   const double* diameters, int cost_type, double* out) {
+  if (!c) return BOPX_E_INVALID;
+  if (n < 0 || n_frames < 0) return fail(c, BOPX_E_INVALID, "negative size");
+  if (n == 0) return BOPX_OK;
+  if (!obj_ids || !pe || !pg || !frame_idx || !frames || !cam || !diameters || !out)
+    return fail(c, BOPX_E_INVALID, "NULL buffer");
+  for (int64_t i = 0; i < n; ++i)
+    if (frame_idx[i] < 0 || frame_idx[i] >= n_frames)
+      return fail(c, BOPX_E_INVALID, "frame_idx[%lld] = %d out of range", (long long)i,
+                  frame_idx[i]);
+  if (int r = set_dev(c)) return r;
+  bopx::VsdArgs a{};
+  if (int r = fill_vsd_args(c, a, width, height, delta, flags, taus, n_tau, normalized,
+                            cost_type))
+    return r;
+  std::vector<int32_t> slots;
+  if (int r = map_slots(c, n, obj_ids, slots, false, true)) return r;
+  const size_t fbytes = (size_t)n_frames * width * height * sizeof(float);
+  const size_t bytes = carve_size({4 * (size_t)n, 96 * (size_t)n, 96 * (size_t)n,
+                                   4 * (size_t)n, fbytes, 32 * (size_t)n_frames,
+                                   8 * (size_t)n, 8 * (size_t)n * n_tau});
+  if (int r = ws_reserve(c, bytes)) return r;
+  Carve cv{(char*)c->ws.p};
+  int32_t* d_s = cv.take<int32_t>(n);
+  double* d_pe = cv.take<double>(12 * n);
+  double* d_pg = cv.take<double>(12 * n);
+  int32_t* d_fi = cv.take<int32_t>(n);
+  float* d_fr = cv.take<float>((size_t)n_frames * width * height);
+  double* d_cam = cv.take<double>(4 * n_frames);
+  double* d_dia = cv.take<double>(n);
+  double* d_out = cv.take<double>((size_t)n * n_tau);
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_s, slots.data(), 4 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_pe, pe, 96 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_pg, pg, 96 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_fi, frame_idx, 4 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_fr, frames, fbytes, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_cam, cam, 32 * n_frames, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_dia, diameters, 8 * n, hipMemcpyHostToDevice, s));
+  a.objs = c->d_desc;
+  a.slots = d_s;
+  a.pose_est = d_pe;
+  a.pose_gt = d_pg;
+  a.frame_idx = d_fi;
+  a.frames = d_fr;
+  a.cam = d_cam;
+  a.diameters = d_dia;
+  a.out = d_out;
+  a.n = n;
+  HIPCHK(c, bopx::launch_vsd(a, cost_type, s));
+  HIPCHK(c, hipMemcpyAsync(out, d_out, 8 * (size_t)n * n_tau, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return BOPX_OK;
+}
+
+int bopx_vsd_from_depths(bopx_ctx* c, int width, int height, const float* depth_test,
+                         const float* depth_est, const float* depth_gt, double fx, double fy,
+                         double cx, double cy, double delta, int flags, const double* taus,
+                         int n_tau, int normalized, double diameter, int cost_type,
+                         double* out) {
+  if (!c) return BOPX_E_INVALID;
+  if (width <= 0 || height <= 0) return fail(c, BOPX_E_INVALID, "bad image size");
+  if (!depth_test || !depth_est || !depth_gt || !out)
+    return fail(c, BOPX_E_INVALID, "NULL buffer");
+  if (int r = check_taus(c, taus, n_tau)) return r;
+  if (int r = set_dev(c)) return r;
+  const size_t npx = (size_t)width * height;
+  const int nb = bopx::vsd_depths_blocks(width, height);
+  const int stride = 2 + 2 * bopx::kMaxTaus;
+  if (int r = ws_reserve(c, carve_size({4 * npx, 4 * npx, 4 * npx, 8 * (size_t)nb * stride})))
+    return r;
+  Carve cv{(char*)c->ws.p};
+  float* d_t = cv.take<float>(npx);
+  float* d_e = cv.take<float>(npx);
+  float* d_g = cv.take<float>(npx);
+  double* d_p = cv.take<double>((size_t)nb * stride);
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_t, depth_test, 4 * npx, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_e, depth_est, 4 * npx, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_g, depth_gt, 4 * npx, hipMemcpyHostToDevice, s));
+  HIPCHK(c, bopx::launch_vsd_depths(width, height, d_t, d_e, d_g, fx, fy, cx, cy, (float)delta,
+                                    (flags & BOPX_DELTA_F64) ? 1 : 0, delta, taus, n_tau,
+                                    normalized ? 1 : 0, diameter, d_p, nb, s));
+  std::vector<double> part((size_t)nb * stride);
+  HIPCHK(c, hipMemcpyAsync(part.data(), d_p, 8 * part.size(), hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  std::vector<double> tot(stride, 0.0);
+  for (int b = 0; b < nb; ++b)
+    for (int k = 0; k < stride; ++k) tot[k] += part[(size_t)b * stride + k];
+  const double un = tot[0], comp = tot[0] - tot[1];
+  if (un == 0.0) {
+    for (int k = 0; k < n_tau; ++k) out[k] = 1.0;
+    return BOPX_OK;
+  }
+  // The reference raises on an unknown cost type only when the union is non-empty
+  // (pose_error.py:75-88).
+  if (cost_type != BOPX_COST_STEP && cost_type != BOPX_COST_TLINEAR)
+    return fail(c, BOPX_E_INVALID, "Unknown pixel matching cost.");
+  for (int k = 0; k < n_tau; ++k) {
+    if (cost_type == BOPX_COST_STEP)
+      out[k] = (double)((int64_t)tot[2 + k] + (int64_t)comp) / un;
+    else
+      out[k] = (tot[2 + bopx::kMaxTaus + k] + comp) / un;
+  }
+  return BOPX_OK;
+}
+
+// -------------------------------------------------------------------- renderer
+int bopx_depth_clear_dev(bopx_ctx* c, float* frames, int64_t n_pixels, void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (int r = set_dev(c)) return r;
+  HIPCHK(c, bopx::launch_depth_fill(frames, n_pixels, 0, pick_stream(c, stream)));
+  return BOPX_OK;
+}
+
+int bopx_depth_finish_dev(bopx_ctx* c, float* frames, int64_t n_pixels, void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (int r = set_dev(c)) return r;
+  HIPCHK(c, bopx::launch_depth_fill(frames, n_pixels, 1, pick_stream(c, stream)));
+  return BOPX_OK;
+}
+
+int bopx_render_depth_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pose,
+                                const int32_t* frame_idx, const double* cam, float* frames,
+                                int width, int height, void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (width <= 0 || height <= 0) return fail(c, BOPX_E_INVALID, "bad image size");
+  if (int r = set_dev(c)) return r;
+  if (n <= 0 || c->max_nf <= 0) return BOPX_OK;
+  HIPCHK(c, bopx::launch_render_batch(c->d_desc, c->max_nf, n, slots, pose, frame_idx, cam,
+                                      frames, width, height, pick_stream(c, stream)));
+  return BOPX_OK;
+}
+
+int bopx_render_depth(bopx_ctx* c, int obj_id, const double* R, const double* t, double fx,
+                      double fy, double cx, double cy, int width, int height, float* out) {
+  if (!c) return BOPX_E_INVALID;
+  if (!R || !t || !out) return fail(c, BOPX_E_INVALID, "NULL buffer");
+  if (width <= 0 || height <= 0) return fail(c, BOPX_E_INVALID, "bad image size");
+  if (int r = set_dev(c)) return r;
+  std::vector<int32_t> slots;
+  int32_t id = obj_id;
+  if (int r = map_slots(c, 1, &id, slots, false, true)) return r;
+  const size_t npx = (size_t)width * height;
+  if (int r = ws_reserve(c, carve_size({4 * npx, 4, 96, 4, 32}))) return r;
+  Carve cv{(char*)c->ws.p};
+  float* d_f = cv.take<float>(npx);
+  int32_t* d_s = cv.take<int32_t>(1);
+  double* d_pose = cv.take<double>(12);
+  int32_t* d_fi = cv.take<int32_t>(1);
+  double* d_cam = cv.take<double>(4);
+  double pose[12], cam[4] = {fx, fy, cx, cy};
+  for (int i = 0; i < 9; ++i) pose[i] = R[i];
+  for (int i = 0; i < 3; ++i) pose[9 + i] = t[i];
+  const int32_t zero = 0;
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_s, slots.data(), 4, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_pose, pose, 96, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_fi, &zero, 4, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_cam, cam, 32, hipMemcpyHostToDevice, s));
+  HIPCHK(c, bopx::launch_depth_fill(d_f, (int64_t)npx, 0, s));
+  HIPCHK(c, bopx::launch_render_batch(c->d_desc, (int)c->objs[slots[0]].nf, 1, d_s, d_pose, d_fi,
+                                      d_cam, d_f, width, height, s));
+  HIPCHK(c, bopx::launch_depth_fill(d_f, (int64_t)npx, 1, s));
+  HIPCHK(c, hipMemcpyAsync(out, d_f, 4 * npx, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return BOPX_OK;
+}
+
+// ------------------------------------------------------- geometry/visibility
+int bopx_dist_im(bopx_ctx* c, int width, int height, const float* depth, double fx, double fy,
+                 double cx, double cy, double* out) {
+  if (!c) return BOPX_E_INVALID;
+  if (width <= 0 || height <= 0 || !depth || !out)
+    return fail(c, BOPX_E_INVALID, "bad arguments");
+  if (int r = set_dev(c)) return r;
+  const size_t npx = (size_t)width * height;
+  if (int r = ws_reserve(c, carve_size({4 * npx, 8 * npx}))) return r;
+  Carve cv{(char*)c->ws.p};
+  float* d_in = cv.take<float>(npx);
+  double* d_out = cv.take<double>(npx);
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_in, depth, 4 * npx, hipMemcpyHostToDevice, s));
+  HIPCHK(c, bopx::launch_dist_im(width, height, d_in, fx, fy, cx, cy, d_out, s));
+  HIPCHK(c, hipMemcpyAsync(out, d_out, 8 * npx, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return BOPX_OK;
+}
+
+int bopx_visib_mask(bopx_ctx* c, int64_t n, const double* d_test, const double* d_model,
+                    const uint8_t* visib_gt, double delta, int flags, int visib_mode,
+                    uint8_t* out) {
+  if (!c) return BOPX_E_INVALID;
+  if (visib_mode != BOPX_VISIB_BOP18 && visib_mode != BOPX_VISIB_BOP19)
+    return fail(c, BOPX_E_INVALID, "Unknown visibility mode.");
+  if (n < 0 || (n > 0 && (!d_test || !d_model || !out)))
+    return fail(c, BOPX_E_INVALID, "bad arguments");
+  if (n == 0) return BOPX_OK;
+  if (int r = set_dev(c)) return r;
+  if (int r = ws_reserve(c, carve_size({8 * (size_t)n, 8 * (size_t)n, (size_t)n, (size_t)n})))
+    return r;
+  Carve cv{(char*)c->ws.p};
+  double* d_t = cv.take<double>(n);
+  double* d_m = cv.take<double>(n);
+  uint8_t* d_vg = cv.take<uint8_t>(n);
+  uint8_t* d_o = cv.take<uint8_t>(n);
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_t, d_test, 8 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_m, d_model, 8 * n, hipMemcpyHostToDevice, s));
+  if (visib_gt) HIPCHK(c, hipMemcpyAsync(d_vg, visib_gt, n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, bopx::launch_visib(n, d_t, d_m, visib_gt ? d_vg : nullptr, (float)delta,
+                               (flags & BOPX_DELTA_F64) ? 1 : 0, delta, visib_mode, d_o, s));
+  HIPCHK(c, hipMemcpyAsync(out, d_o, n, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return BOPX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,129 @@
+"""Host I/O needed around the pose-error path (subset of bop_toolkit_lib/inout.py).
+
+load_ply reads the vertices and triangles of a BOP model (inout.py:401-583
+parses them with a per-vertex Python loop; here the binary body is decoded
+with one structured-dtype read). Other per-vertex attributes are skipped.
+"""
+import json
+
+import numpy as np
+
+_PLY_TYPES = {
+    "char": "i1", "int8": "i1", "uchar": "u1", "uint8": "u1",
+    "short": "i2", "int16": "i2", "ushort": "u2", "uint16": "u2",
+    "int": "i4", "int32": "i4", "uint": "u4", "uint32": "u4",
+    "float": "f4", "float32": "f4", "double": "f8", "float64": "f8",
+}
+
+
+def _read_header(f):
+  elements, fmt = [], None
+  line = f.readline().strip()
+  if line != b"ply":
+    raise ValueError("not a PLY file")
+  while True:
+    line = f.readline()
+    if not line:
+      raise ValueError("truncated PLY header")
+    tok = line.decode("ascii", "replace").split()
+    if not tok:
+      continue
+    if tok[0] == "format":
+      fmt = tok[1]
+    elif tok[0] == "element":
+      elements.append({"name": tok[1], "count": int(tok[2]), "props": []})
+    elif tok[0] == "property":
+      if tok[1] == "list":
+        elements[-1]["props"].append((tok[4], "list", _PLY_TYPES[tok[2]], _PLY_TYPES[tok[3]]))
+      else:
+        elements[-1]["props"].append((tok[2], "scalar", _PLY_TYPES[tok[1]], None))
+    elif tok[0] == "end_header":
+      return fmt, elements
+
+
+def load_ply(path):
+  """Returns {'pts': V x 3 float64, 'faces': F x 3 int64}."""
+  with open(path, "rb") as f:
+    fmt, elements = _read_header(f)
+    body = f.read()
+  if fmt == "ascii":
+    return _load_ascii(body.decode("ascii").split("\n"), elements)
+  if fmt != "binary_little_endian":
+    raise ValueError("unsupported PLY format %r" % fmt)
+  off, pts, faces = 0, None, None
+  for el in elements:
+    n = el["count"]
+    if all(p[1] == "scalar" for p in el["props"]):
+      dt = np.dtype([(p[0], "<" + p[2]) for p in el["props"]])
+      arr = np.frombuffer(body, dt, count=n, offset=off)
+      off += n * dt.itemsize
+      if el["name"] == "vertex":
+        pts = np.stack([arr["x"], arr["y"], arr["z"]], 1).astype(np.float64)
+    elif el["name"] == "face" and len(el["props"]) == 1:
+      _, _, ct, it = el["props"][0]
+      cdt, idt = np.dtype("<" + ct), np.dtype("<" + it)
+      first = int(np.frombuffer(body, cdt, count=1, offset=off)[0]) if n else 3
+      dt = np.dtype([("n", cdt), ("i", idt, (first,))])
+      arr = np.frombuffer(body, dt, count=n, offset=off)
+      if n and not np.all(arr["n"] == first):
+        raise ValueError("mixed polygon sizes are not supported")
+      if first != 3 and n:
+        raise ValueError("only triangle meshes are supported")
+      faces = arr["i"].astype(np.int64)
+      off += n * dt.itemsize
+    else:
+      raise ValueError("unsupported PLY element layout %r" % el["name"])
+  return {"pts": pts, "faces": faces if faces is not None else np.zeros((0, 3), np.int64)}
+
+
+def _load_ascii(lines, elements):
+  pos, pts, faces = 0, None, None
+  for el in elements:
+    rows = [l.split() for l in lines[pos:pos + el["count"]]]
+    pos += el["count"]
+    if el["name"] == "vertex":
+      names = [p[0] for p in el["props"]]
+      a = np.array(rows, np.float64)
+      pts = a[:, [names.index("x"), names.index("y"), names.index("z")]]
+    elif el["name"] == "face":
+      faces = np.array([[int(v) for v in r[1:4]] for r in rows], np.int64).reshape(-1, 3)
+  return {"pts": pts, "faces": faces if faces is not None else np.zeros((0, 3), np.int64)}
+
+
+def save_ply(path, pts, faces):
+  """Minimal binary PLY writer (vertices as float32, triangles as int32)."""
+  pts = np.asarray(pts, np.float32)
+  faces = np.asarray(faces, np.int32)
+  head = ("ply\nformat binary_little_endian 1.0\nelement vertex %d\n"
+          "property float x\nproperty float y\nproperty float z\n"
+          "element face %d\nproperty list uchar int vertex_indices\nend_header\n"
+          % (len(pts), len(faces)))
+  fdt = np.dtype([("n", "u1"), ("i", "<i4", (3,))])
+  farr = np.empty(len(faces), fdt)
+  farr["n"] = 3
+  farr["i"] = faces
+  with open(path, "wb") as f:
+    f.write(head.encode("ascii"))
+    f.write(pts.astype("<f4").tobytes())
+    f.write(farr.tobytes())
+
+
+def save_json(path, content):
+  """JSON with one top-level element per line and sorted keys
+  (inout.py:85-113), the format of the errors_*.json hand-off files."""
+  with open(path, "w") as f:
+    if isinstance(content, dict):
+      items = sorted(content.items(), key=lambda x: x[0])
+      f.write("{\n")
+      for i, (k, v) in enumerate(items):
+        f.write('  "{}": {}'.format(k, json.dumps(v, sort_keys=True)))
+        f.write(",\n" if i != len(items) - 1 else "\n")
+      f.write("}")
+    elif isinstance(content, list):
+      f.write("[\n")
+      for i, e in enumerate(content):
+        f.write("  {}".format(json.dumps(e, sort_keys=True)))
+        f.write(",\n" if i != len(content) - 1 else "\n")
+      f.write("]")
+    else:
+      json.dump(content, f, sort_keys=True)

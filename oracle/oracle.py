@@ -1,0 +1,206 @@
+"""ctypes front-end of the CPU oracle (oracle/bopx_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package (bop_toolkit_amd).
+
+Poses are passed as 12-vectors [R row-major | t]; symmetry sets as S x 12.
+Each function names the reference lines it restates (see bopx_oracle.c).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+_d = ctypes.POINTER(ctypes.c_double)
+_f = ctypes.POINTER(ctypes.c_float)
+_u8 = ctypes.POINTER(ctypes.c_uint8)
+_u32 = ctypes.POINTER(ctypes.c_uint32)
+_i32 = ctypes.POINTER(ctypes.c_int32)
+_i64 = ctypes.POINTER(ctypes.c_int64)
+_I64 = ctypes.c_int64
+_I = ctypes.c_int
+_D = ctypes.c_double
+
+
+def build():
+  """Compile liboracle.so with the committed Makefile (gcc)."""
+  subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+  global _lib
+  if _lib is None:
+    if not os.path.exists(_LIB_PATH):
+      build()
+    L = ctypes.CDLL(_LIB_PATH)
+    L.oracle_mssd.restype = _D
+    L.oracle_mssd.argtypes = [_d, _I64, _d, _I64, _d, _d]
+    L.oracle_mspd.restype = _D
+    L.oracle_mspd.argtypes = [_d, _I64, _d, _I64, _d, _d, _d]
+    L.oracle_add.restype = _D
+    L.oracle_add.argtypes = [_d, _I64, _d, _d]
+    L.oracle_adi.restype = _D
+    L.oracle_adi.argtypes = [_d, _I64, _d, _d]
+    L.oracle_proj.restype = _D
+    L.oracle_proj.argtypes = [_d, _I64, _d, _d, _d]
+    L.oracle_dist_im.restype = None
+    L.oracle_dist_im.argtypes = [_f, _I, _I, _D, _D, _D, _D, _d]
+    L.oracle_visib_mask.restype = None
+    L.oracle_visib_mask.argtypes = [_I64, _d, _d, _u8, _D, _I, _I, _u8]
+    L.oracle_vsd_depths.restype = _I
+    L.oracle_vsd_depths.argtypes = [_I, _I, _f, _f, _f, _D, _D, _D, _D, _D, _I, _d, _I, _I,
+                                    _D, _I, _d]
+    L.oracle_render_depth.restype = None
+    L.oracle_render_depth.argtypes = [_d, _I64, _u32, _I64, _d, _d, _D, _D, _D, _D, _I, _I,
+                                      _f]
+    L.oracle_coverage.restype = None
+    L.oracle_coverage.argtypes = [_d, _I64, _u32, _I64, _d, _d, _D, _D, _D, _D, _I, _I, _i32]
+    L.oracle_bop19_batch.restype = None
+    L.oracle_bop19_batch.argtypes = [_I64, _i32, _i64, _i64, _d, _i64, _i64, _u32, _i64, _i64,
+                                     _d, _d, _d, _i32, _f, _I, _I, _d, _D, _d, _I, _d, _d, _d,
+                                     _d]
+    _lib = L
+  return _lib
+
+
+def _p(a, ct):
+  return a.ctypes.data_as(ct)
+
+
+def _f64(a):
+  return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def pose12(R, t):
+  return np.concatenate([np.asarray(R, np.float64).reshape(9),
+                         np.asarray(t, np.float64).reshape(3)])
+
+
+def syms12(syms):
+  """List of {'R','t'} dicts (misc.get_symmetry_transformations) -> S x 12."""
+  return np.stack([pose12(s["R"], s["t"]) for s in syms]) if len(syms) else np.zeros((0, 12))
+
+
+def mssd(pts, syms, pe, pg):
+  pts, syms, pe, pg = _f64(pts), _f64(syms), _f64(pe), _f64(pg)
+  return lib().oracle_mssd(_p(pts, _d), len(pts), _p(syms, _d), len(syms), _p(pe, _d),
+                           _p(pg, _d))
+
+
+def mspd(pts, syms, pe, pg, K):
+  pts, syms, pe, pg, K = _f64(pts), _f64(syms), _f64(pe), _f64(pg), _f64(K)
+  return lib().oracle_mspd(_p(pts, _d), len(pts), _p(syms, _d), len(syms), _p(pe, _d),
+                           _p(pg, _d), _p(K, _d))
+
+
+def add(pts, pe, pg):
+  pts, pe, pg = _f64(pts), _f64(pe), _f64(pg)
+  return lib().oracle_add(_p(pts, _d), len(pts), _p(pe, _d), _p(pg, _d))
+
+
+def adi(pts, pe, pg):
+  pts, pe, pg = _f64(pts), _f64(pe), _f64(pg)
+  return lib().oracle_adi(_p(pts, _d), len(pts), _p(pe, _d), _p(pg, _d))
+
+
+def proj(pts, pe, pg, K):
+  pts, pe, pg, K = _f64(pts), _f64(pe), _f64(pg), _f64(K)
+  return lib().oracle_proj(_p(pts, _d), len(pts), _p(pe, _d), _p(pg, _d), _p(K, _d))
+
+
+def dist_im(depth, fx, fy, cx, cy):
+  depth = np.ascontiguousarray(depth, dtype=np.float32)
+  H, W = depth.shape
+  out = np.empty((H, W), np.float64)
+  lib().oracle_dist_im(_p(depth, _f), W, H, fx, fy, cx, cy, _p(out, _d))
+  return out
+
+
+def visib_mask(d_test, d_model, delta, visib_gt=None, delta_f64=False, mode="bop19"):
+  d_test, d_model = _f64(d_test), _f64(d_model)
+  out = np.empty(d_test.shape, np.uint8)
+  vg = None
+  if visib_gt is not None:
+    vg = np.ascontiguousarray(visib_gt, dtype=np.uint8)
+  lib().oracle_visib_mask(d_test.size, _p(d_test, _d), _p(d_model, _d),
+                          _p(vg, _u8) if vg is not None else None, float(delta),
+                          int(delta_f64), 1 if mode == "bop19" else 0, _p(out, _u8))
+  return out.astype(bool)
+
+
+def vsd_depths(depth_test, depth_est, depth_gt, fx, fy, cx, cy, delta, taus, normalized,
+               diameter, cost_type="step", delta_f64=False):
+  dt = np.ascontiguousarray(depth_test, np.float32)
+  de = np.ascontiguousarray(depth_est, np.float32)
+  dg = np.ascontiguousarray(depth_gt, np.float32)
+  H, W = dt.shape
+  taus = _f64(taus)
+  out = np.empty(len(taus), np.float64)
+  ct = {"step": 0, "tlinear": 1}.get(cost_type, 99)
+  rc = lib().oracle_vsd_depths(W, H, _p(dt, _f), _p(de, _f), _p(dg, _f), fx, fy, cx, cy,
+                               float(delta), int(delta_f64), _p(taus, _d), len(taus),
+                               int(bool(normalized)), float(diameter), ct, _p(out, _d))
+  if rc != 0:
+    raise ValueError("Unknown pixel matching cost.")
+  return list(out)
+
+
+def render_depth(pts, faces, R, t, fx, fy, cx, cy, W, H):
+  pts = _f64(pts)
+  faces = np.ascontiguousarray(faces, np.uint32)
+  R, t = _f64(R).reshape(9), _f64(t).reshape(3)
+  out = np.empty((H, W), np.float32)
+  lib().oracle_render_depth(_p(pts, _d), len(pts), _p(faces, _u32), len(faces), _p(R, _d),
+                            _p(t, _d), fx, fy, cx, cy, W, H, _p(out, _f))
+  return out
+
+
+def coverage(pts, faces, R, t, fx, fy, cx, cy, W, H):
+  pts = _f64(pts)
+  faces = np.ascontiguousarray(faces, np.uint32)
+  R, t = _f64(R).reshape(9), _f64(t).reshape(3)
+  out = np.empty((H, W), np.int32)
+  lib().oracle_coverage(_p(pts, _d), len(pts), _p(faces, _u32), len(faces), _p(R, _d),
+                        _p(t, _d), fx, fy, cx, cy, W, H, _p(out, _i32))
+  return out
+
+
+def bop19_batch(objects, obj, pose_est, pose_gt, frame_idx, frames, cam, delta, taus,
+                diameters):
+  """CPU baseline: VSD + MSSD + MSPD per tuple. objects: list of dicts with
+  'pts' (V x 3), 'faces' (F x 3), 'syms' (S x 12). Returns (vsd n x n_tau,
+  mssd n, mspd n)."""
+  nv = np.array([len(o["pts"]) for o in objects], np.int64)
+  nf = np.array([len(o["faces"]) for o in objects], np.int64)
+  ns = np.array([len(o["syms"]) for o in objects], np.int64)
+  pts_off = np.concatenate([[0], np.cumsum(nv)[:-1]]).astype(np.int64)
+  face_off = np.concatenate([[0], np.cumsum(nf)[:-1]]).astype(np.int64)
+  sym_off = np.concatenate([[0], np.cumsum(ns)[:-1]]).astype(np.int64)
+  pts_all = _f64(np.concatenate([o["pts"] for o in objects]))
+  faces_all = np.ascontiguousarray(np.concatenate([o["faces"] for o in objects]), np.uint32)
+  syms_all = _f64(np.concatenate([o["syms"] for o in objects]))
+  obj = np.ascontiguousarray(obj, np.int32)
+  pe, pg = _f64(pose_est), _f64(pose_gt)
+  fi = np.ascontiguousarray(frame_idx, np.int32)
+  fr = np.ascontiguousarray(frames, np.float32)
+  cam = _f64(cam)
+  taus = _f64(taus)
+  dia = _f64(diameters)
+  n = len(obj)
+  H, W = fr.shape[1], fr.shape[2]
+  out_vsd = np.empty((n, len(taus)), np.float64)
+  out_mssd = np.empty(n, np.float64)
+  out_mspd = np.empty(n, np.float64)
+  lib().oracle_bop19_batch(n, _p(obj, _i32), _p(pts_off, _i64), _p(nv, _i64),
+                           _p(pts_all, _d), _p(face_off, _i64), _p(nf, _i64),
+                           _p(faces_all, _u32), _p(sym_off, _i64), _p(ns, _i64),
+                           _p(syms_all, _d), _p(pe, _d), _p(pg, _d), _p(fi, _i32),
+                           _p(fr, _f), W, H, _p(cam, _d), float(delta), _p(taus, _d),
+                           len(taus), _p(dia, _d), _p(out_vsd, _d), _p(out_mssd, _d),
+                           _p(out_mspd, _d))
+  return out_vsd, out_mssd, out_mspd

@@ -1,0 +1,51 @@
+"""The C-ABI library loads on a CPU-only host and exports exactly the entry
+points include/bopx.h declares (no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "bopx.h")
+LIB = os.path.join(REPO, "bop_toolkit_amd", "lib", "libbopx.so")
+
+
+def declared_symbols():
+  src = open(HEADER).read()
+  src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+  return sorted(set(re.findall(r"\b(bopx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_api():
+  syms = declared_symbols()
+  for s in ("bopx_create", "bopx_vsd_batch", "bopx_mssd_batch", "bopx_mspd_batch",
+            "bopx_add_batch", "bopx_adi_batch", "bopx_render_depth", "bopx_visib_mask",
+            "bopx_dist_im", "bopx_vsd_batch_dev"):
+    assert s in syms
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libbopx.so not built")
+def test_library_exports_every_declared_symbol():
+  L = ctypes.CDLL(LIB)
+  missing = [s for s in declared_symbols() if not hasattr(L, s)]
+  assert not missing, missing
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libbopx.so not built")
+def test_ctypes_table_matches_header():
+  from bop_toolkit_amd import _lib
+  assert sorted(_lib.SIGNATURES) == declared_symbols()
+  L = _lib.load()
+  assert L.bopx_version() >= 1
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libbopx.so not built")
+def test_no_gpu_fails_loudly():
+  """Without a GPU the product raises instead of silently falling back."""
+  from bop_toolkit_amd import _lib
+  if _lib.device_count() > 0:
+    pytest.skip("GPU present")
+  with pytest.raises(_lib.BopxError):
+    _lib.Context(0)

@@ -1,0 +1,296 @@
+"""HIP path vs the oracle / golden vectors, through the C-ABI (libbopx.so).
+
+Bars (BASELINE.json north_star): bit-exact for masks, counts, raster depth,
+distance images and VSD; within 1e-4 mm / 1e-4 px for MSSD/MSPD/ADD/ADI/PROJ
+(observed ~1e-12)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def ctx():
+  from bop_toolkit_amd import _lib
+  return _lib.Context(0)
+
+
+@pytest.fixture(scope="module")
+def golden_ctx(ctx, golden_errors):
+  g = golden_errors
+  for o in range(4):
+    ctx.add_object(100 + o, g["pts_%d" % o], g["faces_%d" % o])
+    ctx.set_symmetries(100 + o, g["syms_%d" % o])
+  return ctx
+
+
+def _batch(ctx, name, ids, pe, pg, K=None):
+  from bop_toolkit_amd._lib import _d, _i32, ptr
+  ids = np.ascontiguousarray(ids, np.int32)
+  pe = np.ascontiguousarray(pe, np.float64)
+  pg = np.ascontiguousarray(pg, np.float64)
+  out = np.empty(len(ids))
+  if K is None:
+    ctx.call(name, len(ids), ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(out, _d))
+  else:
+    K = np.ascontiguousarray(K, np.float64)
+    ctx.call(name, len(ids), ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(K, _d), ptr(out, _d))
+  return out
+
+
+@pytest.mark.parametrize("name", ["mssd", "mspd", "add", "adi", "proj"])
+def test_point_errors_vs_golden(golden_ctx, golden_errors, name):
+  g = golden_errors
+  ids = g["obj"] + 100
+  K = g["K"] if name in ("mspd", "proj") else None
+  out = _batch(golden_ctx, "bopx_%s_batch" % name, ids, g["pose_est"], g["pose_gt"], K)
+  np.testing.assert_allclose(out, g["out_" + name], rtol=0, atol=TOL)
+  # scale-aware: float64 rounding only
+  assert np.max(np.abs(out - g["out_" + name]) / np.maximum(1.0, np.abs(g["out_" + name]))) < 1e-9
+
+
+def test_drop_in_point_errors(golden_errors):
+  from bop_toolkit_amd import pose_error as pe
+  g = golden_errors
+  for i in range(0, len(g["obj"]), 3):
+    o = int(g["obj"][i])
+    pts = g["pts_%d" % o]
+    syms = [{"R": s[:9].reshape(3, 3), "t": s[9:].reshape(3, 1)} for s in g["syms_%d" % o]]
+    Re, te_ = g["pose_est"][i][:9].reshape(3, 3), g["pose_est"][i][9:].reshape(3, 1)
+    Rg, tg = g["pose_gt"][i][:9].reshape(3, 3), g["pose_gt"][i][9:].reshape(3, 1)
+    K = g["K"][i].reshape(3, 3)
+    assert abs(pe.mssd(Re, te_, Rg, tg, pts, syms) - g["out_mssd"][i]) < TOL
+    assert abs(pe.mspd(Re, te_, Rg, tg, K, pts, syms) - g["out_mspd"][i]) < TOL
+    assert abs(pe.add(Re, te_, Rg, tg, pts) - g["out_add"][i]) < TOL
+    assert abs(pe.adi(Re, te_, Rg, tg, pts) - g["out_adi"][i]) < TOL
+    assert abs(pe.proj(Re, te_, Rg, tg, K, pts) - g["out_proj"][i]) < TOL
+
+
+def test_dist_and_visibility_bit_exact(golden_vsd):
+  from bop_toolkit_amd import misc, visibility
+  g = golden_vsd
+  for i in range(3):
+    dt = misc.depth_im_to_dist_im_fast(g["depth_test"][i], g["K"])
+    dgt = misc.depth_im_to_dist_im_fast(g["depth_gt"][i], g["K"])
+    de = misc.depth_im_to_dist_im_fast(g["depth_est"][i], g["K"])
+    assert np.array_equal(dt, g["dist_test_%d" % i])
+    assert np.array_equal(dgt, g["dist_gt_%d" % i])
+    assert np.array_equal(de, g["dist_est_%d" % i])
+    vg = visibility.estimate_visib_mask_gt(dt, dgt, 15.0, visib_mode="bop19")
+    ve = visibility.estimate_visib_mask_est(dt, de, vg, 15.0, visib_mode="bop19")
+    vg18 = visibility.estimate_visib_mask_gt(dt, dgt, 15.0, visib_mode="bop18")
+    assert np.array_equal(np.packbits(vg), g["visib_gt_%d" % i])
+    assert np.array_equal(np.packbits(ve), g["visib_est_%d" % i])
+    assert np.array_equal(np.packbits(vg18), g["visib_gt18_%d" % i])
+  with pytest.raises(ValueError):
+    visibility.estimate_visib_mask_gt(dt, dgt, 15.0, visib_mode="bop17")
+
+
+class _Stub:
+  def __init__(self, maps):
+    self.maps = list(maps)
+
+  def render_object(self, obj_id, R, t, fx, fy, cx, cy):
+    return {"depth": self.maps.pop(0)}
+
+
+def test_vsd_foreign_renderer_bit_exact(golden_vsd):
+  from bop_toolkit_amd import pose_error as pe
+  g = golden_vsd
+  K, taus = g["K"], list(g["taus"])
+  I, z = np.eye(3), np.zeros((3, 1))
+  for i in range(len(g["vsd_step"])):
+    de, dg, dt = g["depth_est"][i], g["depth_gt"][i], g["depth_test"][i]
+    r = pe.vsd(I, z, I, z, dt, K, 15.0, taus, True, 120.0, _Stub([de, dg]), 1, "step")
+    assert r == list(g["vsd_step"][i])
+    r = pe.vsd(I, z, I, z, dt, K, 15.0, [5.0, 10.0, 20.0], False, 120.0, _Stub([de, dg]), 1)
+    assert r == list(g["vsd_step_raw"][i])
+    r = pe.vsd(I, z, I, z, dt, K, 5.0, taus, True, 120.0, _Stub([de, dg]), 1)
+    assert r == list(g["vsd_delta5"][i])
+    r = pe.vsd(I, z, I, z, dt, K, 15.0, taus, True, 120.0, _Stub([de, dg]), 1, "tlinear")
+    np.testing.assert_allclose(r, g["vsd_tlinear"][i], rtol=0, atol=1e-12)
+  zz = np.zeros_like(g["depth_test"][0])
+  assert pe.vsd(I, z, I, z, g["depth_test"][0], K, 15.0, taus, True, 120.0, _Stub([zz, zz]), 1,
+                "bogus") == list(g["vsd_empty"])
+  with pytest.raises(ValueError):
+    pe.vsd(I, z, I, z, g["depth_test"][3], K, 15.0, taus, True, 120.0,
+           _Stub([g["depth_est"][3], g["depth_gt"][3]]), 1, "bogus")
+
+
+def _scene(seed, n, W=640, H=480, n_lat=20, n_lon=40, K=None):
+  from bop_toolkit_amd import synth
+  rng = np.random.default_rng(seed)
+  pts, faces = synth.superellipsoid(n_lat, n_lon, (45.0, 35.0, 55.0), 0.7)
+  Rg, tg = synth.gt_poses(rng, n, z_range=(450.0, 1200.0))
+  Re, te_ = synth.perturb(rng, Rg, tg)
+  K = synth.LMO_K if K is None else K
+  return rng, pts, faces, Rg, tg, Re, te_, K
+
+
+def test_raster_bit_exact_vs_oracle(ctx, oracle_mod):
+  from bop_toolkit_amd.renderer import create_renderer
+  rng, pts, faces, Rg, tg, Re, te_, K = _scene(7, 24)
+  ren = create_renderer(640, 480, "hip", mode="depth")
+  ren.add_object_arrays(5, pts, faces)
+  fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+  for i in range(24):
+    R, t = (Re[i], te_[i]) if i % 2 else (Rg[i], tg[i])
+    if i == 3:
+      t = np.array([0.0, 0.0, 60.0])  # very close: vertices beyond the guard band
+    if i == 4:
+      t = np.array([0.0, 0.0, -200.0])  # behind the camera
+    d_hip = ren.render_object(5, R, t, fx, fy, cx, cy)["depth"]
+    d_ref = oracle_mod.render_depth(pts, faces, R, t, fx, fy, cx, cy, 640, 480)
+    assert np.array_equal(d_hip, d_ref), i
+    if i not in (3, 4):
+      assert (d_hip > 0).sum() > 100
+
+
+def _fused_vs_oracle(oracle_mod, seed, n, W, H, K, n_lat, n_lon, delta=15.0, cost="step",
+                     normalized=True):
+  """Fused k_vsd (raster + VSD) vs oracle raster + oracle VSD, bit for bit."""
+  from bop_toolkit_amd import _lib
+  from bop_toolkit_amd._lib import _d, _f, _i32, ptr
+  rng, pts, faces, Rg, tg, Re, te_, _ = _scene(seed, n, W, H, n_lat, n_lon)
+  ctx = _lib.Context(0)
+  ctx.add_object(9, pts, faces)
+  fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+  frames = []
+  for i in range(n):
+    dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, W, H)
+    dt = np.where(dg > 0, dg, 1600.0).astype(np.float32)
+    dt += rng.normal(0, 3.0, dt.shape).astype(np.float32)
+    dt[rng.random(dt.shape) < 0.1] = 0.0
+    frames.append(np.round(dt).astype(np.float32))
+  frames = np.stack(frames)
+  taus = np.arange(0.05, 0.51, 0.05)
+  ids = np.full(n, 9, np.int32)
+  pe = np.concatenate([Re.reshape(n, 9), te_], 1)
+  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
+  fi = np.arange(n, dtype=np.int32)
+  cam = np.tile([fx, fy, cx, cy], (n, 1)).astype(np.float64)
+  dia = np.full(n, 160.0)
+  out = np.empty((n, len(taus)))
+  code = {"step": 0, "tlinear": 1}[cost]
+  ctx.call("bopx_vsd_batch", n, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(fi, _i32),
+           ptr(frames, _f), n, W, H, ptr(cam, _d), delta, 0, ptr(taus, _d), len(taus),
+           int(normalized), ptr(dia, _d), code, ptr(out, _d))
+  for i in range(n):
+    de = oracle_mod.render_depth(pts, faces, Re[i], te_[i], fx, fy, cx, cy, W, H)
+    dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, W, H)
+    ref = oracle_mod.vsd_depths(frames[i], de, dg, fx, fy, cx, cy, delta, taus, normalized,
+                                160.0, cost)
+    if cost == "step":
+      assert list(out[i]) == ref, (i, out[i], ref)
+    else:
+      np.testing.assert_allclose(out[i], ref, rtol=0, atol=1e-12)
+  ctx.close()
+  return out
+
+
+def test_fused_vsd_bit_exact_lmo(oracle_mod):
+  from bop_toolkit_amd import synth
+  out = _fused_vs_oracle(oracle_mod, 11, 40, 640, 480, synth.LMO_K, 30, 60)
+  assert np.ptp(out) > 0.1  # non-trivial errors
+
+
+def test_fused_vsd_bit_exact_ycbv_big_mesh(oracle_mod):
+  from bop_toolkit_amd import synth
+  _fused_vs_oracle(oracle_mod, 12, 16, 640, 480, synth.YCBV_K, 50, 100)
+
+
+def test_fused_vsd_tlinear_and_raw(oracle_mod):
+  from bop_toolkit_amd import synth
+  _fused_vs_oracle(oracle_mod, 13, 12, 640, 480, synth.LMO_K, 20, 40, cost="tlinear")
+  _fused_vs_oracle(oracle_mod, 14, 12, 720, 540, synth.TLESS_K, 20, 40, delta=5.0,
+                   normalized=False)
+
+
+def test_drop_in_vsd_with_hip_renderer(oracle_mod):
+  from bop_toolkit_amd import pose_error as pe, synth
+  from bop_toolkit_amd.renderer import create_renderer
+  rng, pts, faces, Rg, tg, Re, te_, K = _scene(15, 6)
+  ren = create_renderer(640, 480, "hip", mode="depth")
+  ren.add_object_arrays(21, pts, faces)
+  fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+  taus = list(np.arange(0.05, 0.51, 0.05))
+  for i in range(6):
+    dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, 640, 480)
+    dt = np.where(dg > 0, dg + 1.0, 0.0).astype(np.float32)
+    e = pe.vsd(Re[i], te_[i].reshape(3, 1), Rg[i], tg[i].reshape(3, 1), dt, K, 15.0, taus, True,
+               150.0, ren, 21, "step")
+    de = oracle_mod.render_depth(pts, faces, Re[i], te_[i], fx, fy, cx, cy, 640, 480)
+    assert e == oracle_mod.vsd_depths(dt, de, dg, fx, fy, cx, cy, 15.0, taus, True, 150.0)
+    # est == gt on its own render: VSD = 0
+    e0 = pe.vsd(Rg[i], tg[i].reshape(3, 1), Rg[i], tg[i].reshape(3, 1), dt, K, 15.0, taus,
+                True, 150.0, ren, 21, "step")
+    assert e0 == [0.0] * len(taus)
+
+
+def test_batch_evaluator_matches_oracle(oracle_mod):
+  import torch
+  from bop_toolkit_amd import misc, synth
+  from bop_toolkit_amd.batch import BatchEvaluator
+  rng = np.random.default_rng(21)
+  ev = BatchEvaluator(0)
+  objs = []
+  for o, (nd, cont) in enumerate([(1, False), (4, False), (2, False), (1, True)]):
+    pts, faces = synth.superellipsoid(16, 32, (30.0 + 5 * o, 40.0, 50.0 - 5 * o), 0.6 + 0.1 * o)
+    info = synth.models_info_entry(pts, nd, cont)
+    syms = misc.get_symmetry_transformations(info, 0.01)
+    ev.add_object(o, pts, faces, syms, info["diameter"])
+    objs.append({"pts": pts, "faces": faces, "syms": misc.symmetries_to_array(syms),
+                 "diameter": info["diameter"]})
+  n, W, H = 32, 640, 480
+  K = synth.LMO_K
+  obj = rng.integers(0, 4, n).astype(np.int32)
+  Rg, tg = synth.gt_poses(rng, n)
+  Re, te_ = synth.perturb(rng, Rg, tg)
+  pe = np.concatenate([Re.reshape(n, 9), te_], 1)
+  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
+  cam = np.array([[K[0, 0], K[1, 1], K[0, 2], K[1, 2]]])
+  dev = ev.device
+  t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+  slots = ev.slots(obj)
+  fi = np.zeros(n, np.int32)
+  # composite test depth of all GT instances in one frame, rendered on the GPU
+  frames = ev.render(slots, t(pg, torch.float64), t(fi, torch.int32), t(cam, torch.float64), 1, W,
+                     H)
+  frames = torch.round(torch.where(frames > 0, frames, torch.full_like(frames, 1500.0)))
+  dia = np.array([objs[o]["diameter"] for o in obj])
+  Kt = t(np.tile(K.reshape(9), (n, 1)), torch.float64)
+  res = ev.bop19(slots, t(pe, torch.float64), t(pg, torch.float64), Kt, t(fi, torch.int32),
+                 frames, t(cam, torch.float64), 15.0, np.arange(0.05, 0.51, 0.05),
+                 t(dia, torch.float64))
+  torch.cuda.synchronize()
+  fr = frames.cpu().numpy()
+  ref_vsd, ref_mssd, ref_mspd = oracle_mod.bop19_batch(objs, obj, pe, pg, fi, fr, cam, 15.0,
+                                                       np.arange(0.05, 0.51, 0.05), dia)
+  assert np.array_equal(res["vsd"].cpu().numpy(), ref_vsd)
+  np.testing.assert_allclose(res["mssd"].cpu().numpy(), ref_mssd, rtol=0, atol=TOL)
+  np.testing.assert_allclose(res["mspd"].cpu().numpy(), ref_mspd, rtol=0, atol=TOL)
+  # the composited frame equals the oracle's min-composite of the GT renders
+  comp = np.full((H, W), np.inf, np.float32)
+  for i in range(n):
+    d = oracle_mod.render_depth(objs[obj[i]]["pts"], objs[obj[i]]["faces"], Rg[i], tg[i],
+                                K[0, 0], K[1, 1], K[0, 2], K[1, 2], W, H)
+    comp = np.where(d > 0, np.minimum(comp, d), comp)
+  comp[np.isinf(comp)] = 1500.0
+  assert np.array_equal(np.round(comp), fr[0])
+
+
+def test_errors_on_bad_input(ctx):
+  from bop_toolkit_amd._lib import _d, _i32, ptr
+  ids = np.array([12345], np.int32)
+  pe = np.zeros(12)
+  out = np.empty(1)
+  with pytest.raises(KeyError):
+    ctx.call("bopx_mssd_batch", 1, ptr(ids, _i32), ptr(pe, _d), ptr(pe, _d), ptr(out, _d))
+  ctx.add_object(77, np.zeros((3, 3)), None)
+  with pytest.raises(ValueError):  # no symmetry set registered
+    ids = np.array([77], np.int32)
+    ctx.call("bopx_mssd_batch", 1, ptr(ids, _i32), ptr(pe, _d), ptr(pe, _d), ptr(out, _d))
+  # n == 0 is a no-op
+  ctx.call("bopx_mssd_batch", 0, ptr(ids, _i32), ptr(pe, _d), ptr(pe, _d), ptr(out, _d))

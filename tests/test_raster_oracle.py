@@ -1,0 +1,108 @@
+"""Analytic and property tests of the raster spec on the CPU
+twin. The reference renderers (vispy/glumpy/bop_renderer) cannot run here, so
+raster parity with them is unpinned; these tests pin the spec itself, and
+tests/test_gpu_parity.py pins the HIP rasteriser to this twin bit for bit."""
+import numpy as np
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+FX, FY, CX, CY = 500.0, 500.0, 31.7, 23.3
+W, H = 64, 48
+I3 = np.eye(3)
+
+
+def grid_plane(n, size, z=0.0, jitter=0.0, rng=None):
+  xs = np.linspace(-size, size, n + 1)
+  X, Y = np.meshgrid(xs, xs, indexing="ij")
+  pts = np.stack([X.ravel(), Y.ravel(), np.full(X.size, z)], 1)
+  if jitter and rng is not None:
+    inner = (np.abs(X.ravel()) < size) & (np.abs(Y.ravel()) < size)
+    pts[inner, :2] += rng.uniform(-jitter, jitter, (inner.sum(), 2))
+  faces = []
+  for i in range(n):
+    for j in range(n):
+      a, b, c, d = i * (n + 1) + j, (i + 1) * (n + 1) + j, (i + 1) * (n + 1) + j + 1, i * (n + 1) + j + 1
+      faces += [(a, b, c), (a, c, d)]
+  return pts, np.array(faces, np.uint32)
+
+
+def test_fronto_parallel_quad_exact(oracle_mod):
+  pts, faces = grid_plane(1, 20.0)
+  d = oracle_mod.render_depth(pts, faces, I3, np.array([0.0, 0.0, 1000.0]), FX, FY, CX, CY, W, H)
+  cov = d > 0
+  assert np.all(d[cov] == np.float32(1000.0))
+  # covered pixel centres: |c + 0.5 - CX| * 1000 / FX < 20 (edges not on centres here)
+  c = np.arange(W) + 0.5
+  r = np.arange(H) + 0.5
+  exp = (np.abs(c[None, :] - CX) < 10.0) & (np.abs(r[:, None] - CY) < 10.0)
+  assert np.array_equal(cov, exp)
+
+
+def test_slanted_plane_depth(oracle_mod):
+  # plane z_model = 0 rotated about the y axis by 30 deg, at Z = 800
+  a = np.deg2rad(30.0)
+  R = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+  t = np.array([0.0, 0.0, 800.0])
+  pts, faces = grid_plane(4, 15.0)
+  d = oracle_mod.render_depth(pts, faces, R, t, FX, FY, CX, CY, W, H)
+  n = R[:, 2]  # plane normal in camera frame; plane: n . X = n . t
+  rr, cc = np.nonzero(d)
+  assert len(rr) > 50
+  ray = np.stack([(cc + 0.5 - CX) / FX, (rr + 0.5 - CY) / FY, np.ones(len(rr))], 1)
+  z_exact = (n @ t) / (ray @ n)
+  np.testing.assert_allclose(d[rr, cc], z_exact, rtol=2e-6)
+
+
+def test_watertight_grid(oracle_mod):
+  rng = np.random.default_rng(3)
+  pts, faces = grid_plane(9, 18.0, jitter=1.5, rng=rng)
+  t = np.array([0.3, -0.2, 1000.0])
+  cov = oracle_mod.coverage(pts, faces, I3, t, FX, FY, CX, CY, W, H)
+  assert cov.max() == 1  # no pixel centre claimed by two triangles
+  d = oracle_mod.render_depth(pts, faces, I3, t, FX, FY, CX, CY, W, H)
+  assert np.array_equal(cov == 1, d > 0)
+  # no holes: the covered set is exactly the outer square's pixel centres
+  c = np.arange(W) + 0.5
+  r = np.arange(H) + 0.5
+  u = (c - CX) * 1000.0 / FX - 0.3
+  v = (r - CY) * 1000.0 / FY + 0.2
+  inside = (np.abs(u)[None, :] < 18.0) & (np.abs(v)[:, None] < 18.0)
+  assert np.array_equal(cov == 1, inside)
+
+
+def test_winding_and_nearest(oracle_mod):
+  pts, faces = grid_plane(2, 10.0)
+  t = np.array([0.0, 0.0, 900.0])
+  d1 = oracle_mod.render_depth(pts, faces, I3, t, FX, FY, CX, CY, W, H)
+  d2 = oracle_mod.render_depth(pts, faces[:, ::-1].copy(), I3, t, FX, FY, CX, CY, W, H)
+  assert np.array_equal(d1, d2)  # no culling: both windings rasterise identically
+  # two layers: the nearer one wins
+  pts2 = np.concatenate([pts, pts + [0.0, 0.0, 50.0]])
+  faces2 = np.concatenate([faces, faces + len(pts)])
+  d3 = oracle_mod.render_depth(pts2, faces2, I3, t, FX, FY, CX, CY, W, H)
+  assert np.array_equal(d3, d1)
+
+
+def test_behind_camera_and_background(oracle_mod):
+  pts, faces = grid_plane(2, 10.0)
+  d = oracle_mod.render_depth(pts, faces, I3, np.array([0.0, 0.0, -500.0]), FX, FY, CX, CY, W, H)
+  assert not d.any()
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.lists(st.floats(-25, 25, allow_nan=False), min_size=8, max_size=8),
+       st.floats(300, 3000))
+def test_shared_edge_property(coords, z):
+  """Two triangles sharing an edge: every pixel centre strictly inside the
+  union is covered exactly once (top-left rule), never twice."""
+  from oracle import oracle
+  a, b, c, d = (np.array(coords[i:i + 2]) for i in (0, 2, 4, 6))
+  pts = np.array([[*a, 0.0], [*b, 0.0], [*c, 0.0], [*d, 0.0]])
+  faces = np.array([[0, 1, 2], [0, 2, 3]], np.uint32)  # shared edge 0-2
+  cov = oracle.coverage(pts, faces, I3, np.array([0.0, 0.0, z]), FX, FY, CX, CY, W, H)
+  # the two triangles lie on opposite sides of edge 0-2 only if b, d are on
+  # opposite sides; otherwise they overlap and double coverage is legitimate.
+  def side(p):
+    return np.sign((c[0] - a[0]) * (p[1] - a[1]) - (c[1] - a[1]) * (p[0] - a[0]))
+  if side(b) * side(d) < 0:
+    assert cov.max() <= 1
