@@ -1,0 +1,330 @@
+#!/usr/bin/env python
+"""BOP19 pose-error throughput on MI355X: VSD (10 taus) + MSSD + MSPD tuples/s.
+
+One step = the full BOP19 error set of every (est, gt) tuple of a synthetic
+batch (BASELINE.json configs[3], per-GPU shard): 21 LM-O/YCB-V-like objects
+(5,002 verts / 10,000 faces, S in {1,2,4,8} + one continuous-symmetry object
+with S = 314), 640x480 test depth, YCB-V intrinsics, 6 objects per image,
+12,500 tuples per GPU by default (100k tuples over 8 GPUs = configs[3]).
+Inputs are resident in HBM before timing; each step runs k_vsd (both renders
++ VSD fused), k_sym_error<MSSD> and k_sym_error<MSPD>, and for N > 1 an RCCL
+all-gather of the per-tuple error rows. Weak scaling: each rank owns a fixed
+shard of images (tuples are independent).
+
+    python bench.py [--gpus N --steps K --warmup W --tuples T]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+N_TAU = 10
+TAUS = np.arange(0.05, 0.51, 0.05)
+DELTA = 15.0
+W, H = 640, 480
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level table)
+HBM_PEAK_GBS = 8000.0
+FP64_PEAK_TF = 78.6
+FP32_PEAK_TF = 157.3
+
+
+def parse():
+  ap = argparse.ArgumentParser()
+  ap.add_argument("--gpus", type=int, default=1)
+  ap.add_argument("--steps", type=int, default=10)
+  ap.add_argument("--warmup", type=int, default=2)
+  ap.add_argument("--tuples", type=int, default=12500, help="tuples per GPU")
+  ap.add_argument("--objects", type=int, default=21)
+  ap.add_argument("--n-lat", type=int, default=50)
+  ap.add_argument("--n-lon", type=int, default=100)
+  ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                  help="target wall time of the CPU-baseline sample")
+  ap.add_argument("--no-cpu-baseline", action="store_true")
+  ap.add_argument("--seed", type=int, default=20250220 + 4)
+  return ap.parse_args()
+
+
+def build_objects(ev, args, torch):
+  from bop_toolkit_amd import misc, synth
+  rng = np.random.default_rng(args.seed)
+  objs = []
+  for o in range(args.objects):
+    axes = tuple(rng.uniform(30.0, 100.0, 3))
+    pts, faces = synth.superellipsoid(args.n_lat, args.n_lon, axes, float(rng.uniform(0.5, 1.0)))
+    p = torch.as_tensor(pts, device=ev.device)
+    dia = float(torch.cdist(p, p, compute_mode="donot_use_mm_for_euclid_dist").max())
+    info = {"diameter": dia}
+    if o == args.objects - 1:
+      info["symmetries_continuous"] = [{"axis": [0, 0, 1], "offset": [0, 0, 0]}]
+    else:
+      n_disc = [1, 2, 4, 8][o % 4]
+      info["symmetries_discrete"] = [
+          np.concatenate([np.concatenate([synth.rot_z(2 * np.pi * j / n_disc), np.zeros((3, 1))],
+                                         1), [[0, 0, 0, 1]]]).reshape(-1).tolist()
+          for j in range(1, n_disc)]
+    syms = misc.get_symmetry_transformations(info, 0.01)
+    ev.add_object(o, pts, faces, syms, dia)
+    objs.append({"pts": pts, "faces": faces, "syms": misc.symmetries_to_array(syms),
+                 "diameter": dia, "bbox": (pts.min(0), pts.max(0))})
+  return objs
+
+
+def build_workload(ev, objs, args, rank, torch):
+  """Images with 6 objects each; test depth = composite GT render + background
+  plane + occluder + noise + 10 % holes, rounded to integer mm (uint16 PNG)."""
+  from bop_toolkit_amd import synth
+  rng = np.random.default_rng(args.seed + 1000 * (rank + 1))
+  per_img = 6
+  n_img = (args.tuples + per_img - 1) // per_img
+  n = n_img * per_img
+  obj = np.stack([rng.choice(len(objs), per_img, replace=False) for _ in range(n_img)]).reshape(-1)
+  obj = obj.astype(np.int32)
+  Rg, tg = synth.gt_poses(rng, n)
+  Re, te = synth.perturb(rng, Rg, tg)
+  pe = np.concatenate([Re.reshape(n, 9), te], 1)
+  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
+  frame_idx = np.repeat(np.arange(n_img, dtype=np.int32), per_img)
+  K = synth.YCBV_K
+  cam = np.tile([K[0, 0], K[1, 1], K[0, 2], K[1, 2]], (n_img, 1)).astype(np.float64)
+  dev = ev.device
+  t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+  d = {"slots": ev.slots(obj), "pose_est": t(pe, torch.float64), "pose_gt": t(pg, torch.float64),
+       "frame_idx": t(frame_idx, torch.int32), "cam": t(cam, torch.float64),
+       "K": t(np.tile(K.reshape(9), (n, 1)), torch.float64),
+       "diameters": t([objs[o]["diameter"] for o in obj], torch.float64)}
+  frames = ev.render(d["slots"], d["pose_gt"], d["frame_idx"], d["cam"], n_img, W, H)
+  g = torch.Generator(device=dev)
+  g.manual_seed(args.seed + rank)
+  frames = torch.where(frames > 0, frames, torch.full_like(frames, 1600.0))
+  # one occluder rectangle per image in front of the scene
+  ys = torch.arange(H, device=dev).view(1, H, 1)
+  xs = torch.arange(W, device=dev).view(1, 1, W)
+  x0 = torch.randint(0, W - 120, (n_img, 1, 1), device=dev, generator=g)
+  y0 = torch.randint(0, H - 120, (n_img, 1, 1), device=dev, generator=g)
+  sz = torch.randint(40, 120, (n_img, 1, 1), device=dev, generator=g)
+  occ = (xs >= x0) & (xs < x0 + sz) & (ys >= y0) & (ys < y0 + sz)
+  frames = torch.where(occ, torch.full_like(frames, 450.0), frames)
+  frames = frames + 2.0 * torch.randn(frames.shape, device=dev, generator=g)
+  frames = torch.round(frames).clamp_(0, 65535)
+  frames[torch.rand(frames.shape, device=dev, generator=g) < 0.1] = 0.0
+  d["frames"] = frames.contiguous()
+  d["host"] = {"obj": obj, "pe": pe, "pg": pg, "frame_idx": frame_idx, "cam": cam}
+  torch.cuda.synchronize()
+  return n, d
+
+
+def roi_pixels(objs, obj, poses, K):
+  """Survey §8d ROI: union over both poses of the clipped screen bbox of the
+  projected 8 model-bbox corners (whole image if a corner is behind the camera)."""
+  n = len(obj)
+  lo = np.stack([objs[o]["bbox"][0] for o in obj])
+  hi = np.stack([objs[o]["bbox"][1] for o in obj])
+  corners = np.stack([np.where(np.array([(k >> a) & 1 for a in range(3)]) == 1, hi, lo)
+                      for k in range(8)], 1)  # n x 8 x 3
+  x0 = np.full(n, np.inf)
+  y0 = np.full(n, np.inf)
+  x1 = np.full(n, -np.inf)
+  y1 = np.full(n, -np.inf)
+  full = np.zeros(n, bool)
+  for p in poses:
+    R = p[:, :9].reshape(n, 3, 3)
+    t = p[:, 9:]
+    X = np.einsum("nij,nkj->nki", R, corners) + t[:, None, :]
+    full |= (X[..., 2] <= 0).any(1)
+    Z = np.where(X[..., 2] > 0, X[..., 2], 1.0)
+    u = K[0, 0] * X[..., 0] / Z + K[0, 2]
+    v = K[1, 1] * X[..., 1] / Z + K[1, 2]
+    x0 = np.minimum(x0, u.min(1))
+    x1 = np.maximum(x1, u.max(1))
+    y0 = np.minimum(y0, v.min(1))
+    y1 = np.maximum(y1, v.max(1))
+  w = np.clip(np.floor(x1), -1, W - 1) - np.clip(np.ceil(x0), 0, W) + 1
+  h = np.clip(np.floor(y1), -1, H - 1) - np.clip(np.ceil(y0), 0, H) + 1
+  area = np.maximum(w, 0) * np.maximum(h, 0)
+  area[full] = W * H
+  return area
+
+
+def algorithmic_cost(objs, host, n):
+  """Compulsory HBM bytes and VALU flops per launch (SURVEY.md §8d formulas)."""
+  from bop_toolkit_amd import synth
+  obj = host["obj"]
+  roi = roi_pixels(objs, obj, [host["pe"], host["pg"]], synth.YCBV_K)
+  used = np.unique(obj)
+  V = np.array([len(objs[o]["pts"]) for o in obj], np.float64)
+  F = np.array([len(objs[o]["faces"]) for o in obj], np.float64)
+  S = np.array([len(objs[o]["syms"]) for o in obj], np.float64)
+  mesh_bytes = sum(12 * len(objs[o]["pts"]) + 12 * len(objs[o]["faces"]) for o in used)
+  sym_bytes = sum(96 * len(objs[o]["syms"]) for o in used)
+  vsd_bytes = n * (192 + 16 + 8 * N_TAU) + 4.0 * roi.sum() + mesh_bytes
+  vsd_f32 = (40 * V + 60 * F + 34 * roi).sum()
+  vsd_f64 = (58 * roi).sum()
+  mssd_bytes = n * (192 + 4 + 8) + sum(24 * len(objs[o]["pts"]) for o in used) + sym_bytes
+  mspd_bytes = mssd_bytes + n * 72
+  mssd_f64 = (V * (18 + 28 * S)).sum()
+  mspd_f64 = (V * (20 + 27 * S)).sum()
+  return {"vsd": (vsd_bytes, vsd_f32, vsd_f64), "mssd": (mssd_bytes, 0.0, mssd_f64),
+          "mspd": (mspd_bytes, 0.0, mspd_f64), "roi_mean": float(roi.mean())}
+
+
+def load_traffic():
+  """HBM bytes per k_vsd launch from the committed rocprofv3 PMC summary
+  (profiles/*_pmc.json, written by tools/pmc_summary.py), or None."""
+  import glob
+  best = None
+  for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json"))):
+    try:
+      with open(path) as f:
+        best = json.load(f).get("k_vsd", {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+      pass
+  return best
+
+
+def cpu_baseline(objs, d, n, seconds):
+  """Oracle (C restatement of the reference per-tuple algorithm: two full-frame
+  renders, three full-frame distance images, per-symmetry loops) on the host
+  cores, OpenMP over tuples, on a bounded sample of the same workload."""
+  threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), 16))
+  os.environ["OMP_NUM_THREADS"] = str(threads)
+  from oracle import oracle
+  h = d["host"]
+  frames = d["frames"]
+
+  def run(m):
+    fidx = h["frame_idx"][:m]
+    used = np.unique(fidx)
+    remap = np.searchsorted(used, fidx).astype(np.int32)
+    fr = frames[used.tolist()].cpu().numpy()
+    t0 = time.perf_counter()
+    oracle.bop19_batch(objs, h["obj"][:m], h["pe"][:m], h["pg"][:m], remap, fr, h["cam"][used],
+                       DELTA, TAUS, np.array([objs[o]["diameter"] for o in h["obj"][:m]]))
+    return time.perf_counter() - t0
+
+  m0 = min(n, 2 * threads)
+  t0 = run(m0)
+  m = int(min(n, max(m0, m0 * seconds / max(t0, 1e-3))))
+  t1 = run(m)
+  return {"value": m / t1, "unit": "tuples/s", "cores": threads, "kind": "port",
+          "sample": "%d tuples (first %d of this rank's workload), BOP19 set, %.1f s wall; "
+                    "oracle/bopx_oracle.c, reference per-tuple algorithm in C" % (m, m, t1)}
+
+
+def main():
+  args = parse()
+  import torch
+  import torch.distributed as dist
+
+  rank = int(os.environ.get("RANK", 0))
+  world = int(os.environ.get("WORLD_SIZE", 1))
+  local = int(os.environ.get("LOCAL_RANK", 0))
+  torch.cuda.set_device(local)
+  if world > 1:
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+  from bop_toolkit_amd.batch import BatchEvaluator
+  ev = BatchEvaluator(local)
+  objs = build_objects(ev, args, torch)
+  n, d = build_workload(ev, objs, args, rank, torch)
+
+  out_vsd = torch.empty((n, N_TAU), dtype=torch.float64, device=ev.device)
+  out_mssd = torch.empty(n, dtype=torch.float64, device=ev.device)
+  out_mspd = torch.empty(n, dtype=torch.float64, device=ev.device)
+  rows = torch.empty((n, N_TAU + 2), dtype=torch.float64, device=ev.device)
+  gathered = torch.empty((world * n, N_TAU + 2), dtype=torch.float64, device=ev.device)
+  ktime = {"vsd": 0.0, "mssd": 0.0, "mspd": 0.0}
+  marks = []  # per timed step: HIP events bracketing each kernel on the launch stream
+
+  def step(timed):
+    e = {k: [torch.cuda.Event(enable_timing=True) for _ in range(2)] for k in ktime} \
+        if timed else None
+    if e: e["vsd"][0].record()
+    ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"], d["frames"], d["cam"], DELTA,
+           TAUS, d["diameters"], out=out_vsd)
+    if e: e["vsd"][1].record(); e["mssd"][0].record()
+    ev.mssd(d["slots"], d["pose_est"], d["pose_gt"], out=out_mssd)
+    if e: e["mssd"][1].record(); e["mspd"][0].record()
+    ev.mspd(d["slots"], d["pose_est"], d["pose_gt"], d["K"], out=out_mspd)
+    if e: e["mspd"][1].record(); marks.append(e)
+    if world > 1:
+      rows[:, :N_TAU] = out_vsd
+      rows[:, N_TAU] = out_mssd
+      rows[:, N_TAU + 1] = out_mspd
+      dist.all_gather_into_tensor(gathered, rows)
+
+  for _ in range(args.warmup):
+    step(False)
+  torch.cuda.synchronize()
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  for _ in range(args.steps):
+    step(True)
+  torch.cuda.synchronize()
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize()
+  elapsed = time.perf_counter() - t0
+  for e in marks:
+    for k in ktime:
+      ktime[k] += e[k][0].elapsed_time(e[k][1]) * 1e-3
+  if world > 1:
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=ev.device)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    elapsed = float(tt.item())
+
+  if rank == 0:
+    steps = args.steps
+    total = n * world * steps
+    cost = algorithmic_cost(objs, d["host"], n)
+    kt = {k: v / steps for k, v in ktime.items()}
+    roof = None
+    kernels = {}
+    if kt:
+      for k in ("vsd", "mssd", "mspd"):
+        b, f32, f64 = cost[k]
+        t_valu = f64 / (FP64_PEAK_TF * 1e12) + f32 / (FP32_PEAK_TF * 1e12)
+        kernels[k] = {"ms": kt[k] * 1e3, "alg_GBps": b / kt[k] / 1e9,
+                      "valu_roof_frac": t_valu / kt[k]}
+      dom = max(kt, key=kt.get)
+      b, f32, f64 = cost[dom]
+      ach = b / kt[dom] / 1e9
+      t_valu = f64 / (FP64_PEAK_TF * 1e12) + f32 / (FP32_PEAK_TF * 1e12)
+      traffic = load_traffic() if dom == "vsd" else None
+      roof = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": traffic,
+              "kernel": "k_vsd" if dom == "vsd" else "k_sym_error<%s>" % dom.upper(),
+              "binding": {"roof": "valu", "frac": round(t_valu / kt[dom], 4),
+                          "note": "VALU-bound by SURVEY.md §8d flop/byte; fp64 %.1f TF + "
+                                  "fp32 %.1f TF peaks" % (FP64_PEAK_TF, FP32_PEAK_TF)}}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+      cpu = cpu_baseline(objs, d, n, args.cpu_seconds)
+    line = {
+        "metric": "pose-error tuples/sec (VSD+MSSD+MSPD) at 640x480, ~5k-vert meshes",
+        "value": total / elapsed, "unit": "tuples/s", "n_gpus": world, "steps": steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64+f32", "data": "synthetic",
+        "config": {"workload": "BASELINE configs[3] per-GPU shard: BOP19 error set (VSD 10 taus "
+                               "+ MSSD + MSPD), %d objs V=%d F=%d S in {1,2,4,8,314}, "
+                               "%dx%d YCB-V K, %d tuples/GPU" % (
+                                   args.objects, len(objs[0]["pts"]), len(objs[0]["faces"]), W,
+                                   H, n),
+                   "global_batch": n * world, "parallelism": "image-sharded x%d" % world,
+                   "roi_mean_px": round(cost["roi_mean"], 1)},
+        "roofline": roof, "kernels": kernels, "cpu_baseline": cpu}
+    print(json.dumps(line), flush=True)
+  if world > 1:
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+  main()

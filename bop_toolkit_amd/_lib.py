@@ -79,6 +79,14 @@ def load():
   global _lib
   with _lock:
     if _lib is None:
+      # One HIP runtime per process: torch ships its own libamdhip64 (SONAME
+      # libamdhip64.so.7, like /opt/rocm's). Loading torch first lets the
+      # dynamic linker bind libbopx's NEEDED libamdhip64.so.7 to torch's copy;
+      # the other order leaves two runtimes and torch then finds no GPU.
+      try:
+        import torch  # noqa: F401
+      except ImportError:
+        pass
       if not os.path.exists(LIB_PATH):
         raise ImportError(
             "libbopx.so not found at %s: build it with `python -c 'import __graft_entry__ as g;"
