@@ -11,11 +11,11 @@
 //     the vertices) into a conservative pixel rectangle kept in LDS. Their
 //     union is the tuple's region of interest (ROI): pixels outside both
 //     silhouettes cannot change VSD (masks need d_model > 0, visibility.py:37).
-//  2. The ROI is swept in 64x64 screen tiles. Per tile, both depth buffers
-//     (est, gt) live in LDS (2 x 16 KiB, +inf cleared); the meshlets whose
-//     rectangle touches the tile are listed, and each wave rasterises one
+//  2. The ROI is swept in 64x64 screen tiles. Per tile, both q-buffers
+//     (est, gt; q = 1/Z, 0 = empty) live in LDS (2 x 16 KiB); the meshlets
+//     whose rectangle touches the tile are listed, and each wave rasterises one
 //     meshlet per step (lane = triangle) with exact integer edge functions and
-//     an LDS atomicMin on the float bits (order-independent z-buffer).
+//     an LDS atomicMax on the float bits (order-independent z-buffer, raster.h).
 //  3. The tile's pixels are then evaluated in place: test depth is read from
 //     HBM (coalesced rows), the three float64 distances and the float32
 //     visibility tests follow the reference operation order exactly
@@ -29,7 +29,6 @@
 namespace bopx {
 
 constexpr int kVsdThreads = 256;
-constexpr uint32_t kInfBits = 0x7F800000u;
 
 // float64 distance of a float32 depth at pixel (pX, pY) (misc.py:158-161).
 __device__ __forceinline__ double dist_of(double pX, double pY, float depth) {
@@ -99,8 +98,10 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
   __shared__ float s_pose[2][12];
   __shared__ int s_roi[4];
   __shared__ int s_nlist;
-  __shared__ uint32_t s_cnt[kVsdThreads / 64][2 + kMaxTaus];
-  __shared__ double s_lin[kVsdThreads / 64][kMaxTaus];
+  __shared__ double s_pX[kTileW], s_pY[kTileH];
+  // Final per-wave partial counters reuse the depth tiles (after the tile loop).
+  uint32_t(*s_cnt)[2 + kMaxTaus] = reinterpret_cast<uint32_t(*)[2 + kMaxTaus]>(&s_dep[0][0]);
+  double(*s_lin)[kMaxTaus] = reinterpret_cast<double(*)[kMaxTaus]>(&s_dep[1][0]);
 
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -156,8 +157,11 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
       const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
       // 2a. clear both depth tiles, list the meshlets touching the tile.
       uint32_t* dep_flat = &s_dep[0][0];
-      for (int i = tid; i < 2 * kTileW * kTileH; i += kVsdThreads) dep_flat[i] = kInfBits;
+      for (int i = tid; i < 2 * kTileW * kTileH; i += kVsdThreads) dep_flat[i] = 0u;
       if (tid == 0) s_nlist = 0;
+      // float64 distance coefficients of the tile's columns / rows (misc.py:137-138)
+      if (tid < kTileW) s_pX[tid] = ((double)(tx0 + tid) - cx) / fx;
+      else if (tid < kTileW + kTileH) s_pY[tid - kTileW] = ((double)(ty0 + tid - kTileW) - cy) / fy;
       __syncthreads();
       for (int i = tid; i < 2 * nm; i += kVsdThreads) {
         const short4 rc = s_rect[i];
@@ -182,15 +186,11 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
           const RVtx C = r_vertex(Rf, c32, v2.x, v2.y, v2.z);
           RTri T;
           if (r_setup(A, B, C, T)) {
-            const int cc0 = max(T.c0, tx0), cc1 = min(T.c1, tx1);
-            const int rr0 = max(T.r0, ty0), rr1 = min(T.r1, ty1);
             uint32_t* dep = s_dep[r];
-            for (int row = rr0; row <= rr1; ++row)
-              for (int col = cc0; col <= cc1; ++col) {
-                float z;
-                if (r_fragment(T, col, row, z))
-                  atomicMin(&dep[(row - ty0) * kTileW + (col - tx0)], __float_as_uint(z));
-              }
+            r_raster(T, max(T.c0, tx0), min(T.c1, tx1), max(T.r0, ty0), min(T.r1, ty1),
+                     [&](int col, int row, float q) {
+                       atomicMax(&dep[(row - ty0) * kTileW + (col - tx0)], __float_as_uint(q));
+                     });
           }
         }
       }
@@ -199,16 +199,16 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
       for (int p = tid; p < kTileW * kTileH; p += kVsdThreads) {
         const int row = ty0 + p / kTileW, col = tx0 + p % kTileW;
         if (row > ty1 || col > tx1) continue;
-        const uint32_t ue = s_dep[0][p], ug = s_dep[1][p];
-        if (ue == kInfBits && ug == kInfBits) continue;
-        const float de = ue == kInfBits ? 0.0f : __uint_as_float(ue);
-        const float dg = ug == kInfBits ? 0.0f : __uint_as_float(ug);
+        const uint32_t qe = s_dep[0][p], qg = s_dep[1][p];
+        if ((qe | qg) == 0u) continue;  // neither pose covers this pixel
+        const float de = qe ? 1.0f / __uint_as_float(qe) : 0.0f;
+        const float dg = qg ? 1.0f / __uint_as_float(qg) : 0.0f;
         const float dtest = frame[(int64_t)row * W + col];
-        const double pX = ((double)col - cx) / fx;
-        const double pY = ((double)row - cy) / fy;
+        const double pX = s_pX[p % kTileW];
+        const double pY = s_pY[p / kTileW];
         const double dist_t = dist_of(pX, pY, dtest);
-        const double dist_g = dist_of(pX, pY, dg);
-        const double dist_e = dist_of(pX, pY, de);
+        const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
+        const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
         const bool vg = visib19(dist_t, dist_g, a.delta32, a.delta_f64, a.delta64);
         bool ve = visib19(dist_t, dist_e, a.delta32, a.delta_f64, a.delta64);
         ve = ve || (vg && dist_e > 0.0);  // visibility.py:74
@@ -235,6 +235,7 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
   }
 
   // 4. workgroup reduction (fixed order) and the error formula (pose_error.py:75-91).
+  __syncthreads();  // s_cnt / s_lin alias the depth tiles
   c_union = wave_sum_u32(c_union);
   c_inter = wave_sum_u32(c_inter);
 #pragma unroll
@@ -408,14 +409,18 @@ hipError_t launch_visib(int64_t n, const double* dt, const double* dm, const uin
 
 // ---------------------------------------------------------------------------
 // Batched full-frame renderer: one thread per (instance, triangle), global
-// atomicMin z-buffer. Frames are +inf-filled first and background-mapped after.
+// atomicMax q-buffer (max 1/Z). Frames are zero-filled first and converted to
+// depth after.
+// Frames hold the q-buffer (max 1/Z, 0 = empty) while instances are composited;
+// to_background = 1 converts it in place to depth = 1.0f / q (0 stays 0).
 __global__ void k_depth_fill(uint32_t* __restrict__ f, int64_t n, int to_background) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (to_background) {
-    if (f[i] == kInfBits) f[i] = 0u;
+    const uint32_t q = f[i];
+    f[i] = q ? __float_as_uint(1.0f / __uint_as_float(q)) : 0u;
   } else {
-    f[i] = kInfBits;
+    f[i] = 0u;
   }
 }
 
@@ -454,13 +459,11 @@ __global__ __launch_bounds__(256) void k_render_batch(const ObjDesc* __restrict_
   if (!r_setup(r_vertex(s_pose, c, v0.x, v0.y, v0.z), r_vertex(s_pose, c, v1.x, v1.y, v1.z),
                r_vertex(s_pose, c, v2.x, v2.y, v2.z), T))
     return;
-  const int c0 = max(T.c0, 0), c1 = min(T.c1, W - 1), r0 = max(T.r0, 0), r1 = min(T.r1, H - 1);
   uint32_t* fr = frames + f * (int64_t)W * H;
-  for (int row = r0; row <= r1; ++row)
-    for (int col = c0; col <= c1; ++col) {
-      float z;
-      if (r_fragment(T, col, row, z)) atomicMin(&fr[(int64_t)row * W + col], __float_as_uint(z));
-    }
+  r_raster(T, max(T.c0, 0), min(T.c1, W - 1), max(T.r0, 0), min(T.r1, H - 1),
+           [&](int col, int row, float q) {
+             atomicMax(&fr[(int64_t)row * W + col], __float_as_uint(q));
+           });
 }
 
 hipError_t launch_render_batch(const ObjDesc* objs, int max_nf, int64_t n, const int32_t* slots,

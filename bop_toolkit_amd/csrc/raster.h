@@ -2,16 +2,22 @@
 //
 // Replaces the OpenGL depth pass of renderer_vispy.py:433-538 /
 // renderer_py.py:422-555 (eye-Z depth, pixel-centre sampling, no culling,
-// GL_LESS z-test, background 0). The arithmetic follows the raster spec of
+// GL_LESS z-test, background 0). The arithmetic follows raster spec v2 of
 // DESIGN.md §4 exactly, so results are bit-identical to the CPU twin
 // (oracle/bopx_oracle.c: oracle_render_depth) whatever the tiling, culling or
 // triangle order:
-//   * vertex: float32, no FMA contraction (built with -ffp-contract=off);
-//   * snap to 1/256 px with round-half-even (v_rndne_f32);
-//   * exact int64 edge functions with the top-left fill rule (watertight:
-//     a pixel centre on a shared edge belongs to exactly one triangle);
-//   * depth = area / ((w0/Z0 + w1/Z1) + w2/Z2) in float64 -> float32, combined
-//     with an order-independent unsigned atomicMin on the positive-float bits.
+//   * vertex: float32, no FMA contraction (built with -ffp-contract=off),
+//     snapped to 1/256 px with round-half-even (v_rndne_f32), iz = 1/Z;
+//   * exact integer edge functions with the top-left fill rule (watertight:
+//     a pixel centre on a shared edge belongs to exactly one triangle).
+//     Triangles whose fixed-point extent is < 2^15 (128 px) step their edge
+//     functions incrementally in int32 (|E| < 2^31 is guaranteed there); larger
+//     ones evaluate them directly in int64 — the same integers either way;
+//   * 1/Z is affine in screen space: q = (iz0 + ga*dx) + gb*dy in float32 per
+//     fragment (gradients set up once per triangle in float64);
+//   * the z-buffer keeps max q with an order-independent unsigned atomicMax on
+//     the positive-float bits; depth = 1.0f / q_max (= min of the per-fragment
+//     depths, RN(1/x) being monotone). 0 bits = no fragment = background.
 #pragma once
 #include "bopx_internal.h"
 
@@ -23,7 +29,7 @@ struct Cam32 {
 
 struct RVtx {
   int32_t U, V;
-  float Z;
+  float iz;
   bool ok;
 };
 
@@ -32,90 +38,134 @@ struct RVtx {
 __device__ __forceinline__ RVtx r_vertex(const float* __restrict__ Rf, const Cam32& c,
                                          float x, float y, float z) {
   RVtx o;
-  float X = ((Rf[0] * x + Rf[1] * y) + Rf[2] * z) + Rf[9];
-  float Y = ((Rf[3] * x + Rf[4] * y) + Rf[5] * z) + Rf[10];
-  float Z = ((Rf[6] * x + Rf[7] * y) + Rf[8] * z) + Rf[11];
-  o.Z = Z;
+  const float X = ((Rf[0] * x + Rf[1] * y) + Rf[2] * z) + Rf[9];
+  const float Y = ((Rf[3] * x + Rf[4] * y) + Rf[5] * z) + Rf[10];
+  const float Z = ((Rf[6] * x + Rf[7] * y) + Rf[8] * z) + Rf[11];
   o.U = 0;
   o.V = 0;
+  o.iz = 0.0f;
   o.ok = false;
   if (!(Z > 0.0f)) return o;
-  float u = (c.fx * X) / Z + c.cx;
-  float v = (c.fy * Y) / Z + c.cy;
+  const float u = (c.fx * X) / Z + c.cx;
+  const float v = (c.fy * Y) / Z + c.cy;
   if (!(fabsf(u) <= kGuardBand) || !(fabsf(v) <= kGuardBand)) return o;
   o.U = (int32_t)__builtin_rintf(u * 256.0f);
   o.V = (int32_t)__builtin_rintf(v * 256.0f);
+  o.iz = 1.0f / Z;
   o.ok = true;
   return o;
-}
-
-__device__ __forceinline__ int64_t r_edge(int32_t aU, int32_t aV, int32_t bU, int32_t bV,
-                                          int64_t px, int64_t py) {
-  return (int64_t)(bU - aU) * (py - aV) - (int64_t)(bV - aV) * (px - aU);
-}
-
-__device__ __forceinline__ bool r_top_left(int32_t aU, int32_t aV, int32_t bU, int32_t bV) {
-  int32_t dx = bU - aU, dy = bV - aV;
-  return dy < 0 || (dy == 0 && dx > 0);
 }
 
 __device__ __forceinline__ int64_t r_floor_div256(int64_t a) {
   return a >= 0 ? a / 256 : -((-a + 255) / 256);
 }
 
-// A set-up triangle: vertices ordered so that area > 0.
+// A set-up triangle: vertices ordered so that area > 0; edge k is the edge
+// opposite vertex k (k=0: b->c, 1: c->a, 2: a->b), E_k(P) = dU*(Py-Vs) - dV*(Px-Us).
 struct RTri {
-  int32_t U0, V0, U1, V1, U2, V2;
-  int64_t area;
-  double iz0, iz1, iz2;
-  bool tl0, tl1, tl2;
-  int32_t c0, c1, r0, r1;  // pixel bbox (unclipped against any tile)
+  int32_t U0, V0;           // vertex a (reference point of the 1/Z plane)
+  float iz0, ga, gb;        // 1/Z plane
+  int32_t Us[3], Vs[3];     // edge start vertices
+  int32_t dU[3], dV[3];     // edge vectors
+  int32_t tl[3];            // top-left bias (1 = edge owns its centres)
+  int32_t c0, c1, r0, r1;   // pixel bbox (unclipped)
+  bool small;               // int32 incremental path is exact
 };
 
-// Returns false for triangles that produce no fragments (invalid vertex, zero area).
 __device__ __forceinline__ bool r_setup(RVtx a, RVtx b, RVtx c, RTri& t) {
   if (!(a.ok && b.ok && c.ok)) return false;
-  int64_t area = r_edge(a.U, a.V, b.U, b.V, c.U, c.V);
+  int64_t area = (int64_t)(b.U - a.U) * (c.V - a.V) - (int64_t)(b.V - a.V) * (c.U - a.U);
   if (area == 0) return false;
   if (area < 0) {
-    RVtx tmp = b;
+    const RVtx tmp = b;
     b = c;
     c = tmp;
     area = -area;
   }
-  t.U0 = a.U; t.V0 = a.V; t.U1 = b.U; t.V1 = b.V; t.U2 = c.U; t.V2 = c.V;
-  t.area = area;
-  t.iz0 = 1.0 / (double)a.Z;
-  t.iz1 = 1.0 / (double)b.Z;
-  t.iz2 = 1.0 / (double)c.Z;
-  t.tl0 = r_top_left(b.U, b.V, c.U, c.V);
-  t.tl1 = r_top_left(c.U, c.V, a.U, a.V);
-  t.tl2 = r_top_left(a.U, a.V, b.U, b.V);
-  int32_t minU = min(a.U, min(b.U, c.U)), maxU = max(a.U, max(b.U, c.U));
-  int32_t minV = min(a.V, min(b.V, c.V)), maxV = max(a.V, max(b.V, c.V));
+  const double na = ((double)(b.V - c.V) * (double)a.iz + (double)(c.V - a.V) * (double)b.iz) +
+                    (double)(a.V - b.V) * (double)c.iz;
+  const double nb = ((double)(c.U - b.U) * (double)a.iz + (double)(a.U - c.U) * (double)b.iz) +
+                    (double)(b.U - a.U) * (double)c.iz;
+  t.ga = (float)(na / (double)area);
+  t.gb = (float)(nb / (double)area);
+  t.U0 = a.U;
+  t.V0 = a.V;
+  t.iz0 = a.iz;
+  const RVtx s[3] = {b, c, a}, e[3] = {c, a, b};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    t.Us[k] = s[k].U;
+    t.Vs[k] = s[k].V;
+    t.dU[k] = e[k].U - s[k].U;
+    t.dV[k] = e[k].V - s[k].V;
+    t.tl[k] = (t.dV[k] < 0 || (t.dV[k] == 0 && t.dU[k] > 0)) ? 1 : 0;
+  }
+  const int32_t minU = min(a.U, min(b.U, c.U)), maxU = max(a.U, max(b.U, c.U));
+  const int32_t minV = min(a.V, min(b.V, c.V)), maxV = max(a.V, max(b.V, c.V));
   t.c0 = (int32_t)(-r_floor_div256(-((int64_t)minU - 128)));
   t.c1 = (int32_t)r_floor_div256((int64_t)maxU - 128);
   t.r0 = (int32_t)(-r_floor_div256(-((int64_t)minV - 128)));
   t.r1 = (int32_t)r_floor_div256((int64_t)maxV - 128);
+  t.small = (maxU - minU) < 32768 && (maxV - minV) < 32768;
   return true;
 }
 
-// Fragment test + depth at pixel (col, row). Returns +inf bits when not covered.
-__device__ __forceinline__ bool r_fragment(const RTri& t, int32_t col, int32_t row, float& z) {
-  int64_t px = 256 * (int64_t)col + 128, py = 256 * (int64_t)row + 128;
-  int64_t w0 = r_edge(t.U1, t.V1, t.U2, t.V2, px, py);
-  int64_t w1 = r_edge(t.U2, t.V2, t.U0, t.V0, px, py);
-  int64_t w2 = r_edge(t.U0, t.V0, t.U1, t.V1, px, py);
-  bool in = (w0 > 0 || (w0 == 0 && t.tl0)) && (w1 > 0 || (w1 == 0 && t.tl1)) &&
-            (w2 > 0 || (w2 == 0 && t.tl2));
-  if (!in) return false;
-  double den = ((double)w0 * t.iz0 + (double)w1 * t.iz1) + (double)w2 * t.iz2;
-  z = (float)((double)t.area / den);
-  return true;
+__device__ __forceinline__ float r_q(const RTri& t, int32_t px, int32_t py) {
+  return (t.iz0 + t.ga * (float)(px - t.U0)) + t.gb * (float)(py - t.V0);
 }
 
-__device__ __forceinline__ void load_pose32(const double* __restrict__ p, float* Rf) {
-  for (int i = 0; i < 12; ++i) Rf[i] = (float)p[i];
+// Visit every fragment of t inside the pixel rectangle [cc0,cc1] x [rr0,rr1]
+// (already clipped to the triangle bbox); plot(col, row, q) with q > 0.
+template <class Plot>
+__device__ __forceinline__ void r_raster(const RTri& t, int cc0, int cc1, int rr0, int rr1,
+                                         Plot plot) {
+  if (cc0 > cc1 || rr0 > rr1) return;
+  const int32_t px0 = 256 * cc0 + 128, py0 = 256 * rr0 + 128;
+  if (t.small) {
+    // uint32 wrap-around arithmetic: exact at every visited pixel (|E| < 2^31),
+    // and well-defined one step past the rectangle where the value is unused.
+    uint32_t er[3], sx[3], sy[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      er[k] = (uint32_t)t.dU[k] * (uint32_t)(py0 - t.Vs[k]) -
+              (uint32_t)t.dV[k] * (uint32_t)(px0 - t.Us[k]) + (uint32_t)t.tl[k];
+      sx[k] = (uint32_t)(-256 * t.dV[k]);
+      sy[k] = (uint32_t)(256 * t.dU[k]);
+    }
+    int32_t py = py0;
+    for (int row = rr0; row <= rr1; ++row, py += 256) {
+      uint32_t e0 = er[0], e1 = er[1], e2 = er[2];
+      int32_t px = px0;
+      for (int col = cc0; col <= cc1; ++col, px += 256) {
+        if (((int32_t)e0 > 0) & ((int32_t)e1 > 0) & ((int32_t)e2 > 0)) {
+          const float q = r_q(t, px, py);
+          if (q > 0.0f) plot(col, row, q);
+        }
+        e0 += sx[0];
+        e1 += sx[1];
+        e2 += sx[2];
+      }
+      er[0] += sy[0];
+      er[1] += sy[1];
+      er[2] += sy[2];
+    }
+  } else {
+    for (int row = rr0; row <= rr1; ++row) {
+      const int64_t py = 256 * (int64_t)row + 128;
+      for (int col = cc0; col <= cc1; ++col) {
+        const int64_t px = 256 * (int64_t)col + 128;
+        bool in = true;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          in = in && ((int64_t)t.dU[k] * (py - t.Vs[k]) - (int64_t)t.dV[k] * (px - t.Us[k]) +
+                      t.tl[k]) > 0;
+        if (in) {
+          const float q = r_q(t, (int32_t)px, (int32_t)py);
+          if (q > 0.0f) plot(col, row, q);
+        }
+      }
+    }
+  }
 }
 
 }  // namespace bopx

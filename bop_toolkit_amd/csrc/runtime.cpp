@@ -80,7 +80,9 @@ int set_dev(bopx_ctx* c) {
   return BOPX_OK;
 }
 
-hipStream_t pick_stream(bopx_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+// *_dev calls run on exactly the stream they are given; NULL is the null
+// (default) stream, as for any HIP API -- never the context's private stream.
+hipStream_t pick_stream(bopx_ctx*, void* s) { return (hipStream_t)s; }
 
 // Grow-only scratch; one allocation serves a whole host-buffer call.
 int ws_reserve(bopx_ctx* c, size_t bytes) {

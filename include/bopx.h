@@ -24,7 +24,7 @@
  *  - *_batch functions take caller-owned HOST buffers that are borrowed for the
  *    duration of the call (copied to HBM, computed, copied back, synchronised).
  *  - *_dev functions take DEVICE pointers, enqueue on `stream` (a hipStream_t;
- *    NULL = the context's own stream) and return without synchronising. Object
+ *    NULL = the null/default stream) and return without synchronising. Object
  *    references in *_dev calls are slots from bopx_object_slot(), not obj_ids.
  *  - One context per device per host thread; a context is not thread-safe
  *    (like the reference's singleton GL context, renderer_vispy.py:235-246).

@@ -258,20 +258,25 @@ int oracle_vsd_depths(int W, int H, const float* depth_test, const float* depth_
 }
 
 /* ------------------------------------------------------------ depth raster */
-/* Spec:
+/* Spec v2:
  *  - R, t, fx, fy, cx, cy rounded to float32 (GL uniforms, renderer_vispy.py:441-442);
  *    vertices float32 (renderer_vispy.py:373).
  *  - X = ((r0*x + r1*y) + r2*z) + t, float32, no FMA; valid iff Z > 0.
  *  - u = (fx*X)/Z + cx, v = (fy*Y)/Z + cy (float32); valid iff |u|,|v| <= 16384.
- *  - Snap to 1/256 px: U = rint(u*256), V = rint(v*256).
+ *  - Snap to 1/256 px: U = rint(u*256), V = rint(v*256); iz = 1.0f / Z (float32).
  *  - Pixel (c, r) samples (256c+128, 256r+128) (= pixel centre (c+0.5, r+0.5)).
  *  - Integer edge functions, top-left fill rule, both windings (no culling).
- *  - Depth = area / ((w0/Z0 + w1/Z1) + w2/Z2) in float64, rounded to float32;
- *    nearest wins; background 0.
+ *  - 1/Z is affine in screen space: per triangle (vertices a, b, c with area > 0)
+ *      ga = (float)(((dVbc*iz_a + dVca*iz_b) + dVab*iz_c) / area)   [float64 setup]
+ *      gb = (float)(((dUcb*iz_a + dUac*iz_b) + dUba*iz_c) / area)
+ *    and per fragment  q = (iz_a + ga*(float)(px - Ua)) + gb*(float)(py - Va)  [float32];
+ *    fragments with q <= 0 are dropped.
+ *  - z-test: keep the largest q per pixel; depth = 1.0f / q_max (float32), 0 = background.
+ *    Since RN(1/x) is monotone, this equals min over fragments of RN(1/q).
  * The HIP rasteriser (bop_toolkit_amd/csrc/raster.h) must match this bit for bit. */
 typedef struct {
   int32_t U, V;
-  double iz;
+  float iz;
   int ok;
 } ovtx;
 
@@ -283,14 +288,14 @@ static ovtx oracle_vertex(const float* Rf, const float* tf, float fx, float fy, 
   float Z = ((Rf[6] * p[0] + Rf[7] * p[1]) + Rf[8] * p[2]) + tf[2];
   o.ok = 0;
   o.U = o.V = 0;
-  o.iz = 0.0;
+  o.iz = 0.0f;
   if (!(Z > 0.0f)) return o;
   float u = (fx * X) / Z + cx;
   float v = (fy * Y) / Z + cy;
   if (!(fabsf(u) <= 16384.0f) || !(fabsf(v) <= 16384.0f)) return o;
   o.U = (int32_t)rintf(u * 256.0f);
   o.V = (int32_t)rintf(v * 256.0f);
-  o.iz = 1.0 / (double)Z;
+  o.iz = 1.0f / Z;
   o.ok = 1;
   return o;
 }
@@ -306,6 +311,47 @@ static int top_left(const ovtx* a, const ovtx* b) {
   return dy < 0 || (dy == 0 && dx > 0);
 }
 
+/* Rasterise into q-buffer `qbuf` (largest 1/Z per pixel, 0 = empty). */
+static void raster_tri(ovtx a, ovtx b, ovtx c, int W, int H, float* qbuf) {
+  if (!a.ok || !b.ok || !c.ok) return;
+  int64_t area = edge(&a, &b, c.U, c.V);
+  if (area == 0) return;
+  if (area < 0) {
+    ovtx tmp = b;
+    b = c;
+    c = tmp;
+    area = -area;
+  }
+  double na = ((double)(b.V - c.V) * a.iz + (double)(c.V - a.V) * b.iz) + (double)(a.V - b.V) * c.iz;
+  double nb = ((double)(c.U - b.U) * a.iz + (double)(a.U - c.U) * b.iz) + (double)(b.U - a.U) * c.iz;
+  float ga = (float)(na / (double)area), gb = (float)(nb / (double)area);
+  int32_t minU = a.U < b.U ? (a.U < c.U ? a.U : c.U) : (b.U < c.U ? b.U : c.U);
+  int32_t maxU = a.U > b.U ? (a.U > c.U ? a.U : c.U) : (b.U > c.U ? b.U : c.U);
+  int32_t minV = a.V < b.V ? (a.V < c.V ? a.V : c.V) : (b.V < c.V ? b.V : c.V);
+  int32_t maxV = a.V > b.V ? (a.V > c.V ? a.V : c.V) : (b.V > c.V ? b.V : c.V);
+  /* pixel c covers centre 256c+128: c in [ceil((minU-128)/256), floor((maxU-128)/256)] */
+  int64_t c0 = -floor_div256(-((int64_t)minU - 128)), c1 = floor_div256((int64_t)maxU - 128);
+  int64_t r0 = -floor_div256(-((int64_t)minV - 128)), r1 = floor_div256((int64_t)maxV - 128);
+  if (c0 < 0) c0 = 0;
+  if (r0 < 0) r0 = 0;
+  if (c1 > W - 1) c1 = W - 1;
+  if (r1 > H - 1) r1 = H - 1;
+  int tl0 = top_left(&b, &c), tl1 = top_left(&c, &a), tl2 = top_left(&a, &b);
+  for (int64_t r = r0; r <= r1; ++r) {
+    int64_t py = 256 * r + 128;
+    for (int64_t col = c0; col <= c1; ++col) {
+      int64_t px = 256 * col + 128;
+      int64_t w0 = edge(&b, &c, px, py), w1 = edge(&c, &a, px, py), w2 = edge(&a, &b, px, py);
+      if (!(w0 > 0 || (w0 == 0 && tl0))) continue;
+      if (!(w1 > 0 || (w1 == 0 && tl1))) continue;
+      if (!(w2 > 0 || (w2 == 0 && tl2))) continue;
+      float q = (a.iz + ga * (float)(px - a.U)) + gb * (float)(py - a.V);
+      float* o = qbuf + (size_t)r * W + col;
+      if (q > *o) *o = q;
+    }
+  }
+}
+
 void oracle_render_depth(const double* pts, int64_t nv, const uint32_t* faces, int64_t nf,
                          const double* R, const double* t, double fx, double fy, double cx,
                          double cy, int W, int H, float* out) {
@@ -318,49 +364,14 @@ void oracle_render_depth(const double* pts, int64_t nv, const uint32_t* faces, i
     float p[3] = {(float)pts[3 * v], (float)pts[3 * v + 1], (float)pts[3 * v + 2]};
     vt[v] = oracle_vertex(Rf, tf, fxf, fyf, cxf, cyf, p);
   }
-  for (size_t i = 0; i < (size_t)W * H; ++i) out[i] = INFINITY;
+  memset(out, 0, sizeof(float) * (size_t)W * H);
   for (int64_t f = 0; f < nf; ++f) {
     uint32_t i0 = faces[3 * f], i1 = faces[3 * f + 1], i2 = faces[3 * f + 2];
     if (i0 >= nv || i1 >= nv || i2 >= nv) continue;
-    ovtx a = vt[i0], b = vt[i1], c = vt[i2];
-    if (!a.ok || !b.ok || !c.ok) continue;
-    int64_t area = edge(&a, &b, c.U, c.V);
-    if (area == 0) continue;
-    if (area < 0) {
-      ovtx tmp = b;
-      b = c;
-      c = tmp;
-      area = -area;
-    }
-    int32_t minU = a.U < b.U ? (a.U < c.U ? a.U : c.U) : (b.U < c.U ? b.U : c.U);
-    int32_t maxU = a.U > b.U ? (a.U > c.U ? a.U : c.U) : (b.U > c.U ? b.U : c.U);
-    int32_t minV = a.V < b.V ? (a.V < c.V ? a.V : c.V) : (b.V < c.V ? b.V : c.V);
-    int32_t maxV = a.V > b.V ? (a.V > c.V ? a.V : c.V) : (b.V > c.V ? b.V : c.V);
-    /* pixel c covers centre 256c+128: c in [ceil((minU-128)/256), floor((maxU-128)/256)] */
-    int64_t c0 = -floor_div256(-((int64_t)minU - 128)), c1 = floor_div256((int64_t)maxU - 128);
-    int64_t r0 = -floor_div256(-((int64_t)minV - 128)), r1 = floor_div256((int64_t)maxV - 128);
-    if (c0 < 0) c0 = 0;
-    if (r0 < 0) r0 = 0;
-    if (c1 > W - 1) c1 = W - 1;
-    if (r1 > H - 1) r1 = H - 1;
-    int tl0 = top_left(&b, &c), tl1 = top_left(&c, &a), tl2 = top_left(&a, &b);
-    for (int64_t r = r0; r <= r1; ++r) {
-      int64_t py = 256 * r + 128;
-      for (int64_t col = c0; col <= c1; ++col) {
-        int64_t px = 256 * col + 128;
-        int64_t w0 = edge(&b, &c, px, py), w1 = edge(&c, &a, px, py), w2 = edge(&a, &b, px, py);
-        if (!(w0 > 0 || (w0 == 0 && tl0))) continue;
-        if (!(w1 > 0 || (w1 == 0 && tl1))) continue;
-        if (!(w2 > 0 || (w2 == 0 && tl2))) continue;
-        double den = ((double)w0 * a.iz + (double)w1 * b.iz) + (double)w2 * c.iz;
-        float z = (float)((double)area / den);
-        float* o = out + (size_t)r * W + col;
-        if (z < *o) *o = z;
-      }
-    }
+    raster_tri(vt[i0], vt[i1], vt[i2], W, H, out);
   }
   for (size_t i = 0; i < (size_t)W * H; ++i)
-    if (out[i] == INFINITY) out[i] = 0.0f;
+    if (out[i] > 0.0f) out[i] = 1.0f / out[i];
   free(vt);
 }
 

@@ -30,7 +30,10 @@ def test_fronto_parallel_quad_exact(oracle_mod):
   pts, faces = grid_plane(1, 20.0)
   d = oracle_mod.render_depth(pts, faces, I3, np.array([0.0, 0.0, 1000.0]), FX, FY, CX, CY, W, H)
   cov = d > 0
-  assert np.all(d[cov] == np.float32(1000.0))
+  # constant 1/Z plane: q = 1.0f/1000 exactly, depth = 1.0f/q (spec v2, 1 ulp of 1000)
+  one = np.float32(1.0)
+  assert np.all(d[cov] == one / (one / np.float32(1000.0)))
+  assert np.all(np.abs(d[cov] - 1000.0) <= 1e-4)
   # covered pixel centres: |c + 0.5 - CX| * 1000 / FX < 20 (edges not on centres here)
   c = np.arange(W) + 0.5
   r = np.arange(H) + 0.5
