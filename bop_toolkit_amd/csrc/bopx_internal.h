@@ -16,18 +16,30 @@
 namespace bopx {
 
 constexpr int kMeshletTris = 64;    // one wave lane per triangle
-constexpr int kMaxMeshlets = 1024;  // per object => <= 65,536 triangles for VSD
+constexpr int kMeshletVerts = 128;  // unique vertices per meshlet (LDS staging)
+#ifndef BOPX_MAX_MESHLETS
+#define BOPX_MAX_MESHLETS 1024
+#endif
+#ifndef BOPX_TILE_W
+#define BOPX_TILE_W 64
+#define BOPX_TILE_H 64
+#endif
+constexpr int kMaxMeshlets = BOPX_MAX_MESHLETS;  // per object (VSD)
 constexpr int kMaxTaus = 16;
-constexpr int kTileW = 64;          // VSD screen tile (LDS-resident depth pair)
-constexpr int kTileH = 64;
+constexpr int kTileW = BOPX_TILE_W;  // VSD screen tile (LDS-resident q pair)
+constexpr int kTileH = BOPX_TILE_H;
 constexpr float kGuardBand = 16384.0f;  // |u|,|v| limit of a rasterised vertex (px)
 
 struct ObjDesc {
-  const double* pts;      // 3*nv, SoA
-  const float4* vtx;      // nv
-  const uint32_t* faces;  // 3*nf (meshlet order)
-  const float* mlet;      // 8*nm
-  const double* syms;     // 12*ns
+  const double* pts;         // 3*nv, SoA
+  const float4* vtx;         // nv
+  const uint32_t* faces;     // 3*nf (meshlet order)
+  const float* mlet;         // 8*nm: object-space AABB per meshlet
+  const int4* mlet_info;     // nm: {first triangle, #triangles, first vertex, #vertices}
+  const float4* mlet_vtx;    // meshlet-local vertex blocks (vertices shared by
+                             // neighbouring meshlets are duplicated)
+  const uint32_t* mlet_tri;  // nf: local vertex indices a | b << 8 | c << 16
+  const double* syms;        // 12*ns
   int nv, nf, nm, ns;
 };
 
@@ -48,6 +60,7 @@ struct VsdArgs {
   double delta64;
   int n_tau;
   int normalized;
+  int ablate;  // timing-only diagnostics (BOPX_VSD_ABLATE): bit0 skip raster, bit1 skip pixels
   double taus[kMaxTaus];
 };
 
@@ -62,6 +75,7 @@ hipError_t launch_mean_error(int mode, const ObjDesc* objs, int64_t n, const int
 hipError_t launch_adi(const ObjDesc* objs, int64_t n, const int32_t* slots, const double* pe,
                       const double* pg, double* out, hipStream_t s);
 hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s);
+hipError_t read_vsd_stats(unsigned long long* out, int reset);  // diagnostics
 hipError_t launch_vsd_depths(int W, int H, const float* dt, const float* de, const float* dg,
                              double fx, double fy, double cx, double cy, float delta32,
                              int delta_f64, double delta64, const double* taus_host, int n_tau,

@@ -30,6 +30,10 @@ namespace bopx {
 
 constexpr int kVsdThreads = 256;
 
+// Workload counters for the timing diagnostics (BOPX_VSD_ABLATE bit 2). Not
+// part of the C-ABI; read with bopx_debug_vsd_stats.
+__device__ unsigned long long g_vsd_stats[8];
+
 // float64 distance of a float32 depth at pixel (pX, pY) (misc.py:158-161).
 __device__ __forceinline__ double dist_of(double pX, double pY, float depth) {
   const double d = (double)depth;
@@ -90,15 +94,26 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
+// Make LDS written by other lanes of this wave visible (LDS is in order per wave;
+// the fences stop the compiler from moving accesses across).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int kVsdWaves = kVsdThreads / 64;
+constexpr int kRectsPerThread = 2 * kMaxMeshlets / kVsdThreads;
+
 template <int COST>  // 0 = step, 1 = tlinear
 __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
-  __shared__ uint32_t s_dep[2][kTileW * kTileH];
-  __shared__ short4 s_rect[2 * kMaxMeshlets];
+  __shared__ uint32_t s_dep[2][kTileW * kTileH];     // q = 1/Z bits, 0 = empty
+  __shared__ RVtx s_vtx[kVsdWaves][kMeshletVerts];   // per-wave staged meshlet vertices
   __shared__ uint16_t s_list[2 * kMaxMeshlets];
+  __shared__ double s_pX[kTileW], s_pY[kTileH];
   __shared__ float s_pose[2][12];
   __shared__ int s_roi[4];
   __shared__ int s_nlist;
-  __shared__ double s_pX[kTileW], s_pY[kTileH];
   // Final per-wave partial counters reuse the depth tiles (after the tile loop).
   uint32_t(*s_cnt)[2 + kMaxTaus] = reinterpret_cast<uint32_t(*)[2 + kMaxTaus]>(&s_dep[0][0]);
   double(*s_lin)[kMaxTaus] = reinterpret_cast<double(*)[kMaxTaus]>(&s_dep[1][0]);
@@ -106,7 +121,7 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const ObjDesc o = a.objs[a.slots[b]];
-  const int W = a.width, H = a.height, nm = o.nm, nf = o.nf;
+  const int W = a.width, H = a.height, nm = o.nm;
   const int64_t fidx = a.frame_idx[b];
   const float* __restrict__ frame = a.frames + fidx * (int64_t)W * H;
   const double fx = a.cam[4 * fidx + 0], fy = a.cam[4 * fidx + 1];
@@ -126,16 +141,21 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
   }
   __syncthreads();
 
-  // 1. per-pose meshlet rectangles + ROI.
-  for (int i = tid; i < 2 * nm; i += kVsdThreads) {
-    const int r = i >= nm, m = i - r * nm;
-    const short4 rc = meshlet_rect(o.mlet + 8 * (int64_t)m, s_pose[r], c32, W, H);
-    s_rect[i] = rc;
-    if (rc.x <= rc.z && rc.y <= rc.w) {
-      atomicMin(&s_roi[0], (int)rc.x);
-      atomicMin(&s_roi[1], (int)rc.y);
-      atomicMax(&s_roi[2], (int)rc.z);
-      atomicMax(&s_roi[3], (int)rc.w);
+  // 1. per-pose meshlet rectangles (kept in registers: entry tid + 256 j) + ROI.
+  short4 rect[kRectsPerThread];
+#pragma unroll
+  for (int j = 0; j < kRectsPerThread; ++j) {
+    const int i = tid + j * kVsdThreads;
+    rect[j] = make_short4(1, 1, 0, 0);
+    if (i < 2 * nm) {
+      const int r = i >= nm, m = i - r * nm;
+      rect[j] = meshlet_rect(o.mlet + 8 * (int64_t)m, s_pose[r], c32, W, H);
+      if (rect[j].x <= rect[j].z && rect[j].y <= rect[j].w) {
+        atomicMin(&s_roi[0], (int)rect[j].x);
+        atomicMin(&s_roi[1], (int)rect[j].y);
+        atomicMax(&s_roi[2], (int)rect[j].z);
+        atomicMax(&s_roi[3], (int)rect[j].w);
+      }
     }
   }
   __syncthreads();
@@ -152,55 +172,72 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
 
   if (rx0 <= rx1 && ry0 <= ry1) {
     const int ntx = (rx1 - rx0 + kTileW) / kTileW, nty = (ry1 - ry0 + kTileH) / kTileH;
+    if ((a.ablate & 4) && tid == 0) atomicAdd(&g_vsd_stats[0], (unsigned long long)(ntx * nty));
     for (int t = 0; t < ntx * nty; ++t) {
       const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
       const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
-      // 2a. clear both depth tiles, list the meshlets touching the tile.
+      // 2a. clear both q tiles, list the (pose, meshlet) entries touching the tile.
       uint32_t* dep_flat = &s_dep[0][0];
       for (int i = tid; i < 2 * kTileW * kTileH; i += kVsdThreads) dep_flat[i] = 0u;
       if (tid == 0) s_nlist = 0;
       // float64 distance coefficients of the tile's columns / rows (misc.py:137-138)
       if (tid < kTileW) s_pX[tid] = ((double)(tx0 + tid) - cx) / fx;
-      else if (tid < kTileW + kTileH) s_pY[tid - kTileW] = ((double)(ty0 + tid - kTileW) - cy) / fy;
+      if (tid >= kVsdThreads - kTileH)
+        s_pY[tid - (kVsdThreads - kTileH)] = ((double)(ty0 + tid - (kVsdThreads - kTileH)) - cy) / fy;
       __syncthreads();
-      for (int i = tid; i < 2 * nm; i += kVsdThreads) {
-        const short4 rc = s_rect[i];
+#pragma unroll
+      for (int j = 0; j < kRectsPerThread; ++j) {
+        const short4 rc = rect[j];
         if (rc.x <= tx1 && rc.z >= tx0 && rc.y <= ty1 && rc.w >= ty0 && rc.x <= rc.z &&
             rc.y <= rc.w)
-          s_list[atomicAdd(&s_nlist, 1)] = (uint16_t)i;
+          s_list[atomicAdd(&s_nlist, 1)] = (uint16_t)(tid + j * kVsdThreads);
       }
       __syncthreads();
-      // 2b. rasterise: one meshlet per wave step, one triangle per lane.
-      const int nl = s_nlist;
-      for (int li = wave; li < nl; li += kVsdThreads / 64) {
-        const int e = s_list[li];
+      // 2b. rasterise: one meshlet per wave step. The wave transforms the
+      // meshlet's vertex block once (lane = vertex) into LDS, then each lane
+      // sets up and rasterises one triangle from the staged vertices.
+      const int nl = (a.ablate & 1) ? 0 : s_nlist;
+      for (int li = wave; li < nl; li += kVsdWaves) {
+        const int e = __builtin_amdgcn_readfirstlane(s_list[li]);
         const int r = e >= nm, m = e - r * nm;
-        const int tri = m * kMeshletTris + lane;
-        if (tri < nf) {
-          const uint32_t i0 = o.faces[3 * (int64_t)tri], i1 = o.faces[3 * (int64_t)tri + 1],
-                         i2 = o.faces[3 * (int64_t)tri + 2];
-          const float4 v0 = o.vtx[i0], v1 = o.vtx[i1], v2 = o.vtx[i2];
-          const float* Rf = s_pose[r];
-          const RVtx A = r_vertex(Rf, c32, v0.x, v0.y, v0.z);
-          const RVtx B = r_vertex(Rf, c32, v1.x, v1.y, v1.z);
-          const RVtx C = r_vertex(Rf, c32, v2.x, v2.y, v2.z);
+        const int4 info = o.mlet_info[m];
+        const float* Rf = s_pose[r];
+        for (int j = lane; j < info.w; j += 64) {
+          const float4 v = o.mlet_vtx[info.z + j];
+          s_vtx[wave][j] = r_vertex(Rf, c32, v.x, v.y, v.z);
+        }
+        wave_lds_sync();
+        if (lane < info.y) {
+          const uint32_t pk = o.mlet_tri[info.x + lane];
+          const RVtx A = s_vtx[wave][pk & 255u], B = s_vtx[wave][(pk >> 8) & 255u],
+                     C = s_vtx[wave][(pk >> 16) & 255u];
           RTri T;
-          if (r_setup(A, B, C, T)) {
+          if (r_setup(A, B, C, T, tx0, tx1, ty0, ty1)) {
             uint32_t* dep = s_dep[r];
-            r_raster(T, max(T.c0, tx0), min(T.c1, tx1), max(T.r0, ty0), min(T.r1, ty1),
-                     [&](int col, int row, float q) {
-                       atomicMax(&dep[(row - ty0) * kTileW + (col - tx0)], __float_as_uint(q));
-                     });
+            const int cc0 = max(T.c0, tx0), cc1 = min(T.c1, tx1);
+            const int rr0 = max(T.r0, ty0), rr1 = min(T.r1, ty1);
+            if (a.ablate & 4) {
+              const unsigned long long it = (unsigned long long)(cc1 - cc0 + 1) * (rr1 - rr0 + 1);
+              atomicAdd(&g_vsd_stats[2], 1ull);
+              atomicAdd(&g_vsd_stats[3], it);
+            }
+            r_raster(T, cc0, cc1, rr0, rr1, [&](int col, int row, float q) {
+              if (a.ablate & 4) atomicAdd(&g_vsd_stats[5], 1ull);
+              atomicMax(&dep[(row - ty0) * kTileW + (col - tx0)], __float_as_uint(q));
+            });
           }
         }
+        if ((a.ablate & 4) && lane == 0) atomicAdd(&g_vsd_stats[1], 1ull);
+        wave_lds_sync();  // s_vtx is rewritten by the next entry
       }
       __syncthreads();
       // 3. per-pixel distances, visibility masks, counters.
-      for (int p = tid; p < kTileW * kTileH; p += kVsdThreads) {
+      for (int p = tid; p < ((a.ablate & 2) ? 0 : kTileW * kTileH); p += kVsdThreads) {
         const int row = ty0 + p / kTileW, col = tx0 + p % kTileW;
         if (row > ty1 || col > tx1) continue;
         const uint32_t qe = s_dep[0][p], qg = s_dep[1][p];
         if ((qe | qg) == 0u) continue;  // neither pose covers this pixel
+        if (a.ablate & 4) atomicAdd(&g_vsd_stats[6], 1ull);
         const float de = qe ? 1.0f / __uint_as_float(qe) : 0.0f;
         const float dg = qg ? 1.0f / __uint_as_float(qg) : 0.0f;
         const float dtest = frame[(int64_t)row * W + col];
@@ -257,7 +294,7 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
   __syncthreads();
   if (tid == 0) {
     uint64_t un = 0, in = 0;
-    for (int w = 0; w < kVsdThreads / 64; ++w) {
+    for (int w = 0; w < kVsdWaves; ++w) {
       un += s_cnt[w][0];
       in += s_cnt[w][1];
     }
@@ -267,15 +304,23 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
         out[k] = 1.0;
       } else if (COST == 0) {
         uint64_t cnt = 0;
-        for (int w = 0; w < kVsdThreads / 64; ++w) cnt += s_cnt[w][2 + k];
+        for (int w = 0; w < kVsdWaves; ++w) cnt += s_cnt[w][2 + k];
         out[k] = (double)(cnt + (un - in)) / (double)un;
       } else {
         double sum = 0.0;
-        for (int w = 0; w < kVsdThreads / 64; ++w) sum += s_lin[w][k];
+        for (int w = 0; w < kVsdWaves; ++w) sum += s_lin[w][k];
         out[k] = (sum + (double)(un - in)) / (double)un;
       }
     }
   }
+}
+
+
+hipError_t read_vsd_stats(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vsd_stats), sizeof(g_vsd_stats));
+  if (e != hipSuccess || !reset) return e;
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_vsd_stats), z, sizeof(z));
 }
 
 hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s) {
@@ -457,7 +502,7 @@ __global__ __launch_bounds__(256) void k_render_batch(const ObjDesc* __restrict_
                v2 = o.vtx[o.faces[3 * (int64_t)tri + 2]];
   RTri T;
   if (!r_setup(r_vertex(s_pose, c, v0.x, v0.y, v0.z), r_vertex(s_pose, c, v1.x, v1.y, v1.z),
-               r_vertex(s_pose, c, v2.x, v2.y, v2.z), T))
+               r_vertex(s_pose, c, v2.x, v2.y, v2.z), T, 0, W - 1, 0, H - 1))
     return;
   uint32_t* fr = frames + f * (int64_t)W * H;
   r_raster(T, max(T.c0, 0), min(T.c1, W - 1), max(T.r0, 0), min(T.r1, H - 1),

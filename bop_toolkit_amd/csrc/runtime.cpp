@@ -36,6 +36,9 @@ struct Object {
   float4* d_vtx = nullptr;
   uint32_t* d_faces = nullptr;
   float* d_mlet = nullptr;
+  int4* d_minfo = nullptr;
+  float4* d_mvtx = nullptr;
+  uint32_t* d_mtri = nullptr;
   double* d_syms = nullptr;
 };
 
@@ -128,6 +131,9 @@ int sync_desc(bopx_ctx* c) {
       d.vtx = o.d_vtx;
       d.faces = o.d_faces;
       d.mlet = o.d_mlet;
+      d.mlet_info = o.d_minfo;
+      d.mlet_vtx = o.d_mvtx;
+      d.mlet_tri = o.d_mtri;
       d.syms = o.d_syms;
       d.nv = (int)o.nv;
       d.nf = (int)o.nf;
@@ -156,6 +162,9 @@ void free_object(Object& o) {
   if (o.d_vtx) (void)hipFree(o.d_vtx);
   if (o.d_faces) (void)hipFree(o.d_faces);
   if (o.d_mlet) (void)hipFree(o.d_mlet);
+  if (o.d_minfo) (void)hipFree(o.d_minfo);
+  if (o.d_mvtx) (void)hipFree(o.d_mvtx);
+  if (o.d_mtri) (void)hipFree(o.d_mtri);
   if (o.d_syms) (void)hipFree(o.d_syms);
   o = Object();
 }
@@ -299,8 +308,10 @@ int bopx_add_object(bopx_ctx* c, int obj_id, const double* pts, int64_t nv,
   for (int64_t v = 0; v < nv; ++v)
     vtx[v] = make_float4((float)pts[3 * v], (float)pts[3 * v + 1], (float)pts[3 * v + 2], 0.f);
   // Meshlets: triangles sorted by the Morton code of their centroid, 64 per meshlet.
-  std::vector<uint32_t> fsorted;
+  std::vector<uint32_t> fsorted, mtri;
   std::vector<float> mlet;
+  std::vector<int4> minfo;
+  std::vector<float4> mvtx;
   if (nf > 0) {
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int64_t v = 0; v < nv; ++v) {
@@ -325,23 +336,52 @@ int bopx_add_object(bopx_ctx* c, int obj_id, const double* pts, int64_t nv,
     fsorted.resize(3 * (size_t)nf);
     for (int64_t i = 0; i < nf; ++i)
       for (int k = 0; k < 3; ++k) fsorted[3 * i + k] = faces[3 * (size_t)key[i].second + k];
-    o.nm = (nf + bopx::kMeshletTris - 1) / bopx::kMeshletTris;
-    mlet.assign(8 * (size_t)o.nm, 0.f);
-    for (int64_t m = 0; m < o.nm; ++m) {
+    // Greedy meshlets along the Morton order: <= 64 triangles and <= 128 unique
+    // vertices each. Every meshlet carries its own vertex block (what a wave
+    // transforms once and shares through LDS) and 8-bit local indices.
+    std::vector<int32_t> local(nv, -1);
+    std::vector<uint32_t> touched;
+    int64_t f = 0;
+    while (f < nf) {
+      const int32_t tri0 = (int32_t)f, vtx0 = (int32_t)mvtx.size();
+      touched.clear();
       float bl[3] = {INFINITY, INFINITY, INFINITY}, bh[3] = {-INFINITY, -INFINITY, -INFINITY};
-      for (int64_t f = m * bopx::kMeshletTris; f < std::min(nf, (m + 1) * bopx::kMeshletTris); ++f)
+      while (f < nf && f - tri0 < bopx::kMeshletTris) {
+        int fresh = 0;
+        for (int j = 0; j < 3; ++j) fresh += local[fsorted[3 * f + j]] < 0;
+        if ((int)touched.size() + fresh > bopx::kMeshletVerts) break;
+        uint32_t pk = 0;
         for (int j = 0; j < 3; ++j) {
-          const float* p = &vtx[fsorted[3 * f + j]].x;
+          const uint32_t v = fsorted[3 * f + j];
+          if (local[v] < 0) {
+            local[v] = (int32_t)touched.size();
+            touched.push_back(v);
+            mvtx.push_back(vtx[v]);
+          }
+          pk |= (uint32_t)local[v] << (8 * j);
+          const float* p = &vtx[v].x;
           for (int k = 0; k < 3; ++k) bl[k] = std::min(bl[k], p[k]), bh[k] = std::max(bh[k], p[k]);
         }
-      for (int k = 0; k < 3; ++k) mlet[8 * m + k] = bl[k], mlet[8 * m + 4 + k] = bh[k];
+        mtri.push_back(pk);
+        ++f;
+      }
+      for (uint32_t v : touched) local[v] = -1;
+      minfo.push_back(make_int4(tri0, (int32_t)(f - tri0), vtx0, (int32_t)touched.size()));
+      for (int k = 0; k < 3; ++k) mlet.push_back(bl[k]);
+      mlet.push_back(0.f);
+      for (int k = 0; k < 3; ++k) mlet.push_back(bh[k]);
+      mlet.push_back(0.f);
     }
+    o.nm = (int64_t)minfo.size();
   }
   int r;
   if ((r = upload(c, &o.d_pts, soa.data(), soa.size())) ||
       (r = upload(c, &o.d_vtx, vtx.data(), vtx.size())) ||
       (r = upload(c, &o.d_faces, fsorted.data(), fsorted.size())) ||
-      (r = upload(c, &o.d_mlet, mlet.data(), mlet.size()))) {
+      (r = upload(c, &o.d_mlet, mlet.data(), mlet.size())) ||
+      (r = upload(c, &o.d_minfo, minfo.data(), minfo.size())) ||
+      (r = upload(c, &o.d_mvtx, mvtx.data(), mvtx.size())) ||
+      (r = upload(c, &o.d_mtri, mtri.data(), mtri.size()))) {
     free_object(o);
     return r;
   }
@@ -503,6 +543,11 @@ static int fill_vsd_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height, d
   a.delta_f64 = (flags & BOPX_DELTA_F64) ? 1 : 0;
   a.n_tau = n_tau;
   a.normalized = normalized ? 1 : 0;
+  static const int ablate = [] {
+    const char* e = getenv("BOPX_VSD_ABLATE");  // timing diagnostics only
+    return e ? atoi(e) : 0;
+  }();
+  a.ablate = ablate;
   for (int k = 0; k < bopx::kMaxTaus; ++k) a.taus[k] = k < n_tau ? taus[k] : 1.0;
   return BOPX_OK;
 }
@@ -750,6 +795,17 @@ int bopx_visib_mask(bopx_ctx* c, int64_t n, const double* d_test, const double* 
                                (flags & BOPX_DELTA_F64) ? 1 : 0, delta, visib_mode, d_o, s));
   HIPCHK(c, hipMemcpyAsync(out, d_o, n, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
+  return BOPX_OK;
+}
+
+// Diagnostics (not in include/bopx.h): k_vsd workload counters gathered when
+// BOPX_VSD_ABLATE has bit 2 set: tiles, meshlet entries, triangle set-ups,
+// bbox iterations, sum of per-wave max iterations, fragments, covered pixels.
+int bopx_debug_vsd_stats(bopx_ctx* c, unsigned long long* out, int reset) {
+  if (!c || !out) return BOPX_E_INVALID;
+  if (int r = set_dev(c)) return r;
+  HIPCHK(c, hipDeviceSynchronize());
+  HIPCHK(c, bopx::read_vsd_stats(out, reset));
   return BOPX_OK;
 }
 

@@ -266,10 +266,11 @@ int oracle_vsd_depths(int W, int H, const float* depth_test, const float* depth_
  *  - Snap to 1/256 px: U = rint(u*256), V = rint(v*256); iz = 1.0f / Z (float32).
  *  - Pixel (c, r) samples (256c+128, 256r+128) (= pixel centre (c+0.5, r+0.5)).
  *  - Integer edge functions, top-left fill rule, both windings (no culling).
- *  - 1/Z is affine in screen space: per triangle (vertices a, b, c with area > 0)
- *      ga = (float)(((dVbc*iz_a + dVca*iz_b) + dVab*iz_c) / area)   [float64 setup]
- *      gb = (float)(((dUcb*iz_a + dUac*iz_b) + dUba*iz_c) / area)
- *    and per fragment  q = (iz_a + ga*(float)(px - Ua)) + gb*(float)(py - Va)  [float32];
+ *  - 1/Z is affine in screen space: per triangle (vertices a, b, c with area > 0),
+ *    all float32: inv = 1.0f / (float)(double)area, dza = iz_a - iz_c, dzb = iz_b - iz_c,
+ *      ga = ((float)(Vb - Vc)*dza + (float)(Vc - Va)*dzb) * inv
+ *      gb = ((float)(Uc - Ub)*dza + (float)(Ua - Uc)*dzb) * inv
+ *    and per fragment  q = (iz_a + ga*(float)(px - Ua)) + gb*(float)(py - Va);
  *    fragments with q <= 0 are dropped.
  *  - z-test: keep the largest q per pixel; depth = 1.0f / q_max (float32), 0 = background.
  *    Since RN(1/x) is monotone, this equals min over fragments of RN(1/q).
@@ -322,9 +323,10 @@ static void raster_tri(ovtx a, ovtx b, ovtx c, int W, int H, float* qbuf) {
     c = tmp;
     area = -area;
   }
-  double na = ((double)(b.V - c.V) * a.iz + (double)(c.V - a.V) * b.iz) + (double)(a.V - b.V) * c.iz;
-  double nb = ((double)(c.U - b.U) * a.iz + (double)(a.U - c.U) * b.iz) + (double)(b.U - a.U) * c.iz;
-  float ga = (float)(na / (double)area), gb = (float)(nb / (double)area);
+  float inv_area = 1.0f / (float)(double)area;
+  float dza = a.iz - c.iz, dzb = b.iz - c.iz;
+  float ga = ((float)(b.V - c.V) * dza + (float)(c.V - a.V) * dzb) * inv_area;
+  float gb = ((float)(c.U - b.U) * dza + (float)(a.U - c.U) * dzb) * inv_area;
   int32_t minU = a.U < b.U ? (a.U < c.U ? a.U : c.U) : (b.U < c.U ? b.U : c.U);
   int32_t maxU = a.U > b.U ? (a.U > c.U ? a.U : c.U) : (b.U > c.U ? b.U : c.U);
   int32_t minV = a.V < b.V ? (a.V < c.V ? a.V : c.V) : (b.V < c.V ? b.V : c.V);

@@ -1,0 +1,45 @@
+"""Workload counters of one k_vsd launch on the bench workload (diagnostics).
+
+    BOPX_VSD_ABLATE=4 python tools/vsd_stats.py [--tuples N]
+"""
+import ctypes
+import os
+import sys
+
+os.environ.setdefault("BOPX_VSD_ABLATE", "4")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.argv += [] if "--tuples" in sys.argv else ["--tuples", "1200"]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from bop_toolkit_amd.batch import BatchEvaluator  # noqa: E402
+
+
+def main():
+  args = bench.parse()
+  ev = BatchEvaluator(0)
+  objs = bench.build_objects(ev, args, torch)
+  n, d = bench.build_workload(ev, objs, args, 0, torch)
+  fn = ev.ctx.lib.bopx_debug_vsd_stats
+  fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+  st = (ctypes.c_ulonglong * 8)()
+  fn(ev.ctx.h, st, 1)
+  ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"], d["frames"], d["cam"],
+         bench.DELTA, bench.TAUS, d["diameters"])
+  torch.cuda.synchronize()
+  fn(ev.ctx.h, st, 1)
+  names = ["tiles", "meshlet_entries", "tri_setups", "bbox_iters", "wave_max_iters_sum",
+           "fragments", "covered_px"]
+  for i, k in enumerate(names):
+    print("%-20s total %14d  per tuple %12.1f" % (k, st[i], st[i] / n))
+  print("lane efficiency of bbox loops: %.3f" % (st[3] / max(1, 64 * st[4])))
+  roi = bench.roi_pixels(objs, d["host"]["obj"], [d["host"]["pe"], d["host"]["pg"]],
+                         bench.synth_K() if hasattr(bench, "synth_K") else __import__(
+                             "bop_toolkit_amd.synth", fromlist=["YCBV_K"]).YCBV_K)
+  print("bbox-corner ROI mean px %.0f" % np.mean(roi))
+
+
+if __name__ == "__main__":
+  main()
