@@ -1,24 +1,53 @@
-"""Summarise rocprofv3 --pmc counter CSVs: per kernel, mean counter value per dispatch."""
+"""Summarise rocprofv3 --pmc counter CSVs into profiles/<tag>_pmc.json.
+
+    python tools/pmc_summary.py OUT.json DIR [DIR ...]
+
+Per kernel: mean value per dispatch of every counter collected (each DIR is one
+rocprofv3 pass). HBM traffic per launch follows MI355X_MICROARCH.md §HBM:
+FETCH_SIZE and WRITE_SIZE are in KiB (TCC_EA0_RDREQ/_WRREQ based); on gfx950
+FETCH_SIZE under-reports wide (16 B/lane) coalesced streams by 2x and other
+access widths are uncalibrated, so both the raw sum and the 2x-corrected read
+side are recorded, the corrected one being used as `hbm_bytes_per_launch`.
+"""
 import csv
 import glob
+import json
 import os
 import sys
 from collections import defaultdict
 
+SHORT = {"k_vsd<0>": "k_vsd", "k_sym_error<0>": "k_sym_error<MSSD>",
+         "k_sym_error<1>": "k_sym_error<MSPD>"}
 
-def main(dirs):
-  acc = defaultdict(lambda: defaultdict(list))
+
+def short(name):
+  for k, v in SHORT.items():
+    if k in name:
+      return v
+  return name.split("(")[0][-60:]
+
+
+def main(out, dirs):
+  per = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
   for d in dirs:
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
       for row in csv.DictReader(open(path)):
-        name = row.get("Kernel_Name", "?")[:60]
-        acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
-  for k, cs in acc.items():
+        k = short(row.get("Kernel_Name", "?"))
+        per[k][row["Counter_Name"]][row.get("Dispatch_Id", "0")] += float(row["Counter_Value"])
+  res = {}
+  for k, cs in per.items():
+    r = {c: sum(v.values()) / len(v) for c, v in cs.items()}
+    if "FETCH_SIZE" in r and "WRITE_SIZE" in r:
+      r["hbm_bytes_raw_per_launch"] = (r["FETCH_SIZE"] + r["WRITE_SIZE"]) * 1024.0
+      r["hbm_bytes_per_launch"] = (2.0 * r["FETCH_SIZE"] + r["WRITE_SIZE"]) * 1024.0
+    res[k] = r
+  with open(out, "w") as f:
+    json.dump(res, f, indent=1, sort_keys=True)
+  for k, r in res.items():
     print(k)
-    for c, v in sorted(cs.items()):
-      # counters are reported per dispatch and per dimension: sum per dispatch
-      print("   %-28s %16.4g   (n=%d)" % (c, sum(v) / max(1, len(set(range(len(v))))) * len(v) / max(1, len(v)), len(v)))
+    for c, v in sorted(r.items()):
+      print("   %-30s %16.6g" % (c, v))
 
 
 if __name__ == "__main__":
-  main(sys.argv[1:])
+  main(sys.argv[1], sys.argv[2:])
