@@ -228,6 +228,7 @@ def main():
   torch.cuda.set_device(local)
   if world > 1:
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+  from bop_toolkit_amd import shard
   from bop_toolkit_amd.batch import BatchEvaluator
   ev = BatchEvaluator(local)
   objs = build_objects(ev, args, torch)
@@ -237,7 +238,7 @@ def main():
   out_mssd = torch.empty(n, dtype=torch.float64, device=ev.device)
   out_mspd = torch.empty(n, dtype=torch.float64, device=ev.device)
   rows = torch.empty((n, N_TAU + 2), dtype=torch.float64, device=ev.device)
-  gathered = torch.empty((world * n, N_TAU + 2), dtype=torch.float64, device=ev.device)
+  gids = torch.arange(rank * n, (rank + 1) * n, dtype=torch.int64, device=ev.device)
   ktime = {"vsd": 0.0, "mssd": 0.0, "mspd": 0.0}
   marks = []  # per timed step: HIP events bracketing each kernel on the launch stream
 
@@ -256,7 +257,8 @@ def main():
       rows[:, :N_TAU] = out_vsd
       rows[:, N_TAU] = out_mssd
       rows[:, N_TAU + 1] = out_mspd
-      dist.all_gather_into_tensor(gathered, rows)
+      # per-tuple error rows -> rank 0, ordered by global tuple id (RCCL)
+      shard.gather_rows(rows, gids, world * n)
 
   for _ in range(args.warmup):
     step(False)

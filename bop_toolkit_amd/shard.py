@@ -1,0 +1,86 @@
+"""Multi-GPU partitioning of an error-evaluation job.
+
+Tuples are independent (no cross-tuple term in pose_error.*), so the job is
+sharded with no data-path collective: images are assigned to ranks by LPT
+(longest-processing-time-first) bin packing on an estimated cost, each rank
+evaluates its images' tuples on its own GPU, and the per-tuple error rows are
+gathered to rank 0 once at the end (RCCL over xGMI on GPUs, gloo on CPU).
+Images, not scenes, are the unit: LM-O and ITODD have a single test scene
+(dataset_params.py:345,447-451), so scene sharding cannot balance 8 GPUs.
+
+The gathered table is re-ordered by global tuple id, so it is bitwise
+identical to a single-GPU run.
+"""
+import heapq
+
+import numpy as np
+
+
+def tuple_cost(nv, nf, ns, roi_px):
+  """Relative cost of one BOP19 tuple (VSD + MSSD + MSPD), from the per-tuple
+  flop model of SURVEY.md §8d: VSD 40V + 60F + 92 ROI, MSSD V(18 + 28S),
+  MSPD V(20 + 27S)."""
+  nv, nf, ns, roi_px = (np.asarray(x, np.float64) for x in (nv, nf, ns, roi_px))
+  return 40 * nv + 60 * nf + 92 * roi_px + nv * (38 + 55 * ns)
+
+
+def lpt_shard(costs, world):
+  """Assign items (images) to `world` ranks, heaviest first, each to the
+  currently lightest rank (ties -> lowest rank). Returns a list of index
+  arrays, one per rank, each sorted ascending."""
+  costs = np.asarray(costs, np.float64)
+  order = np.argsort(-costs, kind="stable")
+  heap = [(0.0, r) for r in range(world)]
+  heapq.heapify(heap)
+  parts = [[] for _ in range(world)]
+  for i in order:
+    load, r = heapq.heappop(heap)
+    parts[r].append(int(i))
+    heapq.heappush(heap, (load + float(costs[i]), r))
+  return [np.array(sorted(p), dtype=np.int64) for p in parts]
+
+
+def image_costs(frame_of_tuple, per_tuple_cost, n_images):
+  """Sum per-tuple costs into per-image costs."""
+  return np.bincount(np.asarray(frame_of_tuple), weights=per_tuple_cost, minlength=n_images)
+
+
+def gather_rows(rows, ids, n_total, group=None):
+  """Gather per-tuple rows from every rank to rank 0.
+
+  rows: [n_local, C] float64 tensor on this rank's device (or CPU for gloo);
+  ids:  [n_local] int64 tensor of global tuple ids.
+  Returns the [n_total, C] table ordered by global id on rank 0, None elsewhere.
+  One all_gather of the counts, one padded all_gather of [id | row] blocks.
+  """
+  import torch
+  import torch.distributed as dist
+  world = dist.get_world_size(group)
+  rank = dist.get_rank(group)
+  dev = rows.device
+  n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
+  counts = [torch.zeros_like(n) for _ in range(world)]
+  dist.all_gather(counts, n, group=group)
+  counts = [int(c.item()) for c in counts]
+  width = rows.shape[1] + 1
+  pad = max(counts)
+  block = torch.zeros((pad, width), dtype=torch.float64, device=dev)
+  block[:rows.shape[0], 0] = ids.to(torch.float64)
+  block[:rows.shape[0], 1:] = rows
+  out = torch.empty((world * pad, width), dtype=torch.float64, device=dev)
+  if dev.type == "cuda":  # RCCL: one contiguous all-gather
+    dist.all_gather_into_tensor(out, block, group=group)
+  else:  # gloo
+    dist.all_gather(list(out.view(world, pad, width).unbind(0)), block, group=group)
+  if rank != 0:
+    return None
+  table = torch.empty((n_total, rows.shape[1]), dtype=torch.float64, device=dev)
+  filled = torch.zeros(n_total, dtype=torch.bool, device=dev)
+  for r, c in enumerate(counts):
+    seg = out[r * pad:r * pad + c]
+    gid = seg[:, 0].to(torch.int64)
+    table[gid] = seg[:, 1:]
+    filled[gid] = True
+  if not bool(filled.all()):
+    raise RuntimeError("gather_rows: %d tuple rows missing" % int((~filled).sum()))
+  return table
