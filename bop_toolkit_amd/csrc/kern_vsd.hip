@@ -28,7 +28,10 @@
 
 namespace bopx {
 
-constexpr int kVsdThreads = 256;
+#ifndef BOPX_VSD_THREADS
+#define BOPX_VSD_THREADS 512
+#endif
+constexpr int kVsdThreads = BOPX_VSD_THREADS;
 
 // Workload counters for the timing diagnostics (BOPX_VSD_ABLATE bit 2). Not
 // part of the C-ABI; read with bopx_debug_vsd_stats.
@@ -66,7 +69,8 @@ __device__ __forceinline__ short4 meshlet_rect(const float* __restrict__ mb, con
     if (!(Z > 0.0f)) {
       full = true;
     } else {
-      const float u = (c.fx * X) / Z + c.cx, v = (c.fy * Y) / Z + c.cy;
+      const float iz = 1.0f / Z;
+      const float u = (c.fx * X) * iz + c.cx, v = (c.fy * Y) * iz + c.cy;
       umin = fminf(umin, u);
       umax = fmaxf(umax, u);
       vmin = fminf(vmin, v);
@@ -108,7 +112,8 @@ constexpr int kRectsPerThread = 2 * kMaxMeshlets / kVsdThreads;
 template <int COST>  // 0 = step, 1 = tlinear
 __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
   __shared__ uint32_t s_dep[2][kTileW * kTileH];     // q = 1/Z bits, 0 = empty
-  __shared__ RVtx s_vtx[kVsdWaves][kMeshletVerts];   // per-wave staged meshlet vertices
+  // per-wave area: staged meshlet vertices (2 KiB), then triangle records (4 KiB)
+  __shared__ RVtx s_vtx[kVsdWaves][2 * kMeshletVerts];
   __shared__ uint16_t s_list[2 * kMaxMeshlets];
   __shared__ double s_pX[kTileW], s_pY[kTileH];
   __shared__ float s_pose[2][12];
@@ -207,26 +212,48 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
           s_vtx[wave][j] = r_vertex(Rf, c32, v.x, v.y, v.z);
         }
         wave_lds_sync();
+        RTri T;
+        bool act = false;
+        int cc0 = 0, cc1 = -1, rr0 = 0, rr1 = -1;
         if (lane < info.y) {
           const uint32_t pk = o.mlet_tri[info.x + lane];
           const RVtx A = s_vtx[wave][pk & 255u], B = s_vtx[wave][(pk >> 8) & 255u],
                      C = s_vtx[wave][(pk >> 16) & 255u];
-          RTri T;
           if (r_setup(A, B, C, T, tx0, tx1, ty0, ty1)) {
-            uint32_t* dep = s_dep[r];
-            const int cc0 = max(T.c0, tx0), cc1 = min(T.c1, tx1);
-            const int rr0 = max(T.r0, ty0), rr1 = min(T.r1, ty1);
-            if (a.ablate & 4) {
-              const unsigned long long it = (unsigned long long)(cc1 - cc0 + 1) * (rr1 - rr0 + 1);
-              atomicAdd(&g_vsd_stats[2], 1ull);
-              atomicAdd(&g_vsd_stats[3], it);
-            }
-            r_raster(T, cc0, cc1, rr0, rr1, [&](int col, int row, float q) {
-              if (a.ablate & 4) atomicAdd(&g_vsd_stats[5], 1ull);
-              atomicMax(&dep[(row - ty0) * kTileW + (col - tx0)], __float_as_uint(q));
-            });
+            act = true;
+            cc0 = max(T.c0, tx0);
+            cc1 = min(T.c1, tx1);
+            rr0 = max(T.r0, ty0);
+            rr1 = min(T.r1, ty1);
           }
         }
+        if ((a.ablate & 4) && act) {
+          atomicAdd(&g_vsd_stats[2], 1ull);
+          atomicAdd(&g_vsd_stats[3], (unsigned long long)(cc1 - cc0 + 1) * (rr1 - rr0 + 1));
+        }
+        uint32_t* dep = s_dep[r];
+        auto plot = [&](int col, int row, float q) {
+          if (a.ablate & 4) atomicAdd(&g_vsd_stats[5], 1ull);
+          atomicMax(&dep[(row - ty0) * kTileW + (col - tx0)], __float_as_uint(q));
+        };
+        // Compact the small overlapping triangles and split their rows over
+        // s = 64 / m lanes each (records reuse this wave's staging area).
+        const bool sm = act && T.small;
+        const unsigned long long bal = __ballot(sm);
+        const int msm = __popcll(bal);
+        wave_lds_sync();  // staged-vertex reads done before records overwrite them
+        RRec* rec = reinterpret_cast<RRec*>(&s_vtx[wave][0]);
+        if (sm) {
+          RRec rc;
+          r_make_rec(T, cc0, cc1, rr0, rr1, rc);
+          rec[__popcll(bal & ((1ull << lane) - 1ull))] = rc;
+        }
+        wave_lds_sync();
+        if (msm > 0) {
+          const int s = 64 / msm, slot = lane / s;
+          if (slot < msm) r_raster_rows(rec[slot], lane - slot * s, s, plot);
+        }
+        if (act && !T.small) r_raster(T, cc0, cc1, rr0, rr1, plot);
         if ((a.ablate & 4) && lane == 0) atomicAdd(&g_vsd_stats[1], 1ull);
         wave_lds_sync();  // s_vtx is rewritten by the next entry
       }

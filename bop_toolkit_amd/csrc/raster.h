@@ -46,12 +46,13 @@ __device__ __forceinline__ RVtx r_vertex(const float* __restrict__ Rf, const Cam
   o.iz = 0.0f;
   o.ok = false;
   if (!(Z > 0.0f)) return o;
-  const float u = (c.fx * X) / Z + c.cx;
-  const float v = (c.fy * Y) / Z + c.cy;
+  const float iz = 1.0f / Z;  // the one IEEE division per vertex (spec v4)
+  const float u = (c.fx * X) * iz + c.cx;
+  const float v = (c.fy * Y) * iz + c.cy;
   if (!(fabsf(u) <= kGuardBand) || !(fabsf(v) <= kGuardBand)) return o;
   o.U = (int32_t)__builtin_rintf(u * 256.0f);
   o.V = (int32_t)__builtin_rintf(v * 256.0f);
-  o.iz = 1.0f / Z;
+  o.iz = iz;
   o.ok = true;
   return o;
 }
@@ -91,8 +92,8 @@ __device__ __forceinline__ bool r_setup(RVtx a, RVtx b, RVtx c, RTri& t, int x0,
   }
   float farea;
   bool neg;
-  if (t.small) {  // |area| <= 2 * 32767^2 < 2^31
-    const int32_t area = (b.U - a.U) * (c.V - a.V) - (b.V - a.V) * (c.U - a.U);
+  if (t.small) {  // |area| <= 2 * 32767^2 < 2^31; factors < 2^15: exact 24-bit multiplies
+    const int32_t area = __mul24(b.U - a.U, c.V - a.V) - __mul24(b.V - a.V, c.U - a.U);
     if (area == 0) return false;
     neg = area < 0;
     farea = (float)(neg ? -area : area);
@@ -183,6 +184,74 @@ __device__ __forceinline__ void r_raster(const RTri& t, int cc0, int cc1, int rr
         }
       }
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Row-split rasterisation of compacted triangles (the k_vsd fast path).
+// A wave's triangles that overlap the tile are compacted (ballot rank) and
+// published as 64-B records in LDS; each then gets s = 64 / m lanes, lane `sub`
+// walking rows rr0 + sub, rr0 + sub + s, ... with the same int32 incremental
+// edge values as r_raster (so the fragments and q values are identical).
+struct __attribute__((aligned(16))) RRec {
+  uint32_t er[3];     // edge values (+ top-left bias) at (cc0, rr0)
+  int32_t px0u, py0v; // 256*cc0 + 128 - U0, 256*rr0 + 128 - V0
+  float iz0, ga, gb;  // 1/Z plane
+  int32_t dU[3], dV[3];
+  int32_t cc0rr0;     // cc0 | rr0 << 16
+  int32_t wh;         // w | h << 16  (clipped rectangle size)
+};
+static_assert(sizeof(RRec) == 64, "RRec is one 64-B LDS record");
+
+__device__ __forceinline__ void r_make_rec(const RTri& t, int cc0, int cc1, int rr0, int rr1,
+                                           RRec& r) {
+  const int32_t px0 = 256 * cc0 + 128, py0 = 256 * rr0 + 128;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    // small triangles: |dU|, |dV|, |p0 - vertex| < 2^15 -> exact 24-bit multiplies
+    r.er[k] = (uint32_t)(__mul24(t.dU[k], py0 - t.Vs[k]) - __mul24(t.dV[k], px0 - t.Us[k]) +
+                         t.tl[k]);
+    r.dU[k] = t.dU[k];
+    r.dV[k] = t.dV[k];
+  }
+  r.px0u = px0 - t.U0;
+  r.py0v = py0 - t.V0;
+  r.iz0 = t.iz0;
+  r.ga = t.ga;
+  r.gb = t.gb;
+  r.cc0rr0 = cc0 | (rr0 << 16);
+  r.wh = (cc1 - cc0 + 1) | ((rr1 - rr0 + 1) << 16);
+}
+
+// Rows sub, sub + s, ... of a record (small triangles only: int32 exact).
+template <class Plot>
+__device__ __forceinline__ void r_raster_rows(const RRec& r, int sub, int s, Plot plot) {
+  const int cc0 = r.cc0rr0 & 0xFFFF, rr0 = r.cc0rr0 >> 16;
+  const int w = r.wh & 0xFFFF, h = r.wh >> 16;
+  uint32_t er[3], sx[3], sy[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    sx[k] = (uint32_t)(-256 * r.dV[k]);
+    sy[k] = (uint32_t)__mul24(256 * r.dU[k], s);
+    er[k] = r.er[k] + (uint32_t)__mul24(256 * r.dU[k], sub);
+  }
+  int32_t dy = r.py0v + 256 * sub;
+  for (int j = sub; j < h; j += s, dy += 256 * s) {
+    uint32_t e0 = er[0], e1 = er[1], e2 = er[2];
+    int32_t dx = r.px0u;
+    const float qy = (float)dy;
+    for (int i = 0; i < w; ++i, dx += 256) {
+      if (((int32_t)e0 > 0) & ((int32_t)e1 > 0) & ((int32_t)e2 > 0)) {
+        const float q = (r.iz0 + r.ga * (float)dx) + r.gb * qy;
+        if (q > 0.0f) plot(cc0 + i, rr0 + j, q);
+      }
+      e0 += sx[0];
+      e1 += sx[1];
+      e2 += sx[2];
+    }
+    er[0] += sy[0];
+    er[1] += sy[1];
+    er[2] += sy[2];
   }
 }
 

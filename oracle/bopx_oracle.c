@@ -258,12 +258,13 @@ int oracle_vsd_depths(int W, int H, const float* depth_test, const float* depth_
 }
 
 /* ------------------------------------------------------------ depth raster */
-/* Spec v2:
+/* Spec v4:
  *  - R, t, fx, fy, cx, cy rounded to float32 (GL uniforms, renderer_vispy.py:441-442);
  *    vertices float32 (renderer_vispy.py:373).
  *  - X = ((r0*x + r1*y) + r2*z) + t, float32, no FMA; valid iff Z > 0.
- *  - u = (fx*X)/Z + cx, v = (fy*Y)/Z + cy (float32); valid iff |u|,|v| <= 16384.
- *  - Snap to 1/256 px: U = rint(u*256), V = rint(v*256); iz = 1.0f / Z (float32).
+ *  - iz = 1.0f / Z, u = (fx*X)*iz + cx, v = (fy*Y)*iz + cy (float32);
+ *    valid iff |u|,|v| <= 16384.
+ *  - Snap to 1/256 px: U = rint(u*256), V = rint(v*256).
  *  - Pixel (c, r) samples (256c+128, 256r+128) (= pixel centre (c+0.5, r+0.5)).
  *  - Integer edge functions, top-left fill rule, both windings (no culling).
  *  - 1/Z is affine in screen space: per triangle (vertices a, b, c with area > 0),
@@ -291,12 +292,13 @@ static ovtx oracle_vertex(const float* Rf, const float* tf, float fx, float fy, 
   o.U = o.V = 0;
   o.iz = 0.0f;
   if (!(Z > 0.0f)) return o;
-  float u = (fx * X) / Z + cx;
-  float v = (fy * Y) / Z + cy;
+  float iz = 1.0f / Z;
+  float u = (fx * X) * iz + cx;
+  float v = (fy * Y) * iz + cy;
   if (!(fabsf(u) <= 16384.0f) || !(fabsf(v) <= 16384.0f)) return o;
   o.U = (int32_t)rintf(u * 256.0f);
   o.V = (int32_t)rintf(v * 256.0f);
-  o.iz = 1.0f / Z;
+  o.iz = iz;
   o.ok = 1;
   return o;
 }
