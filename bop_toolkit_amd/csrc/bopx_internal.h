@@ -15,8 +15,16 @@
 
 namespace bopx {
 
+// Pointer into global memory (address space 1). Device code that reads a
+// pointer out of memory (e.g. from ObjDesc) only knows it as a generic pointer
+// and emits flat_load; casting to gptr gives global_load, which is tracked by
+// vmcnt alone and can stay in flight across LDS waits.
+template <class T>
+using gptr = __attribute__((address_space(1))) T*;
+typedef float f32x4 __attribute__((ext_vector_type(4)));  // native vector: works in any addrspace
+
 constexpr int kMeshletTris = 64;    // one wave lane per triangle
-constexpr int kMeshletVerts = 128;  // unique vertices per meshlet (LDS staging)
+constexpr int kMeshletVerts = 64;   // unique vertices per meshlet (one per lane)
 #ifndef BOPX_MAX_MESHLETS
 #define BOPX_MAX_MESHLETS 1024
 #endif
@@ -28,6 +36,7 @@ constexpr int kMaxMeshlets = BOPX_MAX_MESHLETS;  // per object (VSD)
 constexpr int kMaxTaus = 16;
 constexpr int kTileW = BOPX_TILE_W;  // VSD screen tile (LDS-resident q pair)
 constexpr int kTileH = BOPX_TILE_H;
+constexpr int kTileStride = kTileW + 1;  // LDS row pitch of a q tile (dwords)
 constexpr float kGuardBand = 16384.0f;  // |u|,|v| limit of a rasterised vertex (px)
 
 struct ObjDesc {
@@ -35,10 +44,10 @@ struct ObjDesc {
   const float4* vtx;         // nv
   const uint32_t* faces;     // 3*nf (meshlet order)
   const float* mlet;         // 8*nm: object-space AABB per meshlet
-  const int4* mlet_info;     // nm: {first triangle, #triangles, first vertex, #vertices}
-  const float4* mlet_vtx;    // meshlet-local vertex blocks (vertices shared by
-                             // neighbouring meshlets are duplicated)
-  const uint32_t* mlet_tri;  // nf: local vertex indices a | b << 8 | c << 16
+  const int4* mlet_info;     // nm: {first triangle, #triangles, first vertex slot, #vertices}
+  const float4* mlet_vtx;    // nm x 64: meshlet-local vertex blocks, fixed stride
+                             // (vertices shared by neighbouring meshlets are duplicated)
+  const uint32_t* mlet_tri;  // nm x 64: local indices a | b << 8 | c << 16, 0xFFFFFFFF = none
   const double* syms;        // 12*ns
   int nv, nf, nm, ns;
 };

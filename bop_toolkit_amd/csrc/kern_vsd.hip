@@ -36,6 +36,19 @@ constexpr int kVsdThreads = BOPX_VSD_THREADS;
 // Workload counters for the timing diagnostics (BOPX_VSD_ABLATE bit 2). Not
 // part of the C-ABI; read with bopx_debug_vsd_stats.
 __device__ unsigned long long g_vsd_stats[8];
+// Diagnostic phase clocks (BOPX_VSD_ABLATE bit 3; s_memtime, summed over waves):
+// [0] clear+coeffs, [1] list, [2] raster work, [3] raster barrier wait,
+// [4] pixel work, [5] pixel barrier wait, [6] pre-loop, [7] epilogue; raster work
+// split: [8] vertex staging, [9] bbox test + compaction, [10] set-up, [11] walk.
+__device__ unsigned long long g_vsd_time[16];
+#define VSD_STAMP(k)                                              \
+  do {                                                            \
+    if (a.ablate & 8) {                                           \
+      const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+      ph[k] += _t - t_prev;                                       \
+      t_prev = _t;                                                \
+    }                                                             \
+  } while (0)
 
 // float64 distance of a float32 depth at pixel (pX, pY) (misc.py:158-161).
 __device__ __forceinline__ double dist_of(double pX, double pY, float depth) {
@@ -54,7 +67,7 @@ __device__ __forceinline__ bool visib19(double dt, double dm, float delta32, int
 
 // Conservative pixel rectangle of one meshlet AABB under a pose. Any corner with
 // Z <= 0 (or a non-finite projection) gives the whole image.
-__device__ __forceinline__ short4 meshlet_rect(const float* __restrict__ mb, const float* Rf,
+__device__ __forceinline__ short4 meshlet_rect(gptr<const float> mb, const float* Rf,
                                                const Cam32& c, int W, int H) {
   float umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
   bool full = false;
@@ -107,14 +120,26 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 constexpr int kVsdWaves = kVsdThreads / 64;
+#ifndef BOPX_VSD_GROUP
+#define BOPX_VSD_GROUP 2
+#endif
+constexpr int kRowWin = 256;  // row items numbered per window (LDS owner map)
+constexpr int kGroup = BOPX_VSD_GROUP;  // (pose, meshlet) entries staged together per wave step
 constexpr int kRectsPerThread = 2 * kMaxMeshlets / kVsdThreads;
 
 template <int COST>  // 0 = step, 1 = tlinear
-__global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
-  __shared__ uint32_t s_dep[2][kTileW * kTileH];     // q = 1/Z bits, 0 = empty
-  // per-wave area: staged meshlet vertices (2 KiB), then triangle records (4 KiB)
-  __shared__ RVtx s_vtx[kVsdWaves][2 * kMeshletVerts];
+// Two workgroups per CU: 2 * kVsdThreads / 256 waves per SIMD (caps VGPRs at 128).
+__global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdArgs a) {
+  // q = 1/Z bits, 0 = empty; rows padded by one dword so lanes that walk the
+  // same column on consecutive rows (row-split) hit different LDS banks.
+  __shared__ uint32_t s_dep[2][kTileStride * kTileH];
+  // per wave: staged vertex blocks of one entry group, compacted triangle refs
+  __shared__ RVtx s_stage[kVsdWaves][kGroup * kMeshletVerts];
+  __shared__ uint32_t s_tri[kVsdWaves][kGroup * kMeshletTris];
+  __shared__ RRow s_rec[kVsdWaves][64];          // set-up triangles of the current chunk
+  __shared__ uint8_t s_own[kVsdWaves][kRowWin];  // row item -> record (lane) of a window
   __shared__ uint16_t s_list[2 * kMaxMeshlets];
+  __shared__ int s_next;
   __shared__ double s_pX[kTileW], s_pY[kTileH];
   __shared__ float s_pose[2][12];
   __shared__ int s_roi[4];
@@ -125,10 +150,17 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
 
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  unsigned long long ph[16] = {}, t_prev = 0;
+  if (a.ablate & 8) t_prev = __builtin_amdgcn_s_memtime();
   const ObjDesc o = a.objs[a.slots[b]];
   const int W = a.width, H = a.height, nm = o.nm;
+  // Object arrays live in global memory: address-space-1 views give
+  // global_load (vmcnt only) instead of flat_load for pointers read from memory.
+  const gptr<const f32x4> g_mvtx = (gptr<const f32x4>)o.mlet_vtx;
+  const gptr<const uint32_t> g_mtri = (gptr<const uint32_t>)o.mlet_tri;
+  const gptr<const float> g_mlet = (gptr<const float>)o.mlet;
   const int64_t fidx = a.frame_idx[b];
-  const float* __restrict__ frame = a.frames + fidx * (int64_t)W * H;
+  const gptr<const float> frame = (gptr<const float>)(a.frames + fidx * (int64_t)W * H);
   const double fx = a.cam[4 * fidx + 0], fy = a.cam[4 * fidx + 1];
   const double cx = a.cam[4 * fidx + 2], cy = a.cam[4 * fidx + 3];
   Cam32 c32;
@@ -154,7 +186,7 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
     rect[j] = make_short4(1, 1, 0, 0);
     if (i < 2 * nm) {
       const int r = i >= nm, m = i - r * nm;
-      rect[j] = meshlet_rect(o.mlet + 8 * (int64_t)m, s_pose[r], c32, W, H);
+      rect[j] = meshlet_rect(g_mlet + 8 * (int64_t)m, s_pose[r], c32, W, H);
       if (rect[j].x <= rect[j].z && rect[j].y <= rect[j].w) {
         atomicMin(&s_roi[0], (int)rect[j].x);
         atomicMin(&s_roi[1], (int)rect[j].y);
@@ -178,18 +210,23 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
   if (rx0 <= rx1 && ry0 <= ry1) {
     const int ntx = (rx1 - rx0 + kTileW) / kTileW, nty = (ry1 - ry0 + kTileH) / kTileH;
     if ((a.ablate & 4) && tid == 0) atomicAdd(&g_vsd_stats[0], (unsigned long long)(ntx * nty));
+    VSD_STAMP(6);
     for (int t = 0; t < ntx * nty; ++t) {
       const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
       const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
       // 2a. clear both q tiles, list the (pose, meshlet) entries touching the tile.
       uint32_t* dep_flat = &s_dep[0][0];
-      for (int i = tid; i < 2 * kTileW * kTileH; i += kVsdThreads) dep_flat[i] = 0u;
-      if (tid == 0) s_nlist = 0;
+      for (int i = tid; i < 2 * kTileStride * kTileH; i += kVsdThreads) dep_flat[i] = 0u;
+      if (tid == 0) {
+        s_nlist = 0;
+        s_next = 0;
+      }
       // float64 distance coefficients of the tile's columns / rows (misc.py:137-138)
       if (tid < kTileW) s_pX[tid] = ((double)(tx0 + tid) - cx) / fx;
       if (tid >= kVsdThreads - kTileH)
         s_pY[tid - (kVsdThreads - kTileH)] = ((double)(ty0 + tid - (kVsdThreads - kTileH)) - cy) / fy;
       __syncthreads();
+      VSD_STAMP(0);
 #pragma unroll
       for (int j = 0; j < kRectsPerThread; ++j) {
         const short4 rc = rect[j];
@@ -198,71 +235,128 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
           s_list[atomicAdd(&s_nlist, 1)] = (uint16_t)(tid + j * kVsdThreads);
       }
       __syncthreads();
-      // 2b. rasterise: one meshlet per wave step. The wave transforms the
-      // meshlet's vertex block once (lane = vertex) into LDS, then each lane
-      // sets up and rasterises one triangle from the staged vertices.
-      const int nl = (a.ablate & 1) ? 0 : s_nlist;
-      for (int li = wave; li < nl; li += kVsdWaves) {
-        const int e = __builtin_amdgcn_readfirstlane(s_list[li]);
-        const int r = e >= nm, m = e - r * nm;
-        const int4 info = o.mlet_info[m];
-        const float* Rf = s_pose[r];
-        for (int j = lane; j < info.w; j += 64) {
-          const float4 v = o.mlet_vtx[info.z + j];
-          s_vtx[wave][j] = r_vertex(Rf, c32, v.x, v.y, v.z);
+      VSD_STAMP(1);
+      // 2b. rasterise. Waves pull groups of kGroup (pose, meshlet) entries from a
+      // shared counter (dynamic balance). Per group: the wave transforms the
+      // three fixed-stride vertex blocks once (lane = vertex) into LDS, tests
+      // every triangle's bbox against the tile, compacts the hits (ballot rank)
+      // and only then sets up and rasterises them, one triangle per lane.
+      const int nl = __builtin_amdgcn_readfirstlane((a.ablate & 1) ? 0 : s_nlist);
+      for (;;) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&s_next, kGroup);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (base >= nl) break;
+        f32x4 v[kGroup];
+        uint32_t pk[kGroup];
+        int pose[kGroup];
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g) {
+          const int e = __builtin_amdgcn_readfirstlane(s_list[min(base + g, nl - 1)]);
+          pose[g] = e >= nm;
+          const int m = e - pose[g] * nm;
+          v[g] = g_mvtx[m * kMeshletVerts + lane];
+          pk[g] = (base + g < nl) ? g_mtri[m * kMeshletTris + lane] : 0xFFFFFFFFu;
         }
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g)
+          s_stage[wave][g * kMeshletVerts + lane] = r_vertex(s_pose[pose[g]], c32, v[g].x, v[g].y,
+                                                             v[g].z);
         wave_lds_sync();
-        RTri T;
-        bool act = false;
-        int cc0 = 0, cc1 = -1, rr0 = 0, rr1 = -1;
-        if (lane < info.y) {
-          const uint32_t pk = o.mlet_tri[info.x + lane];
-          const RVtx A = s_vtx[wave][pk & 255u], B = s_vtx[wave][(pk >> 8) & 255u],
-                     C = s_vtx[wave][(pk >> 16) & 255u];
-          if (r_setup(A, B, C, T, tx0, tx1, ty0, ty1)) {
-            act = true;
-            cc0 = max(T.c0, tx0);
-            cc1 = min(T.c1, tx1);
-            rr0 = max(T.r0, ty0);
-            rr1 = min(T.r1, ty1);
+        VSD_STAMP(8);
+        int cnt = 0;
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g) {
+          bool hit = false;
+          if (pk[g] != 0xFFFFFFFFu) {
+            const RVtx* sg = &s_stage[wave][g * kMeshletVerts];
+            hit = r_touches(sg[pk[g] & 255u], sg[(pk[g] >> 8) & 255u], sg[(pk[g] >> 16) & 255u],
+                            tx0, tx1, ty0, ty1);
           }
-        }
-        if ((a.ablate & 4) && act) {
-          atomicAdd(&g_vsd_stats[2], 1ull);
-          atomicAdd(&g_vsd_stats[3], (unsigned long long)(cc1 - cc0 + 1) * (rr1 - rr0 + 1));
-        }
-        uint32_t* dep = s_dep[r];
-        auto plot = [&](int col, int row, float q) {
-          if (a.ablate & 4) atomicAdd(&g_vsd_stats[5], 1ull);
-          atomicMax(&dep[(row - ty0) * kTileW + (col - tx0)], __float_as_uint(q));
-        };
-        // Compact the small overlapping triangles and split their rows over
-        // s = 64 / m lanes each (records reuse this wave's staging area).
-        const bool sm = act && T.small;
-        const unsigned long long bal = __ballot(sm);
-        const int msm = __popcll(bal);
-        wave_lds_sync();  // staged-vertex reads done before records overwrite them
-        RRec* rec = reinterpret_cast<RRec*>(&s_vtx[wave][0]);
-        if (sm) {
-          RRec rc;
-          r_make_rec(T, cc0, cc1, rr0, rr1, rc);
-          rec[__popcll(bal & ((1ull << lane) - 1ull))] = rc;
+          const unsigned long long bal = __ballot(hit);
+          if (hit)
+            s_tri[wave][cnt + __popcll(bal & ((1ull << lane) - 1ull))] =
+                (pk[g] & 0xFFFFFFu) | ((uint32_t)g << 24) | ((uint32_t)pose[g] << 26);
+          cnt += __popcll(bal);
         }
         wave_lds_sync();
-        if (msm > 0) {
-          const int s = 64 / msm, slot = lane / s;
-          if (slot < msm) r_raster_rows(rec[slot], lane - slot * s, s, plot);
+        if ((a.ablate & 4) && lane == 0) atomicAdd(&g_vsd_stats[1], (unsigned long long)kGroup);
+        VSD_STAMP(9);
+        for (int c0 = 0; c0 < cnt; c0 += 64) {
+          // Set-up, one triangle per lane.
+          RTri T;
+          bool ok = false;
+          int r = 0, cc0 = 0, cc1 = -1, rr0 = 0, rr1 = -1;
+          if (c0 + lane < cnt) {
+            const uint32_t ref = s_tri[wave][c0 + lane];
+            const RVtx* sg = &s_stage[wave][((ref >> 24) & 3u) * kMeshletVerts];
+            r = (int)(ref >> 26);
+            ok = r_setup(sg[ref & 255u], sg[(ref >> 8) & 255u], sg[(ref >> 16) & 255u], T, tx0,
+                         tx1, ty0, ty1);
+            if (ok) {
+              cc0 = max(T.c0, tx0);
+              cc1 = min(T.c1, tx1);
+              rr0 = max(T.r0, ty0);
+              rr1 = min(T.r1, ty1);
+            }
+          }
+          VSD_STAMP(10);
+          if (a.ablate & 4) {
+            if (ok) {
+              atomicAdd(&g_vsd_stats[2], 1ull);
+              atomicAdd(&g_vsd_stats[3], (unsigned long long)(cc1 - cc0 + 1) * (rr1 - rr0 + 1));
+            }
+            if (ok && T.small) atomicAdd(&g_vsd_stats[4], (unsigned long long)(rr1 - rr0 + 1));
+          }
+          if (ok && !T.small) {  // extent >= 128 px: int64 edges, walked by its own lane
+            uint32_t* dep = s_dep[r];
+            r_raster(T, cc0, cc1, rr0, rr1, [&](int col, int row, float q) {
+              if (a.ablate & 4) atomicAdd(&g_vsd_stats[5], 1ull);
+              atomicMax(&dep[(row - ty0) * kTileStride + (col - tx0)], __float_as_uint(q));
+            });
+          }
+          // Row items: publish one record per small triangle, number its rows
+          // (wave prefix sum), then deal the rows out one per lane.
+          const bool rows = ok && T.small;
+          const int h = rows ? rr1 - rr0 + 1 : 0;
+          int inc = h;
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += v;
+          }
+          const int first = inc - h;
+          const int nrow = __builtin_amdgcn_readlane(inc, 63);
+          if (rows) r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first, s_rec[wave][lane]);
+          for (int wb = 0; wb < nrow; wb += kRowWin) {
+            wave_lds_sync();  // records written / previous window's owners consumed
+            for (int k = max(first, wb); k < min(first + h, wb + kRowWin); ++k)
+              s_own[wave][k - wb] = (uint8_t)lane;
+            wave_lds_sync();
+            const int wn = min(nrow - wb, kRowWin);
+            for (int p = lane; p < wn; p += 64) {
+              const RRow rec = s_rec[wave][s_own[wave][p]];
+              r_walk_row(rec, wb + p - (int)(rec.meta >> 19),
+                         [&](int pose, int col, int row, float q) {
+                           if (a.ablate & 4) atomicAdd(&g_vsd_stats[5], 1ull);
+                           atomicMax(&s_dep[pose][row * kTileStride + col], __float_as_uint(q));
+                         });
+            }
+          }
+          VSD_STAMP(11);
+          wave_lds_sync();  // records are rewritten by the next chunk
         }
-        if (act && !T.small) r_raster(T, cc0, cc1, rr0, rr1, plot);
-        if ((a.ablate & 4) && lane == 0) atomicAdd(&g_vsd_stats[1], 1ull);
-        wave_lds_sync();  // s_vtx is rewritten by the next entry
+        wave_lds_sync();  // the staging area is rewritten by the next group
       }
+      VSD_STAMP(2);
       __syncthreads();
+      VSD_STAMP(3);
       // 3. per-pixel distances, visibility masks, counters.
       for (int p = tid; p < ((a.ablate & 2) ? 0 : kTileW * kTileH); p += kVsdThreads) {
         const int row = ty0 + p / kTileW, col = tx0 + p % kTileW;
         if (row > ty1 || col > tx1) continue;
-        const uint32_t qe = s_dep[0][p], qg = s_dep[1][p];
+        const int ps = (p / kTileW) * kTileStride + p % kTileW;
+        const uint32_t qe = s_dep[0][ps], qg = s_dep[1][ps];
         if ((qe | qg) == 0u) continue;  // neither pose covers this pixel
         if (a.ablate & 4) atomicAdd(&g_vsd_stats[6], 1ull);
         const float de = qe ? 1.0f / __uint_as_float(qe) : 0.0f;
@@ -294,7 +388,9 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
           }
         }
       }
+      VSD_STAMP(4);
       __syncthreads();
+      VSD_STAMP(5);
     }
   }
 
@@ -319,6 +415,9 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
     }
   }
   __syncthreads();
+  VSD_STAMP(7);
+  if ((a.ablate & 8) && lane == 0)
+    for (int k = 0; k < 16; ++k) atomicAdd(&g_vsd_time[k], ph[k]);
   if (tid == 0) {
     uint64_t un = 0, in = 0;
     for (int w = 0; w < kVsdWaves; ++w) {
@@ -345,9 +444,12 @@ __global__ __launch_bounds__(kVsdThreads) void k_vsd(VsdArgs a) {
 
 hipError_t read_vsd_stats(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vsd_stats), sizeof(g_vsd_stats));
+  if (e == hipSuccess)
+    e = hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(g_vsd_time), sizeof(g_vsd_time));
   if (e != hipSuccess || !reset) return e;
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_vsd_stats), z, sizeof(z));
+  unsigned long long z[16] = {};
+  e = hipMemcpyToSymbol(HIP_SYMBOL(g_vsd_stats), z, sizeof(g_vsd_stats));
+  return e == hipSuccess ? hipMemcpyToSymbol(HIP_SYMBOL(g_vsd_time), z, sizeof(z)) : e;
 }
 
 hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s) {

@@ -27,10 +27,12 @@ struct Cam32 {
   float fx, fy, cx, cy;
 };
 
+// 12 bytes (ds_read_b96). Valid vertices have |U| <= 2^22; U = INT32_MIN marks
+// a vertex that is not rasterisable (Z <= 0 or outside the guard band).
 struct RVtx {
   int32_t U, V;
   float iz;
-  bool ok;
+  __device__ __forceinline__ bool ok() const { return U != INT32_MIN; }
 };
 
 // Camera-space transform + projection of one float32 vertex. Rf: R row-major
@@ -41,10 +43,9 @@ __device__ __forceinline__ RVtx r_vertex(const float* __restrict__ Rf, const Cam
   const float X = ((Rf[0] * x + Rf[1] * y) + Rf[2] * z) + Rf[9];
   const float Y = ((Rf[3] * x + Rf[4] * y) + Rf[5] * z) + Rf[10];
   const float Z = ((Rf[6] * x + Rf[7] * y) + Rf[8] * z) + Rf[11];
-  o.U = 0;
+  o.U = INT32_MIN;
   o.V = 0;
   o.iz = 0.0f;
-  o.ok = false;
   if (!(Z > 0.0f)) return o;
   const float iz = 1.0f / Z;  // the one IEEE division per vertex (spec v4)
   const float u = (c.fx * X) * iz + c.cx;
@@ -53,7 +54,6 @@ __device__ __forceinline__ RVtx r_vertex(const float* __restrict__ Rf, const Cam
   o.U = (int32_t)__builtin_rintf(u * 256.0f);
   o.V = (int32_t)__builtin_rintf(v * 256.0f);
   o.iz = iz;
-  o.ok = true;
   return o;
 }
 
@@ -78,7 +78,7 @@ struct RTri {
 // the bbox test runs first so culled triangles skip the float64 set-up.
 __device__ __forceinline__ bool r_setup(RVtx a, RVtx b, RVtx c, RTri& t, int x0, int x1, int y0,
                                         int y1) {
-  if (!(a.ok && b.ok && c.ok)) return false;
+  if (!(a.ok() && b.ok() && c.ok())) return false;
   {
     // |U|, |V| <= 2^22 (guard band): floor(x / 256) is an arithmetic shift.
     const int32_t minU = min(a.U, min(b.U, c.U)), maxU = max(a.U, max(b.U, c.U));
@@ -125,6 +125,16 @@ __device__ __forceinline__ bool r_setup(RVtx a, RVtx b, RVtx c, RTri& t, int x0,
     t.tl[k] = (t.dV[k] < 0 || (t.dV[k] == 0 && t.dU[k] > 0)) ? 1 : 0;
   }
   return true;
+}
+
+// Cheap pre-test: all vertices valid and the pixel bbox meets [x0,x1] x [y0,y1]
+// (the same bbox r_setup computes; r_setup may still reject zero-area triangles).
+__device__ __forceinline__ bool r_touches(RVtx a, RVtx b, RVtx c, int x0, int x1, int y0,
+                                          int y1) {
+  const int32_t minU = min(a.U, min(b.U, c.U)), maxU = max(a.U, max(b.U, c.U));
+  const int32_t minV = min(a.V, min(b.V, c.V)), maxV = max(a.V, max(b.V, c.V));
+  return a.ok() && b.ok() && c.ok() && max((minU + 127) >> 8, x0) <= min((maxU - 128) >> 8, x1) &&
+         max((minV + 127) >> 8, y0) <= min((maxV - 128) >> 8, y1);
 }
 
 __device__ __forceinline__ float r_q(const RTri& t, int32_t px, int32_t py) {
@@ -188,70 +198,63 @@ __device__ __forceinline__ void r_raster(const RTri& t, int cc0, int cc1, int rr
 }
 
 // ---------------------------------------------------------------------------
-// Row-split rasterisation of compacted triangles (the k_vsd fast path).
-// A wave's triangles that overlap the tile are compacted (ballot rank) and
-// published as 64-B records in LDS; each then gets s = 64 / m lanes, lane `sub`
-// walking rows rr0 + sub, rr0 + sub + s, ... with the same int32 incremental
-// edge values as r_raster (so the fragments and q values are identical).
-struct __attribute__((aligned(16))) RRec {
-  uint32_t er[3];     // edge values (+ top-left bias) at (cc0, rr0)
-  int32_t px0u, py0v; // 256*cc0 + 128 - U0, 256*rr0 + 128 - V0
-  float iz0, ga, gb;  // 1/Z plane
-  int32_t dU[3], dV[3];
-  int32_t cc0rr0;     // cc0 | rr0 << 16
-  int32_t wh;         // w | h << 16  (clipped rectangle size)
+// Row items (the k_vsd fast path). A wave's set-up triangles publish one 48-B
+// record each in LDS; the wave then hands out (triangle, row) items, one per
+// lane, and each lane walks the columns of its row with the same int32
+// incremental edge values and q expression as r_raster (identical fragments).
+// Balancing rows instead of whole triangles bounds a lane's walk by the widest
+// row in the batch instead of the largest bounding box.
+struct __attribute__((aligned(16))) RRow {
+  uint32_t er[3];      // edge values (+ top-left bias) at (cc0, rr0)
+  uint32_t duv[3];     // dU | dV << 16 (int16 each: small triangles)
+  int32_t px0u, py0v;  // 256*cc0 + 128 - U0, 256*rr0 + 128 - V0
+  float iz0, ga, gb;   // 1/Z plane
+  uint32_t meta;       // cc0-x0 | (rr0-y0) << 6 | (w-1) << 12 | pose << 18 | first item << 19
 };
-static_assert(sizeof(RRec) == 64, "RRec is one 64-B LDS record");
+static_assert(sizeof(RRow) == 48, "RRow is a 48-B LDS record");
 
-__device__ __forceinline__ void r_make_rec(const RTri& t, int cc0, int cc1, int rr0, int rr1,
-                                           RRec& r) {
+// Small triangles only; [cc0,cc1] x [rr0,rr1] inside the 64x64 tile at (x0, y0).
+__device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int rr0, int x0,
+                                           int y0, int pose, int first, RRow& r) {
   const int32_t px0 = 256 * cc0 + 128, py0 = 256 * rr0 + 128;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    // small triangles: |dU|, |dV|, |p0 - vertex| < 2^15 -> exact 24-bit multiplies
+    // |dU|, |dV|, |p0 - vertex| < 2^15 -> exact 24-bit multiplies
     r.er[k] = (uint32_t)(__mul24(t.dU[k], py0 - t.Vs[k]) - __mul24(t.dV[k], px0 - t.Us[k]) +
                          t.tl[k]);
-    r.dU[k] = t.dU[k];
-    r.dV[k] = t.dV[k];
+    r.duv[k] = ((uint32_t)t.dU[k] & 0xFFFFu) | ((uint32_t)t.dV[k] << 16);
   }
   r.px0u = px0 - t.U0;
   r.py0v = py0 - t.V0;
   r.iz0 = t.iz0;
   r.ga = t.ga;
   r.gb = t.gb;
-  r.cc0rr0 = cc0 | (rr0 << 16);
-  r.wh = (cc1 - cc0 + 1) | ((rr1 - rr0 + 1) << 16);
+  r.meta = (uint32_t)(cc0 - x0) | ((uint32_t)(rr0 - y0) << 6) | ((uint32_t)(cc1 - cc0) << 12) |
+           ((uint32_t)pose << 18) | ((uint32_t)first << 19);
 }
 
-// Rows sub, sub + s, ... of a record (small triangles only: int32 exact).
+// Walk row j of a record: plot(pose, tile col, tile row, q) per fragment.
 template <class Plot>
-__device__ __forceinline__ void r_raster_rows(const RRec& r, int sub, int s, Plot plot) {
-  const int cc0 = r.cc0rr0 & 0xFFFF, rr0 = r.cc0rr0 >> 16;
-  const int w = r.wh & 0xFFFF, h = r.wh >> 16;
-  uint32_t er[3], sx[3], sy[3];
+__device__ __forceinline__ void r_walk_row(const RRow& r, int j, Plot plot) {
+  const int tc0 = r.meta & 63u, tr = (int)((r.meta >> 6) & 63u) + j;
+  const int w = (int)((r.meta >> 12) & 63u) + 1, pose = (r.meta >> 18) & 1u;
+  uint32_t e[3], sx[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    sx[k] = (uint32_t)(-256 * r.dV[k]);
-    sy[k] = (uint32_t)__mul24(256 * r.dU[k], s);
-    er[k] = r.er[k] + (uint32_t)__mul24(256 * r.dU[k], sub);
+    const int32_t dU = (int32_t)(r.duv[k] << 16) >> 16, dV = (int32_t)r.duv[k] >> 16;
+    e[k] = r.er[k] + (uint32_t)__mul24(256 * dU, j);  // |256 dU| < 2^23, j < 64
+    sx[k] = (uint32_t)(-256 * dV);
   }
-  int32_t dy = r.py0v + 256 * sub;
-  for (int j = sub; j < h; j += s, dy += 256 * s) {
-    uint32_t e0 = er[0], e1 = er[1], e2 = er[2];
-    int32_t dx = r.px0u;
-    const float qy = (float)dy;
-    for (int i = 0; i < w; ++i, dx += 256) {
-      if (((int32_t)e0 > 0) & ((int32_t)e1 > 0) & ((int32_t)e2 > 0)) {
-        const float q = (r.iz0 + r.ga * (float)dx) + r.gb * qy;
-        if (q > 0.0f) plot(cc0 + i, rr0 + j, q);
-      }
-      e0 += sx[0];
-      e1 += sx[1];
-      e2 += sx[2];
+  const float qy = r.gb * (float)(r.py0v + 256 * j);
+  float fdx = (float)r.px0u;  // integers below 2^24: += 256 is exact
+  for (int i = 0; i < w; ++i, fdx += 256.0f) {
+    if (((int32_t)e[0] > 0) & ((int32_t)e[1] > 0) & ((int32_t)e[2] > 0)) {
+      const float q = (r.iz0 + r.ga * fdx) + qy;
+      if (q > 0.0f) plot(pose, tc0 + i, tr, q);
     }
-    er[0] += sy[0];
-    er[1] += sy[1];
-    er[2] += sy[2];
+    e[0] += sx[0];
+    e[1] += sx[1];
+    e[2] += sx[2];
   }
 }
 

@@ -336,14 +336,17 @@ int bopx_add_object(bopx_ctx* c, int obj_id, const double* pts, int64_t nv,
     fsorted.resize(3 * (size_t)nf);
     for (int64_t i = 0; i < nf; ++i)
       for (int k = 0; k < 3; ++k) fsorted[3 * i + k] = faces[3 * (size_t)key[i].second + k];
-    // Greedy meshlets along the Morton order: <= 64 triangles and <= 128 unique
-    // vertices each. Every meshlet carries its own vertex block (what a wave
-    // transforms once and shares through LDS) and 8-bit local indices.
+    // Greedy meshlets along the Morton order: <= 64 triangles and <= 64 unique
+    // vertices each, stored in fixed-stride slots (64 float32x4 vertices, 64
+    // triangle words; padding vertices repeat vertex 0, padding triangles are
+    // 0xFFFFFFFF) so a wave addresses meshlet m's data from m alone. Triangle
+    // words hold 8-bit local vertex indices a | b << 8 | c << 16.
     std::vector<int32_t> local(nv, -1);
     std::vector<uint32_t> touched;
     int64_t f = 0;
     while (f < nf) {
       const int32_t tri0 = (int32_t)f, vtx0 = (int32_t)mvtx.size();
+      const size_t tslot0 = mtri.size();
       touched.clear();
       float bl[3] = {INFINITY, INFINITY, INFINITY}, bh[3] = {-INFINITY, -INFINITY, -INFINITY};
       while (f < nf && f - tri0 < bopx::kMeshletTris) {
@@ -366,6 +369,9 @@ int bopx_add_object(bopx_ctx* c, int obj_id, const double* pts, int64_t nv,
         ++f;
       }
       for (uint32_t v : touched) local[v] = -1;
+      const float4 pad = mvtx[vtx0];
+      while (mvtx.size() - vtx0 < (size_t)bopx::kMeshletVerts) mvtx.push_back(pad);
+      while (mtri.size() - tslot0 < (size_t)bopx::kMeshletTris) mtri.push_back(0xFFFFFFFFu);
       minfo.push_back(make_int4(tri0, (int32_t)(f - tri0), vtx0, (int32_t)touched.size()));
       for (int k = 0; k < 3; ++k) mlet.push_back(bl[k]);
       mlet.push_back(0.f);

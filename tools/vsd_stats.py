@@ -24,17 +24,22 @@ def main():
   n, d = bench.build_workload(ev, objs, args, 0, torch)
   fn = ev.ctx.lib.bopx_debug_vsd_stats
   fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-  st = (ctypes.c_ulonglong * 8)()
+  st = (ctypes.c_ulonglong * 24)()
   fn(ev.ctx.h, st, 1)
   ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"], d["frames"], d["cam"],
          bench.DELTA, bench.TAUS, d["diameters"])
   torch.cuda.synchronize()
   fn(ev.ctx.h, st, 1)
-  names = ["tiles", "meshlet_entries", "tri_setups", "bbox_iters", "wave_max_iters_sum",
+  names = ["tiles", "meshlet_entries", "tri_setups", "bbox_iters", "rows",
            "fragments", "covered_px"]
   for i, k in enumerate(names):
     print("%-20s total %14d  per tuple %12.1f" % (k, st[i], st[i] / n))
-  print("lane efficiency of bbox loops: %.3f" % (st[3] / max(1, 64 * st[4])))
+  ph = ["clear+coeffs", "list", "raster work", "raster barrier", "pixel work",
+        "pixel barrier", "pre-loop", "epilogue", "r:stage", "r:compact", "r:setup", "r:walk"]
+  tot = sum(st[8 + i] for i in range(16))
+  for i, k in enumerate(ph):
+    print("phase %-16s %6.1f %%  (%.3g cycles/wave-tuple)" % (k, 100.0 * st[8 + i] / max(1, tot),
+                                                           st[8 + i] / n / 8))
   roi = bench.roi_pixels(objs, d["host"]["obj"], [d["host"]["pe"], d["host"]["pg"]],
                          bench.synth_K() if hasattr(bench, "synth_K") else __import__(
                              "bop_toolkit_amd.synth", fromlist=["YCBV_K"]).YCBV_K)
