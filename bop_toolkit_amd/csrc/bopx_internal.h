@@ -75,9 +75,10 @@ struct VsdArgs {
 
 // Launchers (kernels in kern_pose.hip / kern_vsd.hip). All return hipError_t of
 // the launch; inputs are device pointers.
-hipError_t launch_sym_error(int mode, const ObjDesc* objs, int64_t n, const int32_t* slots,
-                            const double* pe, const double* pg, const double* K, double* out,
-                            hipStream_t s);  // mode 0 = MSSD, 1 = MSPD
+hipError_t launch_sym_error(int mode, const ObjDesc* objs, int max_ns, int64_t n,
+                            const int32_t* slots, const double* pe, const double* pg,
+                            const double* K, double* out,
+                            hipStream_t s);  // mode 0 = MSSD, 1 = MSPD; max_ns over objects
 hipError_t launch_mean_error(int mode, const ObjDesc* objs, int64_t n, const int32_t* slots,
                              const double* pe, const double* pg, const double* K, double* out,
                              hipStream_t s);  // mode 0 = ADD, 1 = PROJ

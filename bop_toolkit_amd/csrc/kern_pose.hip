@@ -51,94 +51,162 @@ __device__ __forceinline__ void proj_mat(const double* K, const double* R, const
   }
 }
 
+// MSSD / MSPD. Work unit = (tuple b, chunk c of up to kSymChunk symmetries):
+// block id = b * nch + c, so the units of a many-symmetry object (e.g. a
+// discretised continuous symmetry, S = 314) are spread over the whole grid
+// instead of serialising on one CU; units past the object's last chunk exit at
+// once. Inside a unit, lane (k, g) = (symmetry k, vertex group g) keeps its
+// composed transform in VGPRs and sweeps the vertices, staged 256 at a time in
+// LDS (broadcast reads), with independent max chains. The unit's min over symmetries of the max squared
+// distance is merged into out[b] with a 64-bit atomicMin on the bits of the
+// non-negative double (exact and order-independent: deterministic);
+// k_sym_init / k_sym_finish bracket the launch (+inf, then sqrt).
+#ifndef BOPX_SYM_CHUNK
+#define BOPX_SYM_CHUNK 64
+#endif
+constexpr int kSymChunk = BOPX_SYM_CHUNK;  // <= 64: a unit's symmetries fit wave 0
+
+__global__ void k_sym_init(double* __restrict__ out, int64_t n) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) out[i] = INFINITY;
+}
+__global__ void k_sym_finish(double* __restrict__ out, int64_t n) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) out[i] = sqrt(out[i]);
+}
+
+// 1/x to ~1 ulp: hardware reciprocal + one Newton step (tolerance path).
+__device__ __forceinline__ double rcp64(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  const double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+
 template <int MODE>  // 0 = MSSD, 1 = MSPD
 __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __restrict__ objs,
                                                             const int32_t* __restrict__ slots,
                                                             const double* __restrict__ pe,
                                                             const double* __restrict__ pg,
                                                             const double* __restrict__ Km,
-                                                            double* __restrict__ out) {
+                                                            double* __restrict__ out, int nch) {
   __shared__ double s_red[kPoseThreads];
-  __shared__ double s_symmax[kPoseThreads];
-  const int64_t b = blockIdx.x;
+  // A block of vertices staged for every symmetry of the unit: x, y, z and,
+  // for MSPD, the estimate's projection u_e, v_e.
+  __shared__ double s_v[5][kPoseThreads];
+  const int64_t b = blockIdx.x / nch;
+  const int c = blockIdx.x % nch;
   const int tid = threadIdx.x;
   const ObjDesc o = objs[slots[b]];
-  const int nv = o.nv, ns = o.ns;
-  double E[12], G[12], K[9];
+  const int nv = o.nv, ns = o.ns, s0 = c * kSymChunk;
+  if (s0 >= ns) return;
+  const int sp = min(ns - s0, kSymChunk);
+  const int ng = kPoseThreads / sp;
+  const int k = tid % sp, g = tid / sp;
+  double G[12];
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    E[i] = pe[12 * b + i];
-    G[i] = pg[12 * b + i];
+  for (int i = 0; i < 12; ++i) G[i] = pg[12 * b + i];
+  // Compose R_gs = R_g S_R, t_gs = R_g S_t + t_g (pose_error.py:114-115).
+  const double* S = o.syms + 12 * (int64_t)(s0 + k);
+  double Rgs[9], tgs[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      Rgs[3 * i + j] = fma(G[3 * i + 2], S[6 + j], fma(G[3 * i + 1], S[3 + j], G[3 * i] * S[j]));
+    tgs[i] = fma(G[3 * i + 2], S[11], fma(G[3 * i + 1], S[10], fma(G[3 * i], S[9], G[9 + i])));
   }
-  double Pe[12];
-  if (MODE == 1) {
+  const gptr<const double> px = (gptr<const double>)o.pts;
+  const gptr<const double> py = px + nv;
+  const gptr<const double> pz = py + nv;
+  double m0 = -INFINITY, m1 = -INFINITY, m2 = -INFINITY, m3 = -INFINITY;
+  if (MODE == 0) {
+    double E[12], A[12];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) K[i] = Km[9 * b + i];
-    proj_mat(K, E, E + 9, Pe);
-  }
-  const double* __restrict__ px = o.pts;
-  const double* __restrict__ py = o.pts + nv;
-  const double* __restrict__ pz = o.pts + 2 * (int64_t)nv;
-  double best = INFINITY;
-  for (int s0 = 0; s0 < ns; s0 += kPoseThreads) {
-    const int sp = min(ns - s0, kPoseThreads);
-    const int ng = kPoseThreads / sp;
-    const int k = tid % sp, g = tid / sp;
-    double m = -INFINITY;
-    if (g < ng) {
-      // Compose R_gs = R_g S_R, t_gs = R_g S_t + t_g (pose_error.py:114-115).
-      const double* S = o.syms + 12 * (int64_t)(s0 + k);
-      double Rgs[9], tgs[3];
+    for (int i = 0; i < 12; ++i) E[i] = pe[12 * b + i];
+    // Difference-affine form: T_e p - T_gs p = (R_e - R_gs) p + (t_e - t_gs).
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < 3; ++i) {
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          Rgs[3 * i + j] = fma(G[3 * i + 2], S[6 + j], fma(G[3 * i + 1], S[3 + j], G[3 * i] * S[j]));
-        tgs[i] = fma(G[3 * i + 2], S[11], fma(G[3 * i + 1], S[10], fma(G[3 * i], S[9], G[9 + i])));
+      for (int j = 0; j < 3; ++j) A[4 * i + j] = E[3 * i + j] - Rgs[3 * i + j];
+      A[4 * i + 3] = E[9 + i] - tgs[i];
+    }
+    auto d2 = [&](int j) {
+      const double x = s_v[0][j], y = s_v[1][j], z = s_v[2][j];
+      const double dx = aff(A, 0, x, y, z), dy = aff(A, 1, x, y, z), dz = aff(A, 2, x, y, z);
+      return fma(dz, dz, fma(dy, dy, dx * dx));
+    };
+    for (int v0 = 0; v0 < nv; v0 += kPoseThreads) {
+      const int nb = min(kPoseThreads, nv - v0);
+      __syncthreads();
+      if (tid < nb) {
+        s_v[0][tid] = px[v0 + tid];
+        s_v[1][tid] = py[v0 + tid];
+        s_v[2][tid] = pz[v0 + tid];
       }
-      double A[12];
-      if (MODE == 0) {
-        // Difference-affine form: T_e p - T_gs p = (R_e - R_gs) p + (t_e - t_gs).
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-#pragma unroll
-          for (int j = 0; j < 3; ++j) A[4 * i + j] = E[3 * i + j] - Rgs[3 * i + j];
-          A[4 * i + 3] = E[9 + i] - tgs[i];
+      __syncthreads();
+      if (g < ng) {
+        int j = g;
+        for (; j + 3 * ng < nb; j += 4 * ng) {
+          m0 = fmax(m0, d2(j));
+          m1 = fmax(m1, d2(j + ng));
+          m2 = fmax(m2, d2(j + 2 * ng));
+          m3 = fmax(m3, d2(j + 3 * ng));
         }
-        for (int v = g; v < nv; v += ng) {
-          const double x = px[v], y = py[v], z = pz[v];
-          const double dx = aff(A, 0, x, y, z), dy = aff(A, 1, x, y, z), dz = aff(A, 2, x, y, z);
-          m = fmax(m, fma(dz, dz, fma(dy, dy, dx * dx)));
-        }
-      } else {
-        proj_mat(K, Rgs, tgs, A);
-        for (int v = g; v < nv; v += ng) {
-          const double x = px[v], y = py[v], z = pz[v];
-          const double ize = 1.0 / aff(Pe, 2, x, y, z);
-          const double izg = 1.0 / aff(A, 2, x, y, z);
-          const double du = aff(Pe, 0, x, y, z) * ize - aff(A, 0, x, y, z) * izg;
-          const double dv = aff(Pe, 1, x, y, z) * ize - aff(A, 1, x, y, z) * izg;
-          m = fmax(m, fma(dv, dv, du * du));
-        }
+        for (; j < nb; j += ng) m0 = fmax(m0, d2(j));
       }
     }
-    s_red[tid] = m;
-    __syncthreads();
+  } else {
+    double K[9], E[12], Pe[12], A[12];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) K[i] = Km[9 * b + i];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) E[i] = pe[12 * b + i];
+    proj_mat(K, E, E + 9, Pe);
+    proj_mat(K, Rgs, tgs, A);
+    auto d2 = [&](int j) {
+      const double x = s_v[0][j], y = s_v[1][j], z = s_v[2][j];
+      const double izg = rcp64(aff(A, 2, x, y, z));
+      const double du = s_v[3][j] - aff(A, 0, x, y, z) * izg;
+      const double dv = s_v[4][j] - aff(A, 1, x, y, z) * izg;
+      return fma(dv, dv, du * du);
+    };
+    for (int v0 = 0; v0 < nv; v0 += kPoseThreads) {
+      const int nb = min(kPoseThreads, nv - v0);
+      __syncthreads();
+      if (tid < nb) {
+        const double x = px[v0 + tid], y = py[v0 + tid], z = pz[v0 + tid];
+        const double ize = rcp64(aff(Pe, 2, x, y, z));
+        s_v[0][tid] = x;
+        s_v[1][tid] = y;
+        s_v[2][tid] = z;
+        s_v[3][tid] = aff(Pe, 0, x, y, z) * ize;
+        s_v[4][tid] = aff(Pe, 1, x, y, z) * ize;
+      }
+      __syncthreads();
+      if (g < ng) {
+        int j = g;
+        for (; j + ng < nb; j += 2 * ng) {
+          m0 = fmax(m0, d2(j));
+          m1 = fmax(m1, d2(j + ng));
+        }
+        if (j < nb) m2 = fmax(m2, d2(j));
+      }
+    }
+  }
+  s_red[tid] = fmax(fmax(m0, m1), fmax(m2, m3));
+  __syncthreads();
+  if (tid < 64) {  // sp <= 64: the unit's symmetries live in wave 0
+    double mn = INFINITY;
     if (tid < sp) {
       double mx = -INFINITY;
       for (int gg = 0; gg < ng; ++gg) mx = fmax(mx, s_red[gg * sp + tid]);
-      s_symmax[tid] = mx;
+      mn = mx;
     }
-    __syncthreads();
-    if (tid < 64) {
-      double mn = INFINITY;
-      for (int i = tid; i < sp; i += 64) mn = fmin(mn, s_symmax[i]);
-      mn = wave_min(mn);
-      best = fmin(best, mn);
-    }
-    __syncthreads();
+    mn = wave_min(mn);
+    if (tid == 0)
+      atomicMin((unsigned long long*)&out[b], (unsigned long long)__double_as_longlong(mn));
   }
-  if (tid == 0) out[b] = sqrt(best);
 }
 
 template <int MODE>  // 0 = ADD, 1 = PROJ
@@ -284,15 +352,20 @@ __global__ __launch_bounds__(kPoseThreads) void k_adi(const ObjDesc* __restrict_
   }
 }
 
-hipError_t launch_sym_error(int mode, const ObjDesc* objs, int64_t n, const int32_t* slots,
-                            const double* pe, const double* pg, const double* K, double* out,
-                            hipStream_t s) {
+hipError_t launch_sym_error(int mode, const ObjDesc* objs, int max_ns, int64_t n,
+                            const int32_t* slots, const double* pe, const double* pg,
+                            const double* K, double* out, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  dim3 grid((unsigned)n), block(kPoseThreads);
+  const int nch = (max(max_ns, 1) + kSymChunk - 1) / kSymChunk;
+  if ((int64_t)nch * n > 0x7FFFFFFF) return hipErrorInvalidValue;
+  const dim3 gfix((unsigned)((n + 255) / 256)), bfix(256);
+  hipLaunchKernelGGL(k_sym_init, gfix, bfix, 0, s, out, n);
+  dim3 grid((unsigned)(n * nch)), block(kPoseThreads);
   if (mode == 0)
-    hipLaunchKernelGGL(k_sym_error<0>, grid, block, 0, s, objs, slots, pe, pg, K, out);
+    hipLaunchKernelGGL(k_sym_error<0>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch);
   else
-    hipLaunchKernelGGL(k_sym_error<1>, grid, block, 0, s, objs, slots, pe, pg, K, out);
+    hipLaunchKernelGGL(k_sym_error<1>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch);
+  hipLaunchKernelGGL(k_sym_finish, gfix, bfix, 0, s, out, n);
   return hipGetLastError();
 }
 

@@ -53,6 +53,7 @@ struct bopx_ctx {
   ObjDesc* d_desc = nullptr;
   size_t desc_cap = 0;
   int max_nf = 0;
+  int max_ns = 0;  // most symmetries of a live object (MSSD/MSPD grid)
   DevBuf ws;  // scratch for host-buffer calls
 };
 
@@ -122,7 +123,7 @@ static size_t carve_size(std::initializer_list<size_t> bytes) {
 
 int sync_desc(bopx_ctx* c) {
   std::vector<ObjDesc> h(c->objs.size());
-  int max_nf = 0;
+  int max_nf = 0, max_ns = 0;
   for (size_t i = 0; i < c->objs.size(); ++i) {
     const Object& o = c->objs[i];
     ObjDesc d{};
@@ -140,10 +141,12 @@ int sync_desc(bopx_ctx* c) {
       d.nm = (int)o.nm;
       d.ns = (int)o.ns;
       max_nf = std::max(max_nf, (int)o.nf);
+      max_ns = std::max(max_ns, (int)o.ns);
     }
     h[i] = d;
   }
   c->max_nf = max_nf;
+  c->max_ns = max_ns;
   if (h.size() > c->desc_cap) {
     if (c->d_desc) HIPCHK(c, hipFree(c->d_desc));
     size_t cap = std::max<size_t>(64, h.size() * 2);
@@ -470,7 +473,7 @@ static int point_batch(bopx_ctx* c, int kind, int64_t n, const int32_t* obj_ids,
   if (needK) HIPCHK(c, hipMemcpyAsync(d_K, K, 72 * n, hipMemcpyHostToDevice, s));
   hipError_t e;
   if (kind <= 1)
-    e = bopx::launch_sym_error(kind, c->d_desc, n, d_s, d_pe, d_pg, d_K, d_out, s);
+    e = bopx::launch_sym_error(kind, c->d_desc, c->max_ns, n, d_s, d_pe, d_pg, d_K, d_out, s);
   else if (kind == 3)
     e = bopx::launch_adi(c->d_desc, n, d_s, d_pe, d_pg, d_out, s);
   else
@@ -506,7 +509,7 @@ int bopx_mssd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doub
                         const double* pg, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
   if (int r = set_dev(c)) return r;
-  HIPCHK(c, bopx::launch_sym_error(0, c->d_desc, n, slots, pe, pg, nullptr, out,
+  HIPCHK(c, bopx::launch_sym_error(0, c->d_desc, c->max_ns, n, slots, pe, pg, nullptr, out,
                                    pick_stream(c, stream)));
   return BOPX_OK;
 }
@@ -514,7 +517,7 @@ int bopx_mspd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doub
                         const double* pg, const double* K, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
   if (int r = set_dev(c)) return r;
-  HIPCHK(c, bopx::launch_sym_error(1, c->d_desc, n, slots, pe, pg, K, out, pick_stream(c, stream)));
+  HIPCHK(c, bopx::launch_sym_error(1, c->d_desc, c->max_ns, n, slots, pe, pg, K, out, pick_stream(c, stream)));
   return BOPX_OK;
 }
 int bopx_add_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
