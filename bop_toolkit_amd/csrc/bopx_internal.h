@@ -34,6 +34,7 @@ constexpr int kMeshletVerts = 64;   // unique vertices per meshlet (one per lane
 #endif
 constexpr int kMaxMeshlets = BOPX_MAX_MESHLETS;  // per object (VSD)
 constexpr int kMaxTaus = 16;
+constexpr int kVsdMaxTiles = 2048;  // k_vsd keeps 16-bit per-lane tau counters
 constexpr int kTileW = BOPX_TILE_W;  // VSD screen tile (LDS-resident q pair)
 constexpr int kTileH = BOPX_TILE_H;
 constexpr int kTileStride = kTileW + 1;  // LDS row pitch of a q tile (dwords)
@@ -69,7 +70,7 @@ struct VsdArgs {
   double delta64;
   int n_tau;
   int normalized;
-  int ablate;  // timing-only diagnostics (BOPX_VSD_ABLATE): bit0 skip raster, bit1 skip pixels
+  int ablate;  // BOPX_VSD_ABLATE, read only by -DBOPX_VSD_DIAG=1 builds (kern_vsd.hip)
   double taus[kMaxTaus];
 };
 

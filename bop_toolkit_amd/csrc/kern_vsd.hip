@@ -35,15 +35,21 @@ constexpr int kVsdThreads = BOPX_VSD_THREADS;
 
 // Workload counters for the timing diagnostics (BOPX_VSD_ABLATE bit 2). Not
 // part of the C-ABI; read with bopx_debug_vsd_stats.
-__device__ unsigned long long g_vsd_stats[8];
+__device__ unsigned long long g_vsd_stats[16];
 // Diagnostic phase clocks (BOPX_VSD_ABLATE bit 3; s_memtime, summed over waves):
 // [0] clear+coeffs, [1] list, [2] raster work, [3] raster barrier wait,
 // [4] pixel work, [5] pixel barrier wait, [6] pre-loop, [7] epilogue; raster work
 // split: [8] vertex staging, [9] bbox test + compaction, [10] set-up, [11] walk.
 __device__ unsigned long long g_vsd_time[16];
+// Diagnostics are compiled in only with -DBOPX_VSD_DIAG=1 (tools/vsd_stats.py
+// loads such a variant); the product kernel carries none of their state.
+#ifndef BOPX_VSD_DIAG
+#define BOPX_VSD_DIAG 0
+#endif
+#define VSD_DIAG(bit) (BOPX_VSD_DIAG && (a.ablate & (bit)))
 #define VSD_STAMP(k)                                              \
   do {                                                            \
-    if (a.ablate & 8) {                                           \
+    if (VSD_DIAG(8)) {                                            \
       const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
       ph[k] += _t - t_prev;                                       \
       t_prev = _t;                                                \
@@ -124,6 +130,9 @@ constexpr int kVsdWaves = kVsdThreads / 64;
 #define BOPX_VSD_GROUP 2
 #endif
 constexpr int kRowWin = 256;  // row items numbered per window (LDS owner map)
+constexpr int kPixPerWave = kTileW * kTileH / kVsdThreads * 64;  // covered-pixel list
+static_assert(sizeof(RRow) * 64 * kVsdWaves >= 2 * kPixPerWave * kVsdWaves,
+              "pixel lists overlay the raster records");
 constexpr int kGroup = BOPX_VSD_GROUP;  // (pose, meshlet) entries staged together per wave step
 constexpr int kRectsPerThread = 2 * kMaxMeshlets / kVsdThreads;
 
@@ -151,7 +160,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned long long ph[16] = {}, t_prev = 0;
-  if (a.ablate & 8) t_prev = __builtin_amdgcn_s_memtime();
+  if (VSD_DIAG(8)) t_prev = __builtin_amdgcn_s_memtime();
   const ObjDesc o = a.objs[a.slots[b]];
   const int W = a.width, H = a.height, nm = o.nm;
   // Object arrays live in global memory: address-space-1 views give
@@ -199,17 +208,19 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   const int rx0 = s_roi[0], ry0 = s_roi[1], rx1 = s_roi[2], ry1 = s_roi[3];
 
   uint32_t c_union = 0, c_inter = 0;
-  uint32_t c_tau[kMaxTaus];
+  // step cost: two 16-bit per-tau counters per register (a lane evaluates at
+  // most kTileW * kTileH / kVsdThreads pixels per tile, <= kVsdMaxTiles tiles)
+  uint32_t c_tau[kMaxTaus / 2];
   double lin[kMaxTaus];
 #pragma unroll
   for (int k = 0; k < kMaxTaus; ++k) {
-    c_tau[k] = 0;
+    if (k < kMaxTaus / 2) c_tau[k] = 0;
     lin[k] = 0.0;
   }
 
   if (rx0 <= rx1 && ry0 <= ry1) {
     const int ntx = (rx1 - rx0 + kTileW) / kTileW, nty = (ry1 - ry0 + kTileH) / kTileH;
-    if ((a.ablate & 4) && tid == 0) atomicAdd(&g_vsd_stats[0], (unsigned long long)(ntx * nty));
+    if (VSD_DIAG(4) && tid == 0) atomicAdd(&g_vsd_stats[0], (unsigned long long)(ntx * nty));
     VSD_STAMP(6);
     for (int t = 0; t < ntx * nty; ++t) {
       const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
@@ -241,7 +252,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       // three fixed-stride vertex blocks once (lane = vertex) into LDS, tests
       // every triangle's bbox against the tile, compacts the hits (ballot rank)
       // and only then sets up and rasterises them, one triangle per lane.
-      const int nl = __builtin_amdgcn_readfirstlane((a.ablate & 1) ? 0 : s_nlist);
+      const int nl = __builtin_amdgcn_readfirstlane(VSD_DIAG(1) ? 0 : s_nlist);
       for (;;) {
         int base = 0;
         if (lane == 0) base = atomicAdd(&s_next, kGroup);
@@ -280,7 +291,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
           cnt += __popcll(bal);
         }
         wave_lds_sync();
-        if ((a.ablate & 4) && lane == 0) atomicAdd(&g_vsd_stats[1], (unsigned long long)kGroup);
+        if (VSD_DIAG(4) && lane == 0) atomicAdd(&g_vsd_stats[1], (unsigned long long)kGroup);
         VSD_STAMP(9);
         for (int c0 = 0; c0 < cnt; c0 += 64) {
           // Set-up, one triangle per lane.
@@ -301,7 +312,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
             }
           }
           VSD_STAMP(10);
-          if (a.ablate & 4) {
+          if VSD_DIAG(4) {
             if (ok) {
               atomicAdd(&g_vsd_stats[2], 1ull);
               atomicAdd(&g_vsd_stats[3], (unsigned long long)(cc1 - cc0 + 1) * (rr1 - rr0 + 1));
@@ -311,7 +322,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
           if (ok && !T.small) {  // extent >= 128 px: int64 edges, walked by its own lane
             uint32_t* dep = s_dep[r];
             r_raster(T, cc0, cc1, rr0, rr1, [&](int col, int row, float q) {
-              if (a.ablate & 4) atomicAdd(&g_vsd_stats[5], 1ull);
+              if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], 1ull);
               atomicMax(&dep[(row - ty0) * kTileStride + (col - tx0)], __float_as_uint(q));
             });
           }
@@ -334,11 +345,23 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
               s_own[wave][k - wb] = (uint8_t)lane;
             wave_lds_sync();
             const int wn = min(nrow - wb, kRowWin);
+            if VSD_DIAG(4) {  // passes, sum over passes of the widest row
+              for (int p0 = 0; p0 < wn; p0 += 64) {
+                int wmax = p0 + lane < wn
+                               ? (int)((s_rec[wave][s_own[wave][p0 + lane]].meta >> 12) & 63u) + 1
+                               : 0;
+                for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, __shfl_xor(wmax, off, 64));
+                if (lane == 0) {
+                  atomicAdd(&g_vsd_stats[7], 1ull);
+                  atomicAdd(&g_vsd_stats[8], (unsigned long long)wmax);
+                }
+              }
+            }
             for (int p = lane; p < wn; p += 64) {
               const RRow rec = s_rec[wave][s_own[wave][p]];
               r_walk_row(rec, wb + p - (int)(rec.meta >> 19),
                          [&](int pose, int col, int row, float q) {
-                           if (a.ablate & 4) atomicAdd(&g_vsd_stats[5], 1ull);
+                           if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], 1ull);
                            atomicMax(&s_dep[pose][row * kTileStride + col], __float_as_uint(q));
                          });
             }
@@ -351,14 +374,28 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       VSD_STAMP(2);
       __syncthreads();
       VSD_STAMP(3);
-      // 3. per-pixel distances, visibility masks, counters.
-      for (int p = tid; p < ((a.ablate & 2) ? 0 : kTileW * kTileH); p += kVsdThreads) {
+      // 3. per-pixel distances, visibility masks, counters. Each wave first
+      // compacts its covered pixels (rows wave, wave + 8, ...) into its own
+      // list (ballot rank; the raster records are dead here), then evaluates
+      // the list with full lanes. Wave-private: no block barrier, and the
+      // pixel -> lane assignment is fixed (deterministic float64 sums).
+      uint16_t* pix = reinterpret_cast<uint16_t*>(&s_rec[0][0]) + wave * kPixPerWave;
+      int npix = 0;
+      for (int p = tid; p < (VSD_DIAG(2) ? 0 : kTileW * kTileH); p += kVsdThreads) {
+        const int ps = (p / kTileW) * kTileStride + p % kTileW;
+        const bool cov = ty0 + p / kTileW <= ty1 && tx0 + p % kTileW <= tx1 &&
+                         (s_dep[0][ps] | s_dep[1][ps]) != 0u;
+        const unsigned long long bal = __ballot(cov);
+        if (cov) pix[npix + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)p;
+        npix += __popcll(bal);
+      }
+      wave_lds_sync();
+      for (int i = lane; i < npix; i += 64) {
+        const int p = pix[i];
         const int row = ty0 + p / kTileW, col = tx0 + p % kTileW;
-        if (row > ty1 || col > tx1) continue;
         const int ps = (p / kTileW) * kTileStride + p % kTileW;
         const uint32_t qe = s_dep[0][ps], qg = s_dep[1][ps];
-        if ((qe | qg) == 0u) continue;  // neither pose covers this pixel
-        if (a.ablate & 4) atomicAdd(&g_vsd_stats[6], 1ull);
+        if VSD_DIAG(4) atomicAdd(&g_vsd_stats[6], 1ull);
         const float de = qe ? 1.0f / __uint_as_float(qe) : 0.0f;
         const float dg = qg ? 1.0f / __uint_as_float(qg) : 0.0f;
         const float dtest = frame[(int64_t)row * W + col];
@@ -379,7 +416,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
           for (int k = 0; k < kMaxTaus; ++k) {
             if (k < a.n_tau) {
               if (COST == 0) {
-                c_tau[k] += (dd >= a.taus[k]);
+                c_tau[k >> 1] += (uint32_t)(dd >= a.taus[k]) << (16 * (k & 1));
               } else {
                 const double cst = dd / a.taus[k];
                 lin[k] += cst > 1.0 ? 1.0 : cst;
@@ -398,10 +435,12 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   __syncthreads();  // s_cnt / s_lin alias the depth tiles
   c_union = wave_sum_u32(c_union);
   c_inter = wave_sum_u32(c_inter);
+  uint32_t tau_sum[kMaxTaus];
 #pragma unroll
   for (int k = 0; k < kMaxTaus; ++k) {
+    tau_sum[k] = 0;
     if (COST == 0)
-      c_tau[k] = wave_sum_u32(c_tau[k]);
+      tau_sum[k] = wave_sum_u32((c_tau[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
     else
       lin[k] = wave_sum_f64(lin[k]);
   }
@@ -410,13 +449,13 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
     s_cnt[wave][1] = c_inter;
 #pragma unroll
     for (int k = 0; k < kMaxTaus; ++k) {
-      s_cnt[wave][2 + k] = c_tau[k];
+      s_cnt[wave][2 + k] = tau_sum[k];
       s_lin[wave][k] = lin[k];
     }
   }
   __syncthreads();
   VSD_STAMP(7);
-  if ((a.ablate & 8) && lane == 0)
+  if (VSD_DIAG(8) && lane == 0)
     for (int k = 0; k < 16; ++k) atomicAdd(&g_vsd_time[k], ph[k]);
   if (tid == 0) {
     uint64_t un = 0, in = 0;
@@ -445,7 +484,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
 hipError_t read_vsd_stats(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vsd_stats), sizeof(g_vsd_stats));
   if (e == hipSuccess)
-    e = hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(g_vsd_time), sizeof(g_vsd_time));
+    e = hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(g_vsd_time), sizeof(g_vsd_time));
   if (e != hipSuccess || !reset) return e;
   unsigned long long z[16] = {};
   e = hipMemcpyToSymbol(HIP_SYMBOL(g_vsd_stats), z, sizeof(g_vsd_stats));

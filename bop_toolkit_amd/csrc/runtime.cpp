@@ -542,6 +542,10 @@ static int fill_vsd_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height, d
                          int cost_type) {
   if (width <= 0 || height <= 0 || width > 32767 || height > 32767)
     return fail(c, BOPX_E_INVALID, "bad image size %dx%d", width, height);
+  if ((int64_t)((width + bopx::kTileW - 1) / bopx::kTileW) *
+          ((height + bopx::kTileH - 1) / bopx::kTileH) > bopx::kVsdMaxTiles)
+    return fail(c, BOPX_E_UNSUPPORTED, "image %dx%d exceeds the fused VSD kernel's %d tiles",
+                width, height, bopx::kVsdMaxTiles);
   if (cost_type != BOPX_COST_STEP && cost_type != BOPX_COST_TLINEAR)
     return fail(c, BOPX_E_INVALID, "Unknown pixel matching cost.");
   if (int r = check_taus(c, taus, n_tau)) return r;
@@ -807,9 +811,10 @@ int bopx_visib_mask(bopx_ctx* c, int64_t n, const double* d_test, const double* 
   return BOPX_OK;
 }
 
-// Diagnostics (not in include/bopx.h): k_vsd workload counters gathered when
-// BOPX_VSD_ABLATE has bit 2 set: tiles, meshlet entries, triangle set-ups,
-// bbox iterations, sum of per-wave max iterations, fragments, covered pixels.
+// Diagnostics (not in include/bopx.h): out[0..15] = k_vsd workload counters
+// (BOPX_VSD_ABLATE bit 2: tiles, meshlet entries, triangle set-ups, bbox
+// pixels, row items, fragments, covered pixels, row passes, sum of per-pass
+// widest rows), out[16..31] = phase clocks (bit 3). out holds 32 values.
 int bopx_debug_vsd_stats(bopx_ctx* c, unsigned long long* out, int reset) {
   if (!c || !out) return BOPX_E_INVALID;
   if (int r = set_dev(c)) return r;

@@ -1,13 +1,23 @@
 """Workload counters of one k_vsd launch on the bench workload (diagnostics).
 
-    BOPX_VSD_ABLATE=4 python tools/vsd_stats.py [--tuples N]
+    BOPX_VSD_ABLATE=4 python tools/vsd_stats.py [--tuples N]   # counters
+    BOPX_VSD_ABLATE=8 python tools/vsd_stats.py [--tuples N]   # phase clocks
+
+Uses the -DBOPX_VSD_DIAG=1 build (make diag), not the product library.
 """
 import ctypes
 import os
 import sys
 
 os.environ.setdefault("BOPX_VSD_ABLATE", "4")
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+# counters and clocks exist only in the diagnostic build of the library
+if "BOPX_LIB" not in os.environ:
+  import subprocess
+  subprocess.run(["make", "-s", "-C", os.path.join(REPO, "bop_toolkit_amd", "csrc"), "diag"],
+                 check=True)
+  os.environ["BOPX_LIB"] = os.path.join(REPO, "bop_toolkit_amd", "lib", "diag", "libbopx_diag.so")
 sys.argv += [] if "--tuples" in sys.argv else ["--tuples", "1200"]
 
 import numpy as np  # noqa: E402
@@ -24,22 +34,22 @@ def main():
   n, d = bench.build_workload(ev, objs, args, 0, torch)
   fn = ev.ctx.lib.bopx_debug_vsd_stats
   fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-  st = (ctypes.c_ulonglong * 24)()
+  st = (ctypes.c_ulonglong * 32)()
   fn(ev.ctx.h, st, 1)
   ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"], d["frames"], d["cam"],
          bench.DELTA, bench.TAUS, d["diameters"])
   torch.cuda.synchronize()
   fn(ev.ctx.h, st, 1)
   names = ["tiles", "meshlet_entries", "tri_setups", "bbox_iters", "rows",
-           "fragments", "covered_px"]
+           "fragments", "covered_px", "row_passes", "pass_max_w_sum"]
   for i, k in enumerate(names):
     print("%-20s total %14d  per tuple %12.1f" % (k, st[i], st[i] / n))
   ph = ["clear+coeffs", "list", "raster work", "raster barrier", "pixel work",
         "pixel barrier", "pre-loop", "epilogue", "r:stage", "r:compact", "r:setup", "r:walk"]
-  tot = sum(st[8 + i] for i in range(16))
+  tot = sum(st[16 + i] for i in range(16))
   for i, k in enumerate(ph):
-    print("phase %-16s %6.1f %%  (%.3g cycles/wave-tuple)" % (k, 100.0 * st[8 + i] / max(1, tot),
-                                                           st[8 + i] / n / 8))
+    print("phase %-16s %6.1f %%  (%.3g cycles/wave-tuple)" % (k, 100.0 * st[16 + i] / max(1, tot),
+                                                           st[16 + i] / n / 8))
   roi = bench.roi_pixels(objs, d["host"]["obj"], [d["host"]["pe"], d["host"]["pg"]],
                          bench.synth_K() if hasattr(bench, "synth_K") else __import__(
                              "bop_toolkit_amd.synth", fromlist=["YCBV_K"]).YCBV_K)
