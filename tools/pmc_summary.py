@@ -5,9 +5,12 @@
 Per kernel: mean value per dispatch of every counter collected (each DIR is one
 rocprofv3 pass). HBM traffic per launch follows MI355X_MICROARCH.md §HBM:
 FETCH_SIZE and WRITE_SIZE are in KiB (TCC_EA0_RDREQ/_WRREQ based); on gfx950
-FETCH_SIZE under-reports wide (16 B/lane) coalesced streams by 2x and other
-access widths are uncalibrated, so both the raw sum and the 2x-corrected read
-side are recorded, the corrected one being used as `hbm_bytes_per_launch`.
+FETCH_SIZE reports half the bytes of a streaming read. The guide calibrates
+16 B/lane; tools/hbm_calib.hip calibrates the 4 B/lane loads k_vsd also uses
+(profiles/r01_hbm_calib.csv: 1 GiB streamed -> 524,291 KiB at 4 B/lane and
+524,298 KiB at 16 B/lane, i.e. x2 for both). Both the raw sum and the
+2x-corrected read side are recorded; the corrected one is
+`hbm_bytes_per_launch`.
 """
 import csv
 import glob
