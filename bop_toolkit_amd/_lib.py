@@ -59,6 +59,7 @@ SIGNATURES = {
     "bopx_mspd_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _P, _P]),
     "bopx_add_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _P]),
     "bopx_adi_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _P]),
+    "bopx_proj_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _P, _P]),
     "bopx_vsd_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _P, _I, _I, _P, _D, _I, _d, _I, _I,
                                 _P, _I, _P, _P]),
     "bopx_depth_clear_dev": (_I, [_CTX, _P, _I64, _P]),

@@ -94,6 +94,13 @@ class BatchEvaluator:
                   _stream(self.device))
     return out
 
+  def proj(self, slots, pose_est, pose_gt, K, out=None):
+    n = slots.numel()
+    out = self._out(n) if out is None else out
+    self.ctx.call("bopx_proj_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(K),
+                  _p(out), _stream(self.device))
+    return out
+
   def vsd(self, slots, pose_est, pose_gt, frame_idx, frames, cam, delta, taus, diameters,
           normalized_by_diameter=True, cost_type="step", out=None, delta_flags=0):
     n = slots.numel()

@@ -536,6 +536,15 @@ int bopx_adi_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doubl
   return BOPX_OK;
 }
 
+int bopx_proj_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
+                        const double* pg, const double* K, double* out, void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (int r = set_dev(c)) return r;
+  HIPCHK(c, bopx::launch_mean_error(1, c->d_desc, n, slots, pe, pg, K, out,
+                                    pick_stream(c, stream)));
+  return BOPX_OK;
+}
+
 // ------------------------------------------------------------------------ VSD
 static int fill_vsd_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height, double delta,
                          int flags, const double* taus, int n_tau, int normalized,

@@ -1,0 +1,340 @@
+"""Batched counterpart of scripts/eval_calc_errors.py.
+
+Same parameters, command line, tuple enumeration and output files as the
+reference script (eval_calc_errors.py:23-136 parameters, :137-424 loop):
+
+  * estimates per (scene, image, object) sorted by score, descending and
+    stable, est_id = index in the per-(image, object) list; the n_top rule
+    (0 = all, -1 = target inst_count, N = top N) (:247-277);
+  * errors against every GT instance of the same object in the image (:288-290);
+  * the host gates and their fills: VSD/CUS 1.0 when the projected bounding
+    spheres do not overlap, AD*/MSSD inf when the centres are a diameter or
+    more apart; MSPD ungated (:296-339);
+  * errors_{scene:06d}.json per error signature, VSD split per tau (:380-415),
+    written with inout.save_json's one-element-per-line layout.
+
+What differs is the evaluation: instead of one pose_error call per tuple, the
+gated-in tuples of a scene go to the GPU as one batch per error type
+(bop_toolkit_amd.batch: k_vsd fuses both renders, the three distance images,
+both visibility masks and the per-tau costs; MSSD/MSPD/ADD/ADI/PROJ are one
+launch each). RE/TE are 3x3 host arithmetic, kept on the host as in the
+reference. The HIP rasteriser replaces the OpenGL renderer, whatever
+--renderer_type says.
+
+    python -m bop_toolkit_amd.eval_calc_errors --error_type vsd --result_filenames ...
+"""
+import argparse
+import copy
+import os
+import time
+
+import numpy as np
+
+from . import dataset_params, inout, misc, pose_error
+
+DEFAULTS = {
+    "n_top": 1,
+    "error_type": "vsd",
+    "vsd_deltas": {"hb": 15, "icbin": 15, "icmi": 15, "itodd": 5, "lm": 15, "lmo": 15,
+                   "ruapc": 15, "tless": 15, "tudl": 15, "tyol": 15, "ycbv": 15, "hope": 15},
+    "vsd_taus": list(np.arange(0.05, 0.51, 0.05)),
+    "vsd_normalized_by_diameter": True,
+    "max_sym_disc_step": 0.01,
+    "skip_missing": True,
+    "renderer_type": "vispy",
+    "result_filenames": ["/path/to/csv/with/results"],
+    "results_path": "/path/to/results",
+    "eval_path": "/path/to/eval/folder",
+    "datasets_path": os.environ.get("BOP_PATH", "/path/to/bop/datasets"),
+    "targets_filename": "test_targets_bop19.json",
+    "out_errors_tpath": os.path.join("{eval_path}", "{result_name}", "{error_sign}",
+                                     "errors_{scene_id:06d}.json"),
+}
+
+POINT_ERRORS = ("ad", "add", "adi", "mssd", "mspd", "proj")
+ERROR_TYPES = ("vsd", "mssd", "mspd", "ad", "add", "adi", "proj", "rete", "re", "te")
+
+
+def parse_args(argv=None):
+  """The reference's command line (eval_calc_errors.py:89-129), same
+  defaults and the same string-to-type conversions."""
+  p = copy.deepcopy(DEFAULTS)
+  ap = argparse.ArgumentParser()
+  ap.add_argument("--n_top", default=p["n_top"])
+  ap.add_argument("--error_type", default=p["error_type"])
+  ap.add_argument("--vsd_deltas",
+                  default=",".join("{}:{}".format(k, v) for k, v in p["vsd_deltas"].items()))
+  ap.add_argument("--vsd_taus", default=",".join(map(str, p["vsd_taus"])))
+  ap.add_argument("--vsd_normalized_by_diameter", default=p["vsd_normalized_by_diameter"])
+  ap.add_argument("--max_sym_disc_step", default=p["max_sym_disc_step"])
+  ap.add_argument("--skip_missing", default=p["skip_missing"])
+  ap.add_argument("--renderer_type", default=p["renderer_type"])
+  ap.add_argument("--result_filenames", default=",".join(p["result_filenames"]))
+  ap.add_argument("--results_path", default=p["results_path"])
+  ap.add_argument("--eval_path", default=p["eval_path"])
+  ap.add_argument("--datasets_path", default=p["datasets_path"])
+  ap.add_argument("--targets_filename", default=p["targets_filename"])
+  ap.add_argument("--out_errors_tpath", default=p["out_errors_tpath"])
+  a = ap.parse_args(argv)
+  p["n_top"] = int(a.n_top)
+  p["error_type"] = str(a.error_type)
+  p["vsd_deltas"] = {str(e.split(":")[0]): float(e.split(":")[1])
+                     for e in a.vsd_deltas.split(",")}
+  p["vsd_taus"] = list(map(float, a.vsd_taus.split(",")))
+  p["vsd_normalized_by_diameter"] = bool(a.vsd_normalized_by_diameter)
+  p["max_sym_disc_step"] = float(a.max_sym_disc_step)
+  p["skip_missing"] = bool(a.skip_missing)
+  p["renderer_type"] = str(a.renderer_type)
+  p["result_filenames"] = a.result_filenames.split(",")
+  for k in ("results_path", "eval_path", "datasets_path", "targets_filename",
+            "out_errors_tpath"):
+    p[k] = str(getattr(a, k))
+  return p
+
+
+def log(s):
+  misc.log(s)
+
+
+# ----------------------------------------------------------------- enumeration
+def organize(targets, ests):
+  """targets_org[scene][im][obj] = target; ests_org[scene][im][obj] = [est]
+  (insertion order, eval_calc_errors.py:207-228)."""
+  targets_org, ests_org = {}, {}
+  for t in targets:
+    targets_org.setdefault(t["scene_id"], {}).setdefault(t["im_id"], {})[t["obj_id"]] = t
+  for e in ests:
+    ests_org.setdefault(e["scene_id"], {}).setdefault(e["im_id"], {}).setdefault(
+        e["obj_id"], []).append(e)
+  return targets_org, ests_org
+
+
+def scene_records(p, scene_id, scene_targets, ests_org, scene_gt):
+  """The records of one scene in output order, each with the GT ids it is
+  evaluated against (eval_calc_errors.py:238-290)."""
+  recs = []
+  n_ests = 0
+  for im_id, im_targets in scene_targets.items():
+    for obj_id, target in im_targets.items():
+      if p["n_top"] == 0:
+        n_top = None
+      elif p["n_top"] == -1:
+        n_top = target["inst_count"]
+      else:
+        n_top = p["n_top"]
+      obj_ests = ests_org.get(scene_id, {}).get(im_id, {}).get(obj_id, [])
+      if not p["skip_missing"] and len(obj_ests) < n_top:
+        raise ValueError(
+            "Not enough estimates for scene: {}, im: {}, obj: {} (provided: {}, expected: {})"
+            .format(scene_id, im_id, obj_id, len(obj_ests), n_top))
+      ranked = sorted(enumerate(obj_ests), key=lambda x: x[1]["score"], reverse=True)
+      ranked = ranked[slice(0, n_top)]
+      n_ests += len(ranked)
+      gts = [(gt_id, gt) for gt_id, gt in enumerate(scene_gt[im_id]) if gt["obj_id"] == obj_id]
+      for est_id, est in ranked:
+        recs.append({"im_id": im_id, "obj_id": obj_id, "est_id": est_id, "score": est["score"],
+                     "R": est["R"], "t": est["t"], "gts": gts})
+  return recs, n_ests
+
+
+def gate(error_type, diameter, t_e, t_g):
+  """Host pre-check of one tuple: None = evaluate, else the fill value list
+  (eval_calc_errors.py:292-339). n_tau is applied by the caller for VSD."""
+  if error_type in ("vsd", "cus"):
+    if not misc.overlapping_sphere_projections(0.5 * diameter, t_e.squeeze(), t_g.squeeze()):
+      return "vsd_fill"
+  elif error_type in ("ad", "add", "adi", "mssd"):
+    if not np.linalg.norm(t_e - t_g) < diameter:
+      return [float("inf")]
+  return None
+
+
+# ------------------------------------------------------------------ evaluation
+class Models:
+  """Objects of one dataset resident on the GPU (+ host-side info)."""
+
+  def __init__(self, ev, p, dp_model, models_info):
+    self.ev = ev
+    self.info = models_info
+    need_syms = p["error_type"] in ("mssd", "mspd")
+    self.sym_ids = set(dp_model["symmetric_obj_ids"] or [])
+    for obj_id in dp_model["obj_ids"]:
+      path = dp_model["model_tpath"].format(obj_id=obj_id)
+      if not os.path.exists(path):
+        continue
+      m = inout.load_ply(path)
+      syms = None
+      if need_syms:
+        syms = misc.get_symmetry_transformations(models_info[obj_id], p["max_sym_disc_step"])
+      dia = models_info[obj_id]["diameter"] if models_info is not None else None
+      ev.add_object(obj_id, m["pts"], m.get("faces"), syms, dia)
+
+
+def _pose12(R, t):
+  return np.concatenate([np.asarray(R, np.float64).reshape(9),
+                         np.asarray(t, np.float64).reshape(3)])
+
+
+def evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, models_info,
+             symmetric_ids):
+  """errors dict per record; the gated-in tuples of the scene are evaluated
+  as one GPU batch."""
+  et = p["error_type"]
+  n_tau = len(p["vsd_taus"])
+  errs = [dict() for _ in recs]
+  todo = []  # (record, gt_id, R_g, t_g)
+  for ri, r in enumerate(recs):
+    for gt_id, gt in r["gts"]:
+      R_g, t_g = gt["cam_R_m2c"], gt["cam_t_m2c"]
+      dia = models_info[r["obj_id"]]["diameter"] if models_info is not None else None
+      fill = gate(et, dia, r["t"], t_g)
+      if fill == "vsd_fill":
+        errs[ri][gt_id] = [1.0] * (n_tau if et == "vsd" else 1)
+      elif fill is not None:
+        errs[ri][gt_id] = fill
+      elif et in ("re", "te", "rete"):
+        e_re = pose_error.re(r["R"], R_g)
+        e_te = pose_error.te(r["t"], t_g)
+        errs[ri][gt_id] = {"re": [e_re], "te": [e_te], "rete": [e_re, e_te]}[et]
+      else:
+        errs[ri][gt_id] = None  # filled from the batch below
+        todo.append((ri, gt_id, R_g, t_g))
+  if not todo:
+    return errs
+  dev = ev.device
+  n = len(todo)
+  obj = np.array([recs[ri]["obj_id"] for ri, _, _, _ in todo], np.int32)
+  pe = np.stack([_pose12(recs[ri]["R"], recs[ri]["t"]) for ri, _, _, _ in todo])
+  pg = np.stack([_pose12(R_g, t_g) for _, _, R_g, t_g in todo])
+  T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+  slots = ev.slots(obj)
+  d_pe, d_pg = T(pe, torch.float64), T(pg, torch.float64)
+  if et == "vsd":
+    ims = sorted({recs[ri]["im_id"] for ri, _, _, _ in todo})
+    frame_of = {im: k for k, im in enumerate(ims)}
+    depths = []
+    cam = np.empty((len(ims), 4), np.float64)
+    for k, im_id in enumerate(ims):
+      d = inout.load_depth(dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id))
+      d *= scene_camera[im_id]["depth_scale"]  # float32 in place, eval_calc_errors.py:242-243
+      depths.append(d)
+      K = scene_camera[im_id]["cam_K"]
+      cam[k] = (K[0, 0], K[1, 1], K[0, 2], K[1, 2])
+    frames = T(np.stack(depths), torch.float32)
+    fidx = np.array([frame_of[recs[ri]["im_id"]] for ri, _, _, _ in todo], np.int32)
+    dia = np.array([models_info[o]["diameter"] for o in obj], np.float64)
+    delta = p["vsd_deltas"][dataset]
+    from . import runtime
+    out = ev.vsd(slots, d_pe, d_pg, T(fidx, torch.int32), frames, T(cam, torch.float64), delta,
+                 p["vsd_taus"], T(dia, torch.float64),
+                 normalized_by_diameter=p["vsd_normalized_by_diameter"], cost_type="step",
+                 delta_flags=runtime.delta_flags(delta))
+  elif et in ("mspd", "proj"):
+    K = np.stack([scene_camera[recs[ri]["im_id"]]["cam_K"].reshape(9) for ri, _, _, _ in todo])
+    fn = ev.mspd if et == "mspd" else ev.proj
+    out = fn(slots, d_pe, d_pg, T(K, torch.float64))
+  elif et == "mssd":
+    out = ev.mssd(slots, d_pe, d_pg)
+  elif et in ("ad", "add", "adi"):
+    use_adi = np.array([et == "adi" or (et == "ad" and int(o) in symmetric_ids) for o in obj])
+    out = torch.empty(n, dtype=torch.float64, device=dev)
+    for flag, fn in ((False, ev.add), (True, ev.adi)):
+      idx = np.nonzero(use_adi == flag)[0]
+      if len(idx):
+        ii = T(idx, torch.int64)
+        out[ii] = fn(slots[ii], d_pe[ii], d_pg[ii])
+  else:
+    raise ValueError("Unknown pose error function.")
+  vals = out.cpu().numpy().tolist()
+  for (ri, gt_id, _, _), v in zip(todo, vals):
+    errs[ri][gt_id] = v if isinstance(v, list) else [v]
+  return errs
+
+
+# ------------------------------------------------------------------------ main
+def run(p, device=0):
+  """Evaluate every result file of p; returns the written file paths."""
+  import torch
+  from .batch import BatchEvaluator
+
+  if p["error_type"] not in ERROR_TYPES:
+    raise ValueError("Unknown pose error function.")
+  written = []
+  ev = None
+  for result_filename in p["result_filenames"]:
+    log("Processing: {}".format(result_filename))
+    time_start = time.time()
+    result_name = os.path.splitext(os.path.basename(result_filename))[0]
+    info = result_name.split("_")
+    method = str(info[0])
+    ds = info[1].split("-")
+    dataset, split = str(ds[0]), str(ds[1])
+    split_type = str(ds[2]) if len(ds) > 2 else None
+    split_type_str = " - " + split_type if split_type is not None else ""
+    dp_split = dataset_params.get_split_params(p["datasets_path"], dataset, split, split_type)
+    dp_model = dataset_params.get_model_params(p["datasets_path"], dataset, "eval")
+    et = p["error_type"]
+    models_info = None
+    if et in ("ad", "add", "adi", "vsd", "mssd", "mspd", "cus"):
+      models_info = inout.load_json(dp_model["models_info_path"], keys_to_int=True)
+    if et not in ("re", "te", "rete"):
+      if ev is None:
+        ev = BatchEvaluator(device)
+      for o in list(ev.objects):
+        ev.ctx.remove_object(o)
+      ev.objects.clear()
+      log("Loading object models...")
+      Models(ev, p, dp_model, models_info)
+    targets = inout.load_json(os.path.join(dp_split["base_path"], p["targets_filename"]))
+    log("Loading pose estimates...")
+    ests = inout.load_bop_results(os.path.join(p["results_path"], result_filename))
+    targets_org, ests_org = organize(targets, ests)
+    sym_ids = set(dp_model["symmetric_obj_ids"] or [])
+    ests_counter = 0
+    for scene_id, scene_targets in targets_org.items():
+      scene_camera = inout.load_scene_camera(
+          dp_split["scene_camera_tpath"].format(scene_id=scene_id))
+      scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+      log("Calculating error {} - method: {}, dataset: {}{}, scene: {}".format(
+          et, method, dataset, split_type_str, scene_id))
+      recs, n_ests = scene_records(p, scene_id, scene_targets, ests_org, scene_gt)
+      ests_counter += n_ests
+      errs = evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
+                      models_info, sym_ids) if recs else []
+      scene_errs = [{"im_id": r["im_id"], "obj_id": r["obj_id"], "est_id": r["est_id"],
+                     "score": r["score"], "errors": e} for r, e in zip(recs, errs)]
+
+      def save(sign, content):
+        path = p["out_errors_tpath"].format(eval_path=p["eval_path"], result_name=result_name,
+                                           error_sign=sign, scene_id=scene_id)
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        log("Saving errors to: {}".format(path))
+        inout.save_json(path, content)
+        written.append(path)
+
+      if et == "vsd":
+        for k, tau in enumerate(p["vsd_taus"]):
+          sign = misc.get_error_signature(et, p["n_top"], vsd_delta=p["vsd_deltas"][dataset],
+                                          vsd_tau=tau)
+          save(sign, [dict(e, errors={g: [v[k]] for g, v in e["errors"].items()})
+                      for e in scene_errs])
+      else:
+        save(misc.get_error_signature(et, p["n_top"]), scene_errs)
+    log("Calculation of errors for {} estimates took {}s.".format(
+        ests_counter, time.time() - time_start))
+  log("Done.")
+  return written
+
+
+def main(argv=None):
+  p = parse_args(argv)
+  log("-----------")
+  log("Parameters:")
+  for k, v in p.items():
+    log("- {}: {}".format(k, v))
+  log("-----------")
+  run(p, int(os.environ.get("LOCAL_RANK", os.environ.get("BOPX_DEVICE", 0))))
+
+
+if __name__ == "__main__":
+  main()

@@ -127,3 +127,80 @@ def save_json(path, content):
       f.write("]")
     else:
       json.dump(content, f, sort_keys=True)
+
+
+def load_json(path, keys_to_int=False):
+  """JSON file; with keys_to_int, object keys that are (signed) integers
+  become ints (inout.py:66-82)."""
+  def hook(d):
+    return {int(k) if k.lstrip("-").isdigit() else k: v for k, v in d.items()}
+  with open(path, "r") as f:
+    return json.load(f, object_hook=hook) if keys_to_int else json.load(f)
+
+
+def load_depth(path):
+  """16-bit depth image (PNG, or TIFF for ITODD) as float32 (inout.py:39-46;
+  the reference reads it with imageio, here with Pillow)."""
+  from PIL import Image
+  with Image.open(path) as im:
+    return np.asarray(im).astype(np.float32)
+
+
+def load_cam_params(path):
+  """im_size (w, h), K and optional depth_scale of a camera.json (inout.py:116-137)."""
+  c = load_json(path)
+  cam = {"im_size": (c["width"], c["height"]),
+         "K": np.array([[c["fx"], 0.0, c["cx"]], [0.0, c["fy"], c["cy"]], [0.0, 0.0, 1.0]])}
+  if "depth_scale" in c:
+    cam["depth_scale"] = float(c["depth_scale"])
+  return cam
+
+
+def _as(d, key, shape):
+  if key in d:
+    d[key] = np.array(d[key], np.float64).reshape(shape)
+
+
+def load_scene_camera(path):
+  """scene_camera.json: per image cam_K (3x3), cam_R_w2c, cam_t_w2c as float64
+  arrays, other fields as stored (inout.py:140-160)."""
+  scene_camera = load_json(path, keys_to_int=True)
+  for cam in scene_camera.values():
+    _as(cam, "cam_K", (3, 3))
+    _as(cam, "cam_R_w2c", (3, 3))
+    _as(cam, "cam_t_w2c", (3, 1))
+  return scene_camera
+
+
+def load_scene_gt(path):
+  """scene_gt.json: per image a list of GT instances with cam_R_m2c (3x3) and
+  cam_t_m2c (3x1) float64 (inout.py:182-198)."""
+  scene_gt = load_json(path, keys_to_int=True)
+  for im_gt in scene_gt.values():
+    for gt in im_gt:
+      _as(gt, "cam_R_m2c", (3, 3))
+      _as(gt, "cam_t_m2c", (3, 1))
+  return scene_gt
+
+
+def load_bop_results(path, version="bop19"):
+  """BOP19 CSV results: scene_id,im_id,obj_id,score,R,t,time; a first line
+  containing the header is skipped (inout.py:221-261)."""
+  if version != "bop19":
+    raise ValueError("Unknown version of BOP results.")
+  header = "scene_id,im_id,obj_id,score,R,t,time"
+  results = []
+  with open(path, "r") as f:
+    for line_no, line in enumerate(f, 1):
+      if line_no == 1 and header in line:
+        continue
+      e = line.split(",")
+      if len(e) != 7:
+        raise ValueError("A line does not have 7 comma-sep. elements: {}".format(line))
+      results.append({
+          "scene_id": int(e[0]), "im_id": int(e[1]), "obj_id": int(e[2]),
+          "score": float(e[3]),
+          "R": np.array([float(x) for x in e[4].split()], np.float64).reshape((3, 3)),
+          "t": np.array([float(x) for x in e[5].split()], np.float64).reshape((3, 1)),
+          "time": float(e[6])})
+  return results

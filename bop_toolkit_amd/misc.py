@@ -131,3 +131,13 @@ def calc_pts_diameter(pts):
     d = ((pts[i:i + 2048, None, :] - pts[None, :, :]) ** 2).sum(-1)
     best = max(best, float(np.sqrt(d.max())))
   return best
+
+
+def log(s):
+  """Timestamped progress line, flushed (misc.py:18-33)."""
+  import datetime
+  import sys
+  now = datetime.datetime.now(datetime.timezone.utc)
+  sys.stdout.write("{}/{}|{:02d}:{:02d}:{:02d}: {}\n".format(
+      now.month, now.day, now.hour, now.minute, now.second, s))
+  sys.stdout.flush()

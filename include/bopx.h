@@ -157,6 +157,10 @@ int bopx_add_batch_dev(bopx_ctx* ctx, int64_t n, const int32_t* slots,
 int bopx_adi_batch_dev(bopx_ctx* ctx, int64_t n, const int32_t* slots,
                        const double* pose_est, const double* pose_gt, double* out,
                        void* stream);
+/* PROJ (pose_error.py:217-232); K n x 9 row-major. */
+int bopx_proj_batch_dev(bopx_ctx* ctx, int64_t n, const int32_t* slots,
+                        const double* pose_est, const double* pose_gt, const double* K,
+                        double* out, void* stream);
 int bopx_vsd_batch_dev(bopx_ctx* ctx, int64_t n, const int32_t* slots,
                        const double* pose_est, const double* pose_gt,
                        const int32_t* frame_idx, const float* frames, int width,

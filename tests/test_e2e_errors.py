@@ -1,0 +1,119 @@
+"""End-to-end parity of the batched error caller (bop_toolkit_amd.eval_calc_errors)
+with the reference's scripts/eval_calc_errors.py, pinned by the JSON files the
+reference wrote on the committed synthetic LM-O-layout dataset
+(tests/golden/gen_e2e.py).
+
+CPU: tuple enumeration (n_top, score sort, est_id), GT matching, host gates and
+their fills, the JSON layout. GPU: the whole caller, every error file compared
+with the reference's (VSD bit-identical text; point errors to float64
+rounding; RE/TE exact).
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from bop_toolkit_amd import dataset_params, eval_calc_errors as ece, inout, misc
+
+E2E = os.path.join(os.path.dirname(__file__), "golden", "e2e")
+RUNS = json.load(open(os.path.join(E2E, "runs.json")))
+
+
+def _params(et, n_top, eval_path="/nonexistent"):
+  return ece.parse_args([
+      "--error_type", et, "--n_top", str(n_top), "--result_filenames", RUNS["result"],
+      "--results_path", os.path.join(E2E, "results"), "--eval_path", eval_path,
+      "--datasets_path", os.path.join(E2E, "datasets")])
+
+
+def _expected(et, n_top, tau=None):
+  sign = misc.get_error_signature(et, n_top, vsd_delta=15.0, vsd_tau=tau) if et == "vsd" \
+      else misc.get_error_signature(et, n_top)
+  path = os.path.join(E2E, "expected", sign, "errors_000002.json")
+  with open(path) as f:
+    return path, json.load(f)
+
+
+def _plan(p):
+  dp_split = dataset_params.get_split_params(p["datasets_path"], "lmo", "test")
+  dp_model = dataset_params.get_model_params(p["datasets_path"], "lmo", "eval")
+  targets = inout.load_json(os.path.join(dp_split["base_path"], p["targets_filename"]))
+  ests = inout.load_bop_results(os.path.join(p["results_path"], RUNS["result"]))
+  t_org, e_org = ece.organize(targets, ests)
+  info = inout.load_json(dp_model["models_info_path"], keys_to_int=True)
+  scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=2))
+  assert list(t_org) == [2]
+  recs, _ = ece.scene_records(p, 2, t_org[2], e_org, scene_gt)
+  return recs, info
+
+
+@pytest.mark.parametrize("et,n_top", [tuple(r) for r in RUNS["runs"]])
+def test_enumeration_and_gates(et, n_top):
+  p = _params(et, n_top)
+  recs, info = _plan(p)
+  _, exp = _expected(et, n_top, p["vsd_taus"][0] if et == "vsd" else None)
+  assert len(recs) == len(exp)
+  for r, e in zip(recs, exp):
+    assert (r["im_id"], r["obj_id"], r["est_id"], r["score"]) == \
+        (e["im_id"], e["obj_id"], e["est_id"], e["score"])
+    assert [str(g) for g, _ in r["gts"]] == sorted(e["errors"], key=int)
+    for gt_id, gt in r["gts"]:
+      fill = ece.gate(et, info[r["obj_id"]]["diameter"], r["t"], gt["cam_t_m2c"])
+      got = e["errors"][str(gt_id)]
+      if fill == "vsd_fill":
+        assert got == [1.0]
+      elif fill is not None:
+        assert got == fill and math.isinf(got[0])
+
+
+def test_json_layout_round_trip(tmp_path):
+  """save_json reproduces the reference's files byte for byte."""
+  for et, n_top in RUNS["runs"]:
+    path, content = _expected(et, n_top, 0.05 if et == "vsd" else None)
+    content = json.load(open(path), object_hook=lambda d: {
+        (int(k) if k.lstrip("-").isdigit() else k): v for k, v in d.items()})
+    out = tmp_path / "x.json"
+    inout.save_json(str(out), content)
+    assert out.read_text() == open(path).read()
+
+
+def test_dataset_params_paths():
+  dp = dataset_params.get_split_params(os.path.join(E2E, "datasets"), "lmo", "test")
+  assert dp["im_size"] == (640, 480) and dp["scene_ids"] == [2]
+  assert os.path.exists(dp["depth_tpath"].format(scene_id=2, im_id=0))
+  assert os.path.exists(dp["scene_gt_tpath"].format(scene_id=2))
+  dm = dataset_params.get_model_params(os.path.join(E2E, "datasets"), "lmo", "eval")
+  assert dm["symmetric_obj_ids"] == [10, 11]
+  assert all(os.path.exists(dm["model_tpath"].format(obj_id=o)) for o in dm["obj_ids"])
+
+
+def _load(path):
+  with open(path) as f:
+    return f.read(), json.loads(open(path).read())
+
+
+@pytest.mark.gpu
+def test_caller_matches_reference(tmp_path):
+  for et, n_top in RUNS["runs"]:
+    p = _params(et, n_top, str(tmp_path))
+    written = ece.run(p, 0)
+    exp_root = os.path.join(E2E, "expected")
+    assert len(written) == (len(p["vsd_taus"]) if et == "vsd" else 1)
+    for path in written:
+      rel = os.path.relpath(path, os.path.join(str(tmp_path), "synth_lmo-test"))
+      got_txt, got = _load(path)
+      exp_txt, exp = _load(os.path.join(exp_root, rel))
+      if et in ("vsd", "re", "te", "rete"):
+        assert got_txt == exp_txt, rel  # bit-identical values
+        continue
+      assert len(got) == len(exp)
+      for g, e in zip(got, exp):
+        assert {k: v for k, v in g.items() if k != "errors"} == \
+            {k: v for k, v in e.items() if k != "errors"}
+        assert sorted(g["errors"]) == sorted(e["errors"])
+        for k in e["errors"]:
+          a, b = np.array(g["errors"][k]), np.array(e["errors"][k])
+          assert np.array_equal(np.isinf(a), np.isinf(b))
+          np.testing.assert_allclose(a[~np.isinf(a)], b[~np.isinf(b)], rtol=1e-9, atol=1e-9)
