@@ -45,7 +45,7 @@ DEFAULTS = {
     "result_filenames": ["/path/to/csv/with/results"],
     "results_path": "/path/to/results",
     "eval_path": "/path/to/eval/folder",
-    "datasets_path": os.environ.get("BOP_PATH", "/path/to/bop/datasets"),
+    "datasets_path": None,  # config.py: $BOP_PATH, read when the arguments are parsed
     "targets_filename": "test_targets_bop19.json",
     "out_errors_tpath": os.path.join("{eval_path}", "{result_name}", "{error_sign}",
                                      "errors_{scene_id:06d}.json"),
@@ -59,6 +59,7 @@ def parse_args(argv=None):
   """The reference's command line (eval_calc_errors.py:89-129), same
   defaults and the same string-to-type conversions."""
   p = copy.deepcopy(DEFAULTS)
+  p["datasets_path"] = os.environ.get("BOP_PATH", "/path/to/bop/datasets")
   ap = argparse.ArgumentParser()
   ap.add_argument("--n_top", default=p["n_top"])
   ap.add_argument("--error_type", default=p["error_type"])

@@ -1,0 +1,163 @@
+"""Counterpart of scripts/eval_calc_scores.py: match the
+estimates of every scene to the valid GT poses and compute the localization
+recall, from the errors_*.json written by eval_calc_errors.
+
+Same parameters, command line, GT validity rules (visib_gt_min >= 0: visible
+fraction threshold; -1: the inst_count most visible GT instances of every
+target object, eval_calc_scores.py:183-214), error normalisation (by object
+diameter for ad/add/adi/mssd, by 640 / image width for mspd, :221-233) and
+output files (matches_{sign}.json, scores_{sign}.json). Host-only: matching
+and counting are small integer bookkeeping.
+
+`score_error_dir` is the in-process entry point (eval_bop19_pose calls it for
+every threshold without spawning interpreters).
+"""
+import argparse
+import copy
+import os
+import time
+
+from . import dataset_params, inout, misc, pose_matching, score
+
+DEFAULTS = {
+    "correct_th": {"vsd": [0.3], "mssd": [0.2], "mspd": [10], "cus": [0.5], "rete": [5.0, 5.0],
+                   "re": [5.0], "te": [5.0], "proj": [5.0], "ad": [0.1], "add": [0.1],
+                   "adi": [0.1]},
+    "normalized_by_diameter": ["ad", "add", "adi", "mssd"],
+    "normalized_by_im_width": ["mspd"],
+    "visib_gt_min": -1,
+    "error_dir_paths": ["/path/to/calculated/errors"],
+    "eval_path": "/path/to/eval/folder",
+    "datasets_path": None,  # config.py: $BOP_PATH, read when the arguments are parsed
+    "targets_filename": "test_targets_bop19.json",
+    "error_tpath": os.path.join("{eval_path}", "{error_dir_path}", "errors_{scene_id:06d}.json"),
+    "out_matches_tpath": os.path.join("{eval_path}", "{error_dir_path}",
+                                      "matches_{score_sign}.json"),
+    "out_scores_tpath": os.path.join("{eval_path}", "{error_dir_path}",
+                                     "scores_{score_sign}.json"),
+}
+
+
+def parse_args(argv=None):
+  p = copy.deepcopy(DEFAULTS)
+  p["datasets_path"] = os.environ.get("BOP_PATH", "/path/to/bop/datasets")
+  ap = argparse.ArgumentParser()
+  for et, th in p["correct_th"].items():
+    ap.add_argument("--correct_th_" + et, default=",".join(map(str, th)))
+  ap.add_argument("--normalized_by_diameter", default=",".join(p["normalized_by_diameter"]))
+  ap.add_argument("--normalized_by_im_width", default=",".join(p["normalized_by_im_width"]))
+  ap.add_argument("--visib_gt_min", default=p["visib_gt_min"])
+  ap.add_argument("--error_dir_paths", default=",".join(p["error_dir_paths"]))
+  for k in ("eval_path", "datasets_path", "targets_filename", "error_tpath",
+            "out_matches_tpath", "out_scores_tpath"):
+    ap.add_argument("--" + k, default=p[k])
+  a = ap.parse_args(argv)
+  for et in p["correct_th"]:
+    p["correct_th"][et] = [float(x) for x in getattr(a, "correct_th_" + et).split(",")]
+  p["normalized_by_diameter"] = a.normalized_by_diameter.split(",")
+  p["normalized_by_im_width"] = a.normalized_by_im_width.split(",")
+  p["visib_gt_min"] = float(a.visib_gt_min)
+  p["error_dir_paths"] = a.error_dir_paths.split(",")
+  for k in ("eval_path", "datasets_path", "targets_filename", "error_tpath",
+            "out_matches_tpath", "out_scores_tpath"):
+    p[k] = str(getattr(a, k))
+  return p
+
+
+def valid_gts(im_gt, im_gt_info, im_targets, visib_gt_min):
+  """Which GT instances of an image count (eval_calc_scores.py:183-214)."""
+  if visib_gt_min >= 0:
+    return [gt["obj_id"] in im_targets and im_gt_info[g]["visib_fract"] >= visib_gt_min
+            for g, gt in enumerate(im_gt)]
+  valid = [False] * len(im_gt)
+  left = {o: t["inst_count"] for o, t in im_targets.items()}
+  for g in sorted(range(len(im_gt)), key=lambda g: im_gt_info[g]["visib_fract"], reverse=True):
+    o = im_gt[g]["obj_id"]
+    if left.get(o, 0) > 0:
+      valid[g] = True
+      left[o] -= 1
+  return valid
+
+
+class _Cache:
+  """Per-dataset inputs shared by all thresholds of one evaluation."""
+
+  def __init__(self):
+    self.d = {}
+
+  def get(self, key, fn):
+    if key not in self.d:
+      self.d[key] = fn()
+    return self.d[key]
+
+
+def score_error_dir(p, error_dir_path, correct_th=None, cache=None, do_print=True):
+  """Matches + scores of one errors folder; returns (scores, score_sign)."""
+  cache = cache or _Cache()
+  error_sign = os.path.basename(error_dir_path)
+  err_type = str(error_sign.split("_")[0].split("=")[1])
+  n_top = int(error_sign.split("_")[1].split("=")[1])
+  info = os.path.basename(os.path.dirname(error_dir_path)).split("_")
+  method, ds = info[0], info[1].split("-")
+  dataset, split = ds[0], ds[1]
+  split_type = ds[2] if len(ds) > 2 else None
+  th = p["correct_th"][err_type] if correct_th is None else correct_th
+  score_sign = misc.get_score_signature(th, p["visib_gt_min"])
+  misc.log("Calculating score - error: {}, method: {}, dataset: {}.".format(
+      err_type, method, dataset))
+  dp_split = dataset_params.get_split_params(p["datasets_path"], dataset, split, split_type)
+  dp_model = dataset_params.get_model_params(p["datasets_path"], dataset, "eval")
+  models_info = cache.get(("info", dp_model["models_info_path"]), lambda: inout.load_json(
+      dp_model["models_info_path"], keys_to_int=True))
+  tpath = os.path.join(dp_split["base_path"], p["targets_filename"])
+  targets = cache.get(("targets", tpath), lambda: inout.load_json(tpath))
+  targets_org = {}
+  for t in targets:
+    targets_org.setdefault(t["scene_id"], {}).setdefault(t["im_id"], {})[t["obj_id"]] = t
+  matches = []
+  for scene_id, scene_targets in targets_org.items():
+    gpath = dp_split["scene_gt_tpath"].format(scene_id=scene_id)
+    scene_gt = cache.get(("gt", gpath), lambda: inout.load_scene_gt(gpath))
+    ipath = dp_split["scene_gt_info_tpath"].format(scene_id=scene_id)
+    scene_gt_info = cache.get(("gti", ipath), lambda: inout.load_json(ipath, keys_to_int=True))
+    gt_curr = {im: scene_gt[im] for im in scene_targets}
+    gt_valid = {im: valid_gts(scene_gt[im], scene_gt_info[im], tg, p["visib_gt_min"])
+                for im, tg in scene_targets.items()}
+    scene_errs = inout.load_json(p["error_tpath"].format(
+        eval_path=p["eval_path"], error_dir_path=error_dir_path, scene_id=scene_id),
+        keys_to_int=True)
+    if err_type in p["normalized_by_diameter"]:
+      for err in scene_errs:
+        dia = float(models_info[err["obj_id"]]["diameter"])
+        err["errors"] = {g: [e / dia for e in v] for g, v in err["errors"].items()}
+    if err_type in p["normalized_by_im_width"]:
+      factor = 640.0 / float(dp_split["im_size"][0])
+      for err in scene_errs:
+        err["errors"] = {g: [factor * e for e in v] for g, v in err["errors"].items()}
+    matches += pose_matching.match_poses_scene(scene_id, gt_curr, gt_valid, scene_errs, th,
+                                               n_top)
+  scores = score.calc_localization_scores(dp_split["scene_ids"], dp_model["obj_ids"], matches,
+                                          n_top, do_print=do_print)
+  fmt = dict(eval_path=p["eval_path"], error_dir_path=error_dir_path, score_sign=score_sign)
+  inout.save_json(p["out_scores_tpath"].format(**fmt), scores)
+  inout.save_json(p["out_matches_tpath"].format(**fmt), matches)
+  return scores, score_sign
+
+
+def main(argv=None):
+  p = parse_args(argv)
+  misc.log("-----------")
+  misc.log("Parameters:")
+  for k, v in p.items():
+    misc.log("- {}: {}".format(k, v))
+  misc.log("-----------")
+  for error_dir_path in p["error_dir_paths"]:
+    misc.log("Processing: {}".format(error_dir_path))
+    t0 = time.time()
+    score_error_dir(p, error_dir_path)
+    misc.log("Matching and score calculation took {}s.".format(time.time() - t0))
+  misc.log("Done.")
+
+
+if __name__ == "__main__":
+  main()

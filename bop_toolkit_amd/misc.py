@@ -141,3 +141,9 @@ def log(s):
   sys.stdout.write("{}/{}|{:02d}:{:02d}:{:02d}: {}\n".format(
       now.month, now.day, now.hour, now.minute, now.second, s))
   sys.stdout.flush()
+
+
+def get_score_signature(correct_th, visib_gt_min):
+  """Signature of a score setting (misc.py:353-361)."""
+  return "th=" + "-".join("{:.3f}".format(t) for t in correct_th) + \
+      "_min-visib={:.3f}".format(visib_gt_min)

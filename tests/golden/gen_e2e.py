@@ -3,16 +3,20 @@
 Runs ONLY in the build container (the read-only reference checkout is at
 /root/reference). It writes a small synthetic BOP dataset in the LM-O layout
 (8 objects, test scene 2, 4 images) plus a BOP19 results CSV under
-tests/golden/e2e/, then runs the reference's scripts/eval_calc_errors.py
-end to end with runpy for every supported error type, and copies the
-errors_*.json files it writes to tests/golden/e2e/expected/. Those files
-pin tuple enumeration, n_top, gates, the per-tau VSD split, the JSON layout
-and the error values of bop_toolkit_amd.eval_calc_errors
-(tests/test_e2e_errors.py).
+tests/golden/e2e/, then runs the reference's own scripts end to end:
+scripts/eval_calc_errors.py for every supported error type and n_top rule,
+scripts/eval_calc_scores.py on several error folders / thresholds / GT
+validity rules, and scripts/eval_bop19_pose.py (which spawns the other two
+130 times). The files they write are copied to tests/golden/e2e/expected/
+(errors, matches, scores) and expected_bop19/ (scores per threshold +
+scores_bop19.json). They pin tuple enumeration, n_top, gates, the per-tau VSD
+split, the JSON layout, error values, matching, recall and the BOP19 average
+recalls of bop_toolkit_amd (tests/test_e2e_errors.py, tests/test_scores.py).
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_e2e.py
 
-Harness stubs: imageio/png are absent here, so `imageio`
+Harness stubs, installed by a generated sitecustomize.py in
+every reference interpreter: imageio/png are absent here, so `imageio`
 is a module whose imread is backed by Pillow and `png` an empty module;
 NumPy 2 removed np.float, which the reference's inout uses, so it is set to
 float. The reference's OpenGL renderers cannot run here: the vispy slot
@@ -24,11 +28,10 @@ raster itself is pinned against the spec, not against OpenGL).
 """
 import json
 import os
-import runpy
+import subprocess
 import shutil
 import sys
 import tempfile
-import types
 
 import numpy as np
 
@@ -69,21 +72,29 @@ def make_dataset(rng, root):
   sdir = os.path.join(ds, "test", "%06d" % SCENE)
   os.makedirs(os.path.join(sdir, "depth"))
   K = synth.LMO_K
-  cams, gts, targets = {}, {}, []
+  cams, gts, targets, gt_info = {}, {}, [], {}
   for im in range(N_IM):
     objs = list(rng.choice(OBJ_IDS, 5, replace=False))
     objs.append(objs[0])  # two instances of one object
     Rg, tg = synth.gt_poses(rng, len(objs), z_range=(600.0, 1100.0), xy=(120.0, 90.0))
     depth = np.zeros((H, W), np.float32)
-    inst = []
+    inst, renders = [], []
     for j, o in enumerate(objs):
       pts, faces = meshes[o]
       d = oracle.render_depth(pts, faces, Rg[j], tg[j], K[0, 0], K[1, 1], K[0, 2], K[1, 2],
                               W, H)
+      renders.append(d)
       m = (d > 0) & ((depth == 0) | (d < depth))
       depth[m] = d[m]
       inst.append({"cam_R_m2c": Rg[j].reshape(-1).tolist(),
                    "cam_t_m2c": tg[j].reshape(-1).tolist(), "obj_id": int(o)})
+    infos = []
+    for d in renders:  # scene_gt_info.json fields used by the scores (visib_fract)
+      n_all = int((d > 0).sum())
+      n_vis = int(((d > 0) & (d == depth)).sum())
+      infos.append({"px_count_all": n_all, "px_count_visib": n_vis,
+                    "visib_fract": n_vis / n_all if n_all else 0.0})
+    gt_info[str(im)] = infos
     depth[depth == 0] = 1600.0
     depth[40 + 30 * im:120 + 30 * im, 200:330] = 500.0  # occluder
     depth[300:340, 100:400] = 0.0  # missing depth
@@ -97,6 +108,8 @@ def make_dataset(rng, root):
     for o in sorted(set(objs)):
       targets.append({"im_id": im, "inst_count": int(objs.count(o)), "obj_id": int(o),
                       "scene_id": SCENE})
+  with open(os.path.join(sdir, "scene_gt_info.json"), "w") as f:
+    json.dump(gt_info, f, indent=1)
   with open(os.path.join(sdir, "scene_camera.json"), "w") as f:
     json.dump(cams, f, indent=1)
   with open(os.path.join(sdir, "scene_gt.json"), "w") as f:
@@ -123,7 +136,7 @@ def make_results(rng, root, gts, targets):
       lines.append("%d,%d,%d,%s,%s,%s,%s" % (
           SCENE, im, o, repr(score), " ".join(repr(float(x)) for x in Re.reshape(-1)),
           " ".join(repr(float(x)) for x in te.reshape(-1)), "0.5"))
-  lines.append("%d,%d,%d,0.9,%s,%s,0.1" % (  # estimate of an object with no target
+  lines.append("%d,%d,%d,0.9,%s,%s,0.5" % (  # estimate of an object with no target
       SCENE, 0, 99, " ".join(["1.0", "0.0", "0.0", "0.0", "1.0", "0.0", "0.0", "0.0", "1.0"]),
       "0.0 0.0 800.0"))
   os.makedirs(os.path.join(root, "results"))
@@ -131,34 +144,57 @@ def make_results(rng, root, gts, targets):
     f.write("\n".join(lines) + "\n")
 
 
-def install_stubs(meshes_by_path):
-  np.float = float  # removed in NumPy 2, used by the reference's inout
-  from PIL import Image
-  imageio = types.ModuleType("imageio")
-  imageio.imread = lambda p: np.asarray(Image.open(p))
-  sys.modules["imageio"] = imageio
-  sys.modules["png"] = types.ModuleType("png")
-  sys.path.insert(0, REF)
+# Installed in every reference interpreter (errors, scores and the BOP19 driver,
+# which spawns further interpreters) through PYTHONPATH.
+SITECUSTOMIZE = """
+import sys, types
+import numpy as np
+np.float = float  # removed in NumPy 2, used by the reference's inout
+from PIL import Image
+imageio = types.ModuleType("imageio")
+imageio.imread = lambda p: np.asarray(Image.open(p))
+sys.modules["imageio"] = imageio
+sys.modules["png"] = types.ModuleType("png")
 
-  class RendererVispy:  # fills the vispy slot of renderer.create_renderer
-    def __init__(self, width, height, mode="rgb+depth", shading="phong", bg_color=None):
-      self.w, self.h, self.models = width, height, {}
 
-    def add_object(self, obj_id, model_path, **kw):
-      m = inout.load_ply(model_path)
-      self.models[obj_id] = (m["pts"], m["faces"])
+class RendererVispy:  # fills the vispy slot of renderer.create_renderer
+  def __init__(self, width, height, mode="rgb+depth", shading="phong", bg_color=None):
+    self.w, self.h, self.models = width, height, {}
 
-    def render_object(self, obj_id, R, t, fx, fy, cx, cy):
-      pts, faces = self.models[obj_id]
-      return {"depth": oracle.render_depth(pts, faces, np.asarray(R, np.float64),
-                                           np.asarray(t, np.float64).reshape(3), fx, fy, cx, cy,
-                                           self.w, self.h)}
+  def add_object(self, obj_id, model_path, **kw):
+    from bop_toolkit_amd import inout
+    m = inout.load_ply(model_path)
+    self.models[obj_id] = (m["pts"], m["faces"])
 
-  mod = types.ModuleType("bop_toolkit_lib.renderer_vispy")
-  mod.RendererVispy = RendererVispy
-  sys.modules["bop_toolkit_lib.renderer_vispy"] = mod
-  import bop_toolkit_lib
-  bop_toolkit_lib.renderer_vispy = mod
+  def render_object(self, obj_id, R, t, fx, fy, cx, cy):
+    from oracle import oracle
+    pts, faces = self.models[obj_id]
+    return {"depth": oracle.render_depth(pts, faces, np.asarray(R, np.float64),
+                                         np.asarray(t, np.float64).reshape(3), fx, fy, cx, cy,
+                                         self.w, self.h)}
+
+
+mod = types.ModuleType("bop_toolkit_lib.renderer_vispy")
+mod.RendererVispy = RendererVispy
+sys.modules["bop_toolkit_lib.renderer_vispy"] = mod
+"""
+
+# (error folder, extra arguments) of the standalone eval_calc_scores runs
+SCORE_RUNS = [
+    ("error=vsd_ntop=-1_delta=15.000_tau=0.200", ["--correct_th_vsd=0.3"]),
+    ("error=vsd_ntop=1_delta=15.000_tau=0.500", ["--correct_th_vsd=0.25", "--visib_gt_min=0.1"]),
+    ("error=mssd_ntop=-1", ["--correct_th_mssd=0.2"]),
+    ("error=mssd_ntop=0", ["--correct_th_mssd=0.35", "--visib_gt_min=0.3"]),
+    ("error=mspd_ntop=-1", ["--correct_th_mspd=10"]),
+    ("error=ad_ntop=-1", ["--correct_th_ad=0.1"]),
+    ("error=proj_ntop=-1", ["--correct_th_proj=15"]),
+    ("error=rete_ntop=-1", ["--correct_th_rete=5.0,5.0"]),
+]
+
+
+def run_ref(script, args, env):
+  subprocess.run([sys.executable, os.path.join(REF, "scripts", script)] + args, env=env,
+                 check=True, stdout=subprocess.DEVNULL)
 
 
 def main():
@@ -166,23 +202,48 @@ def main():
   if os.path.exists(OUT):
     shutil.rmtree(OUT)
   os.makedirs(OUT)
-  meshes, gts, targets = make_dataset(rng, OUT)
+  make_dataset(rng, OUT)
+  gts = json.load(open(os.path.join(OUT, "datasets", "lmo", "test", "%06d" % SCENE,
+                                    "scene_gt.json")))
+  targets = json.load(open(os.path.join(OUT, "datasets", "lmo", "test_targets_bop19.json")))
   make_results(rng, OUT, gts, targets)
-  install_stubs(meshes)
-  script = os.path.join(REF, "scripts", "eval_calc_errors.py")
-  expected = os.path.join(OUT, "expected")
-  with tempfile.TemporaryDirectory() as ev:
+  datasets = os.path.join(OUT, "datasets")
+  results = os.path.join(OUT, "results")
+  name = os.path.splitext(RESULT)[0]
+  with tempfile.TemporaryDirectory() as tmp:
+    stub = os.path.join(tmp, "stub")
+    os.makedirs(stub)
+    with open(os.path.join(stub, "sitecustomize.py"), "w") as f:
+      f.write(SITECUSTOMIZE)
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([stub, REF, REPO]),
+               PYTHONDONTWRITEBYTECODE="1", BOP_PATH=datasets)
+    ev = os.path.join(tmp, "eval")
     for et, n_top in RUNS:
-      sys.argv = [script, "--error_type", et, "--n_top", str(n_top), "--result_filenames",
-                  RESULT, "--results_path", os.path.join(OUT, "results"), "--eval_path", ev,
-                  "--datasets_path", os.path.join(OUT, "datasets"), "--renderer_type", "vispy"]
-      runpy.run_path(script, run_name="__main__")
-    src = os.path.join(ev, os.path.splitext(RESULT)[0])
-    shutil.copytree(src, expected)
+      run_ref("eval_calc_errors.py", ["--error_type", et, "--n_top", str(n_top),
+                                      "--result_filenames", RESULT, "--results_path", results,
+                                      "--eval_path", ev, "--datasets_path", datasets,
+                                      "--renderer_type", "vispy"], env)
+    for sign, extra in SCORE_RUNS:
+      run_ref("eval_calc_scores.py", ["--error_dir_paths", os.path.join(name, sign),
+                                      "--eval_path", ev, "--datasets_path", datasets] + extra,
+              env)
+    shutil.copytree(os.path.join(ev, name), os.path.join(OUT, "expected"))
+    ev19 = os.path.join(tmp, "eval19")
+    run_ref("eval_bop19_pose.py", ["--result_filenames", RESULT, "--results_path", results,
+                                   "--eval_path", ev19, "--renderer_type", "vispy"], env)
+    keep = os.path.join(OUT, "expected_bop19")
+    for root, _, files in os.walk(os.path.join(ev19, name)):
+      for fn in files:
+        if fn.startswith("scores_"):  # errors and matches are covered above
+          dst = os.path.join(keep, os.path.relpath(os.path.join(root, fn),
+                                                   os.path.join(ev19, name)))
+          os.makedirs(os.path.dirname(dst), exist_ok=True)
+          shutil.copy(os.path.join(root, fn), dst)
   with open(os.path.join(OUT, "runs.json"), "w") as f:
-    json.dump({"result": RESULT, "runs": RUNS, "depth_scale": DEPTH_SCALE}, f)
-  n = sum(len(fs) for _, _, fs in os.walk(expected))
-  print("wrote %d expected files under %s" % (n, expected))
+    json.dump({"result": RESULT, "runs": RUNS, "score_runs": SCORE_RUNS,
+               "depth_scale": DEPTH_SCALE}, f, indent=1)
+  n = sum(len(fs) for _, _, fs in os.walk(OUT))
+  print("wrote %d files under %s" % (n, OUT))
 
 
 if __name__ == "__main__":
