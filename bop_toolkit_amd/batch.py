@@ -116,6 +116,16 @@ class BatchEvaluator:
                   _p(diameters), code, _p(out), _stream(self.device))
     return out
 
+  def cover(self, slots, pose_est, pose_gt, frame_idx, cam, width, height, out=None):
+    """Silhouette overlap per tuple for cus / cou_bb_proj: float64 [n, 10] =
+    union, inter, est bbox (x0, y0, x1, y1), gt bbox (empty: x1 = y1 = -1)."""
+    n = slots.numel()
+    out = self._out(n, 10) if out is None else out
+    self.ctx.call("bopx_cover_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt),
+                  _p(frame_idx), int(width), int(height), _p(cam), _p(out),
+                  _stream(self.device))
+    return out
+
   def render(self, slots, pose, frame_idx, cam, n_frames, width, height, frames=None):
     """Min-composite depth renders of many instances into n_frames frames
     (instances sharing a frame occlude each other). Returns float32 frames."""

@@ -35,6 +35,8 @@ constexpr int kMeshletVerts = 64;   // unique vertices per meshlet (one per lane
 constexpr int kMaxMeshlets = BOPX_MAX_MESHLETS;  // per object (VSD)
 constexpr int kMaxTaus = 16;
 constexpr int kVsdMaxTiles = 2048;  // k_vsd keeps 16-bit per-lane tau counters
+constexpr int kCostCover = 2;  // k_vsd mode: silhouette union/inter + bboxes (cus, cou_bb_proj)
+constexpr int kCoverCols = 10;  // union, inter, est bbox x0 y0 x1 y1, gt bbox x0 y0 x1 y1
 constexpr int kTileW = BOPX_TILE_W;  // VSD screen tile (LDS-resident q pair)
 constexpr int kTileH = BOPX_TILE_H;
 constexpr int kTileStride = kTileW + 1;  // LDS row pitch of a q tile (dwords)
@@ -85,7 +87,9 @@ hipError_t launch_mean_error(int mode, const ObjDesc* objs, int64_t n, const int
                              hipStream_t s);  // mode 0 = ADD, 1 = PROJ
 hipError_t launch_adi(const ObjDesc* objs, int64_t n, const int32_t* slots, const double* pe,
                       const double* pg, double* out, hipStream_t s);
-hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s);
+hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s);  // or kCostCover
+hipError_t launch_cover_depths(int W, int H, const float* de, const float* dg,
+                               long long* acc /* kCoverCols, device */, hipStream_t s);
 hipError_t read_vsd_stats(unsigned long long* out, int reset);  // diagnostics
 hipError_t launch_vsd_depths(int W, int H, const float* dt, const float* de, const float* dg,
                              double fx, double fy, double cx, double cy, float delta32,

@@ -24,6 +24,8 @@
 //  4. Counters are reduced across the workgroup; one thread writes
 //     e_k = (cnt_k + comp) / union (1.0 when union == 0).
 // Results are bit-identical to the reference given identical depth maps.
+#include <algorithm>
+
 #include "raster.h"
 
 namespace bopx {
@@ -136,7 +138,7 @@ static_assert(sizeof(RRow) * 64 * kVsdWaves >= 2 * kPixPerWave * kVsdWaves,
 constexpr int kGroup = BOPX_VSD_GROUP;  // (pose, meshlet) entries staged together per wave step
 constexpr int kRectsPerThread = 2 * kMaxMeshlets / kVsdThreads;
 
-template <int COST>  // 0 = step, 1 = tlinear
+template <int COST>  // 0 = step, 1 = tlinear, kCostCover = silhouette overlap only
 // Two workgroups per CU: 2 * kVsdThreads / 256 waves per SIMD (caps VGPRs at 128).
 __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdArgs a) {
   // q = 1/Z bits, 0 = empty; rows padded by one dword so lanes that walk the
@@ -208,6 +210,8 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   const int rx0 = s_roi[0], ry0 = s_roi[1], rx1 = s_roi[2], ry1 = s_roi[3];
 
   uint32_t c_union = 0, c_inter = 0;
+  // cover mode: est / gt silhouette bboxes (x0, y0, x1, y1), empty = (INT_MAX, INT_MAX, -1, -1)
+  int bb[8] = {INT32_MAX, INT32_MAX, -1, -1, INT32_MAX, INT32_MAX, -1, -1};
   // step cost: two 16-bit per-tau counters per register (a lane evaluates at
   // most kTileW * kTileH / kVsdThreads pixels per tile, <= kVsdMaxTiles tiles)
   uint32_t c_tau[kMaxTaus / 2];
@@ -396,6 +400,23 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         const int ps = (p / kTileW) * kTileStride + p % kTileW;
         const uint32_t qe = s_dep[0][ps], qg = s_dep[1][ps];
         if VSD_DIAG(4) atomicAdd(&g_vsd_stats[6], 1ull);
+        if constexpr (COST == kCostCover) {  // silhouettes only (cus, cou_bb_proj)
+          ++c_union;
+          c_inter += (qe != 0u && qg != 0u);
+          if (qe) {
+            bb[0] = min(bb[0], col);
+            bb[1] = min(bb[1], row);
+            bb[2] = max(bb[2], col);
+            bb[3] = max(bb[3], row);
+          }
+          if (qg) {
+            bb[4] = min(bb[4], col);
+            bb[5] = min(bb[5], row);
+            bb[6] = max(bb[6], col);
+            bb[7] = max(bb[7], row);
+          }
+          continue;
+        }
         const float de = qe ? 1.0f / __uint_as_float(qe) : 0.0f;
         const float dg = qg ? 1.0f / __uint_as_float(qg) : 0.0f;
         const float dtest = frame[(int64_t)row * W + col];
@@ -453,6 +474,17 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       s_lin[wave][k] = lin[k];
     }
   }
+  if constexpr (COST == kCostCover) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      for (int off = 32; off > 0; off >>= 1) {
+        const int o = __shfl_xor(bb[k], off, 64);
+        bb[k] = (k & 2) ? max(bb[k], o) : min(bb[k], o);
+      }
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s_cnt[wave][2 + k] = (uint32_t)bb[k];
+  }
   __syncthreads();
   VSD_STAMP(7);
   if (VSD_DIAG(8) && lane == 0)
@@ -462,6 +494,20 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
     for (int w = 0; w < kVsdWaves; ++w) {
       un += s_cnt[w][0];
       in += s_cnt[w][1];
+    }
+    if constexpr (COST == kCostCover) {
+      double* out = a.out + b * (int64_t)kCoverCols;
+      out[0] = (double)un;
+      out[1] = (double)in;
+      for (int k = 0; k < 8; ++k) {
+        int v = (int)s_cnt[0][2 + k];
+        for (int w = 1; w < kVsdWaves; ++w) {
+          const int o = (int)s_cnt[w][2 + k];
+          v = (k & 2) ? max(v, o) : min(v, o);
+        }
+        out[2 + k] = (double)v;
+      }
+      return;
     }
     double* out = a.out + b * (int64_t)a.n_tau;
     for (int k = 0; k < a.n_tau; ++k) {
@@ -496,8 +542,10 @@ hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s) {
   dim3 grid((unsigned)a.n), block(kVsdThreads);
   if (cost_type == 0)
     hipLaunchKernelGGL(k_vsd<0>, grid, block, 0, s, a);
-  else
+  else if (cost_type == 1)
     hipLaunchKernelGGL(k_vsd<1>, grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL(k_vsd<kCostCover>, grid, block, 0, s, a);
   return hipGetLastError();
 }
 
@@ -575,6 +623,74 @@ hipError_t launch_vsd_depths(int W, int H, const float* dt, const float* de, con
   hipLaunchKernelGGL(k_vsd_depths, dim3(n_blocks), dim3(kVsdThreads), 0, s, W, H, dt, de, dg, fx,
                      fy, cx, cy, delta32, delta_f64, delta64, ta, n_tau, normalized, diameter,
                      partials);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Silhouette overlap of two host-supplied depth maps (foreign renderer path of
+// cus / cou_bb_proj, pose_error.py:256-330): mask = depth > 0. One grid-stride
+// pass; wave-reduced counts and bboxes merged with 64-bit atomics into
+// acc[kCoverCols] (exact, order-independent). acc is set by k_cover_init.
+__global__ void k_cover_init(long long* acc) {
+  const int k = threadIdx.x;
+  if (k < kCoverCols) acc[k] = (k < 2) ? 0 : (((k - 2) & 2) ? -1 : INT32_MAX);
+}
+
+__global__ __launch_bounds__(256) void k_cover_depths(int W, int H, const float* __restrict__ de,
+                                                      const float* __restrict__ dg,
+                                                      long long* __restrict__ acc) {
+  long long un = 0, in = 0;
+  int bb[8] = {INT32_MAX, INT32_MAX, -1, -1, INT32_MAX, INT32_MAX, -1, -1};
+  const int64_t n = (int64_t)W * H;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const bool me = de[i] > 0.0f, mg = dg[i] > 0.0f;
+    if (!(me || mg)) continue;
+    const int row = (int)(i / W), col = (int)(i % W);
+    ++un;
+    in += (me && mg);
+    if (me) {
+      bb[0] = min(bb[0], col);
+      bb[1] = min(bb[1], row);
+      bb[2] = max(bb[2], col);
+      bb[3] = max(bb[3], row);
+    }
+    if (mg) {
+      bb[4] = min(bb[4], col);
+      bb[5] = min(bb[5], row);
+      bb[6] = max(bb[6], col);
+      bb[7] = max(bb[7], row);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    un += __shfl_xor(un, off, 64);
+    in += __shfl_xor(in, off, 64);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int o = __shfl_xor(bb[k], off, 64);
+      bb[k] = (k & 2) ? max(bb[k], o) : min(bb[k], o);
+    }
+  }
+  if ((threadIdx.x & 63) == 0 && un > 0) {
+    atomicAdd((unsigned long long*)&acc[0], (unsigned long long)un);
+    atomicAdd((unsigned long long*)&acc[1], (unsigned long long)in);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k & 2)
+        atomicMax(&acc[2 + k], (long long)bb[k]);
+      else
+        atomicMin(&acc[2 + k], (long long)bb[k]);
+    }
+  }
+}
+
+hipError_t launch_cover_depths(int W, int H, const float* de, const float* dg, long long* acc,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(k_cover_init, dim3(1), dim3(64), 0, s, acc);
+  const int64_t n = (int64_t)W * H;
+  const unsigned blocks = (unsigned)std::min<int64_t>(2048, (n + 255) / 256);
+  if (blocks > 0)
+    hipLaunchKernelGGL(k_cover_depths, dim3(blocks), dim3(256), 0, s, W, H, de, dg, acc);
   return hipGetLastError();
 }
 

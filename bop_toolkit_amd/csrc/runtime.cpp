@@ -658,6 +658,111 @@ int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double*
   return BOPX_OK;
 }
 
+// ----------------------------------------------------------- silhouette cover
+static int cover_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height) {
+  if (width <= 0 || height <= 0 || width > 32767 || height > 32767)
+    return fail(c, BOPX_E_INVALID, "bad image size %dx%d", width, height);
+  if ((int64_t)((width + bopx::kTileW - 1) / bopx::kTileW) *
+          ((height + bopx::kTileH - 1) / bopx::kTileH) > bopx::kVsdMaxTiles)
+    return fail(c, BOPX_E_UNSUPPORTED, "image %dx%d exceeds the fused kernel's %d tiles",
+                width, height, bopx::kVsdMaxTiles);
+  a.width = width;
+  a.height = height;
+  a.n_tau = 0;
+  return BOPX_OK;
+}
+
+int bopx_cover_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
+                         const double* pg, const int32_t* frame_idx, int width, int height,
+                         const double* cam, double* out, void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (int r = set_dev(c)) return r;
+  bopx::VsdArgs a{};
+  if (int r = cover_args(c, a, width, height)) return r;
+  a.objs = c->d_desc;
+  a.slots = slots;
+  a.pose_est = pe;
+  a.pose_gt = pg;
+  a.frame_idx = frame_idx;
+  a.cam = cam;
+  a.out = out;
+  a.n = n;
+  HIPCHK(c, bopx::launch_vsd(a, bopx::kCostCover, pick_stream(c, stream)));
+  return BOPX_OK;
+}
+
+int bopx_cover_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double* pe,
+                     const double* pg, const int32_t* frame_idx, int64_t n_frames, int width,
+                     int height, const double* cam, double* out) {
+  if (!c) return BOPX_E_INVALID;
+  if (n < 0 || n_frames < 0) return fail(c, BOPX_E_INVALID, "negative size");
+  if (n == 0) return BOPX_OK;
+  if (!obj_ids || !pe || !pg || !frame_idx || !cam || !out)
+    return fail(c, BOPX_E_INVALID, "NULL buffer");
+  for (int64_t i = 0; i < n; ++i)
+    if (frame_idx[i] < 0 || frame_idx[i] >= n_frames)
+      return fail(c, BOPX_E_INVALID, "frame_idx[%lld] = %d out of range", (long long)i,
+                  frame_idx[i]);
+  if (int r = set_dev(c)) return r;
+  bopx::VsdArgs a{};
+  if (int r = cover_args(c, a, width, height)) return r;
+  std::vector<int32_t> slots;
+  if (int r = map_slots(c, n, obj_ids, slots, false, true)) return r;
+  const size_t cols = bopx::kCoverCols;
+  if (int r = ws_reserve(c, carve_size({4 * (size_t)n, 96 * (size_t)n, 96 * (size_t)n,
+                                        4 * (size_t)n, 32 * (size_t)n_frames,
+                                        8 * cols * (size_t)n})))
+    return r;
+  Carve cv{(char*)c->ws.p};
+  int32_t* d_s = cv.take<int32_t>(n);
+  double* d_pe = cv.take<double>(12 * n);
+  double* d_pg = cv.take<double>(12 * n);
+  int32_t* d_fi = cv.take<int32_t>(n);
+  double* d_cam = cv.take<double>(4 * n_frames);
+  double* d_out = cv.take<double>(cols * n);
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_s, slots.data(), 4 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_pe, pe, 96 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_pg, pg, 96 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_fi, frame_idx, 4 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_cam, cam, 32 * n_frames, hipMemcpyHostToDevice, s));
+  a.objs = c->d_desc;
+  a.slots = d_s;
+  a.pose_est = d_pe;
+  a.pose_gt = d_pg;
+  a.frame_idx = d_fi;
+  a.cam = d_cam;
+  a.out = d_out;
+  a.n = n;
+  HIPCHK(c, bopx::launch_vsd(a, bopx::kCostCover, s));
+  HIPCHK(c, hipMemcpyAsync(out, d_out, 8 * cols * n, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return BOPX_OK;
+}
+
+int bopx_cover_from_depths(bopx_ctx* c, int width, int height, const float* depth_est,
+                           const float* depth_gt, double* out) {
+  if (!c) return BOPX_E_INVALID;
+  if (width <= 0 || height <= 0) return fail(c, BOPX_E_INVALID, "bad image size");
+  if (!depth_est || !depth_gt || !out) return fail(c, BOPX_E_INVALID, "NULL buffer");
+  if (int r = set_dev(c)) return r;
+  const size_t npx = (size_t)width * height;
+  if (int r = ws_reserve(c, carve_size({4 * npx, 4 * npx, 8 * bopx::kCoverCols}))) return r;
+  Carve cv{(char*)c->ws.p};
+  float* d_e = cv.take<float>(npx);
+  float* d_g = cv.take<float>(npx);
+  long long* d_acc = cv.take<long long>(bopx::kCoverCols);
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_e, depth_est, 4 * npx, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_g, depth_gt, 4 * npx, hipMemcpyHostToDevice, s));
+  HIPCHK(c, bopx::launch_cover_depths(width, height, d_e, d_g, d_acc, s));
+  long long acc[bopx::kCoverCols];
+  HIPCHK(c, hipMemcpyAsync(acc, d_acc, sizeof(acc), hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  for (int k = 0; k < bopx::kCoverCols; ++k) out[k] = (double)acc[k];
+  return BOPX_OK;
+}
+
 int bopx_vsd_from_depths(bopx_ctx* c, int width, int height, const float* depth_test,
                          const float* depth_est, const float* depth_gt, double fx, double fy,
                          double cx, double cy, double delta, int flags, const double* taus,

@@ -52,7 +52,7 @@ DEFAULTS = {
 }
 
 POINT_ERRORS = ("ad", "add", "adi", "mssd", "mspd", "proj")
-ERROR_TYPES = ("vsd", "mssd", "mspd", "ad", "add", "adi", "proj", "rete", "re", "te")
+ERROR_TYPES = ("vsd", "mssd", "mspd", "ad", "add", "adi", "cus", "proj", "rete", "re", "te")
 
 
 def parse_args(argv=None):
@@ -230,6 +230,15 @@ def evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, mode
                  p["vsd_taus"], T(dia, torch.float64),
                  normalized_by_diameter=p["vsd_normalized_by_diameter"], cost_type="step",
                  delta_flags=runtime.delta_flags(delta))
+  elif et == "cus":
+    ims = sorted({recs[ri]["im_id"] for ri, _, _, _ in todo})
+    frame_of = {im: k for k, im in enumerate(ims)}
+    cam = np.array([[K[0, 0], K[1, 1], K[0, 2], K[1, 2]]
+                    for K in (scene_camera[im]["cam_K"] for im in ims)], np.float64)
+    fidx = np.array([frame_of[recs[ri]["im_id"]] for ri, _, _, _ in todo], np.int32)
+    W, H = dp_split["im_size"]
+    cov = ev.cover(slots, d_pe, d_pg, T(fidx, torch.int32), T(cam, torch.float64), W, H)
+    out = [pose_error.cus_from_cover(row) for row in cov.cpu().numpy()]
   elif et in ("mspd", "proj"):
     K = np.stack([scene_camera[recs[ri]["im_id"]]["cam_K"].reshape(9) for ri, _, _, _ in todo])
     fn = ev.mspd if et == "mspd" else ev.proj
@@ -246,7 +255,7 @@ def evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, mode
         out[ii] = fn(slots[ii], d_pe[ii], d_pg[ii])
   else:
     raise ValueError("Unknown pose error function.")
-  vals = out.cpu().numpy().tolist()
+  vals = out if isinstance(out, list) else out.cpu().numpy().tolist()
   for (ri, gt_id, _, _), v in zip(todo, vals):
     errs[ri][gt_id] = v if isinstance(v, list) else [v]
   return errs

@@ -147,3 +147,26 @@ def get_score_signature(correct_th, visib_gt_min):
   """Signature of a score setting (misc.py:353-361)."""
   return "th=" + "-".join("{:.3f}".format(t) for t in correct_th) + \
       "_min-visib={:.3f}".format(visib_gt_min)
+
+
+def calc_2d_bbox(xs, ys, im_size=None, clip=False):
+  """(x, y, w, h) of a point set, w = max - min (misc.py:202-218)."""
+  lo = [xs.min(), ys.min()]
+  hi = [xs.max(), ys.max()]
+  if clip:
+    assert im_size is not None
+    lo = [min(max(lo[0], 0), im_size[0] - 1), min(max(lo[1], 0), im_size[1] - 1)]
+    hi = [min(max(hi[0], 0), im_size[0] - 1), min(max(hi[1], 0), im_size[1] - 1)]
+  return [lo[0], lo[1], hi[0] - lo[0], hi[1] - lo[1]]
+
+
+def iou(bb_a, bb_b):
+  """Intersection over union of two (x, y, w, h) boxes (misc.py:236-263)."""
+  ax1, ay1 = bb_a[0] + bb_a[2], bb_a[1] + bb_a[3]
+  bx1, by1 = bb_b[0] + bb_b[2], bb_b[1] + bb_b[3]
+  w = min(ax1, bx1) - max(bb_a[0], bb_b[0])
+  h = min(ay1, by1) - max(bb_a[1], bb_b[1])
+  if w > 0 and h > 0:
+    inter = w * h
+    return inter / float(bb_a[2] * bb_a[3] + bb_b[2] * bb_b[3] - inter)
+  return 0.0

@@ -15,6 +15,7 @@ import math
 import numpy as np
 
 from . import _lib
+from . import misc
 from . import runtime
 from ._lib import _d, _f, _i32, ptr
 from .renderer_hip import RendererHIP
@@ -123,3 +124,67 @@ def te(t_est, t_gt):
   """Translational error (pose_error.py:205-214). O(1) host math."""
   assert t_est.size == t_gt.size == 3
   return np.linalg.norm(t_gt - t_est)
+
+
+def _cover(R_est, t_est, R_gt, t_gt, K, renderer, obj_id):
+  """[union, inter, est bbox x0 y0 x1 y1, gt bbox x0 y0 x1 y1] of the two
+  rendered silhouettes (depth > 0). RendererHIP: both renders fused into one
+  k_vsd launch in silhouette mode; other renderers: their depth maps are
+  compared on the GPU (k_cover_depths)."""
+  ctx = runtime.context()
+  fx, fy, cx, cy = float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2])
+  out = np.empty(10, np.float64)
+  if isinstance(renderer, RendererHIP) and renderer.ctx is ctx:
+    ids = np.array([obj_id], np.int32)
+    pe, pg = runtime.pose12(R_est, t_est), runtime.pose12(R_gt, t_gt)
+    fi = np.zeros(1, np.int32)
+    cam = np.array([fx, fy, cx, cy], np.float64)
+    ctx.call("bopx_cover_batch", 1, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(fi, _i32), 1,
+             renderer.width, renderer.height, ptr(cam, _d), ptr(out, _d))
+  else:
+    de = np.ascontiguousarray(renderer.render_object(obj_id, R_est, t_est, fx, fy, cx, cy)
+                              ["depth"], np.float32)
+    dg = np.ascontiguousarray(renderer.render_object(obj_id, R_gt, t_gt, fx, fy, cx, cy)
+                              ["depth"], np.float32)
+    assert de.shape == dg.shape
+    ctx.call("bopx_cover_from_depths", de.shape[1], de.shape[0], ptr(de, _f), ptr(dg, _f),
+             ptr(out, _d))
+  return out
+
+
+def cus_from_cover(cov):
+  """1 - |inter| / |union| of two masks, 1.0 for an empty union."""
+  union, inter = float(cov[0]), float(cov[1])
+  return 1.0 - inter / union if union > 0 else 1.0
+
+
+def bbox_from_cover(cov, k):
+  """misc.calc_2d_bbox of mask k (0 = est, 1 = gt) from a cover row."""
+  x0, y0, x1, y1 = (int(v) for v in cov[2 + 4 * k:6 + 4 * k])
+  if x1 < 0:  # numpy's error for xs.min() of an empty mask
+    raise ValueError("zero-size array to reduction operation minimum which has no identity")
+  return [x0, y0, x1 - x0, y1 - y0]
+
+
+def cus(R_est, t_est, R_gt, t_gt, K, renderer, obj_id):
+  """Complement over Union of the projected silhouettes (pose_error.py:256-286)."""
+  return np.float64(cus_from_cover(_cover(R_est, t_est, R_gt, t_gt, K, renderer, obj_id)))
+
+
+def cou_bb_proj(R_est, t_est, R_gt, t_gt, K, renderer, obj_id):
+  """Complement over Union of the silhouettes' 2D bounding boxes (pose_error.py:300-330)."""
+  cov = _cover(R_est, t_est, R_gt, t_gt, K, renderer, obj_id)
+  return 1.0 - misc.iou(bbox_from_cover(cov, 0), bbox_from_cover(cov, 1))
+
+
+def cou_mask(mask_est, mask_gt):
+  """Complement over Union of two given binary masks (pose_error.py:233-253).
+  Host bookkeeping on caller-provided masks."""
+  me, mg = np.asarray(mask_est).astype(bool), np.asarray(mask_gt).astype(bool)
+  union = float(np.logical_or(me, mg).sum())
+  return 1.0 - np.logical_and(me, mg).sum() / union if union > 0 else 1.0
+
+
+def cou_bb(bb_est, bb_gt):
+  """Complement over Union of two 2D boxes (x, y, w, h) (pose_error.py:289-297)."""
+  return 1.0 - misc.iou(bb_est, bb_gt)

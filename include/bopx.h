@@ -127,6 +127,21 @@ int bopx_vsd_from_depths(bopx_ctx* ctx, int width, int height, const float* dept
                          const double* taus, int n_tau, int normalized_by_diameter,
                          double diameter, int cost_type, double* out);
 
+/* ---- silhouette overlap: cus / cou_bb_proj (pose_error.py:256-330) -------- */
+/* Both poses rasterised by the HIP rasteriser (the VSD raster spec). Per tuple
+ * out[10] float64: pixel counts of the union and the intersection of the two
+ * masks (depth > 0), then the est and the gt mask bbox (x0, y0, x1, y1,
+ * inclusive pixel coordinates; an empty mask has x1 = y1 = -1). frame_idx
+ * selects each tuple's camera row in cam (n_frames x 4: fx, fy, cx, cy). */
+int bopx_cover_batch(bopx_ctx* ctx, int64_t n, const int32_t* obj_ids,
+                     const double* pose_est, const double* pose_gt,
+                     const int32_t* frame_idx, int64_t n_frames, int width, int height,
+                     const double* cam, double* out);
+/* The same from two already-rendered h x w float32 depth maps (foreign
+ * renderers); out[10]. */
+int bopx_cover_from_depths(bopx_ctx* ctx, int width, int height, const float* depth_est,
+                           const float* depth_gt, double* out);
+
 /* ---- renderer plugin (renderer.py:62-74) ---------------------------------- */
 /* Depth (eye Z in model units, 0 = background) of one object in one pose;
  * out: height x width float32. */
@@ -168,6 +183,10 @@ int bopx_vsd_batch_dev(bopx_ctx* ctx, int64_t n, const int32_t* slots,
                        const double* taus, int n_tau, int normalized_by_diameter,
                        const double* diameters, int cost_type, double* out,
                        void* stream);
+int bopx_cover_batch_dev(bopx_ctx* ctx, int64_t n, const int32_t* slots,
+                         const double* pose_est, const double* pose_gt,
+                         const int32_t* frame_idx, int width, int height, const double* cam,
+                         double* out, void* stream);
 /* Composite render of many (object, pose) instances into frames:
  * frames (n_frames x h x w f32, device) must be pre-filled with +inf bit
  * patterns by bopx_depth_clear_dev; instances are min-composited (z-buffer);

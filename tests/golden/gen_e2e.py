@@ -51,7 +51,8 @@ N_IM = 4
 DEPTH_SCALE = 0.1  # depth PNG in 0.1 mm units
 RESULT = "synth_lmo-test.csv"
 RUNS = [("vsd", -1), ("vsd", 1), ("mssd", -1), ("mssd", 0), ("mspd", -1), ("ad", -1),
-        ("add", -1), ("adi", -1), ("proj", -1), ("re", -1), ("te", -1), ("rete", -1)]
+        ("add", -1), ("adi", -1), ("cus", -1), ("proj", -1), ("re", -1), ("te", -1),
+        ("rete", -1)]
 
 
 def make_dataset(rng, root):
@@ -189,6 +190,7 @@ SCORE_RUNS = [
     ("error=ad_ntop=-1", ["--correct_th_ad=0.1"]),
     ("error=proj_ntop=-1", ["--correct_th_proj=15"]),
     ("error=rete_ntop=-1", ["--correct_th_rete=5.0,5.0"]),
+    ("error=cus_ntop=-1", ["--correct_th_cus=0.5"]),
 ]
 
 

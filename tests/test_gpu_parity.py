@@ -294,3 +294,81 @@ def test_errors_on_bad_input(ctx):
     ctx.call("bopx_mssd_batch", 1, ptr(ids, _i32), ptr(pe, _d), ptr(pe, _d), ptr(out, _d))
   # n == 0 is a no-op
   ctx.call("bopx_mssd_batch", 0, ptr(ids, _i32), ptr(pe, _d), ptr(pe, _d), ptr(out, _d))
+
+
+def _cover_ref(de, dg):
+  """Reference formulas of pose_error.cus / cou_bb_proj (pose_error.py:256-330)
+  on two depth maps: union, inter, bboxes (x0, y0, x1, y1; empty: -1)."""
+  me, mg = de > 0, dg > 0
+  row = [float(np.logical_or(me, mg).sum()), float(np.logical_and(me, mg).sum())]
+  for m in (me, mg):
+    ys, xs = m.nonzero()
+    row += [xs.min(), ys.min(), xs.max(), ys.max()] if len(xs) else [2147483647] * 2 + [-1] * 2
+  return np.array(row, np.float64)
+
+
+def test_cover_bit_exact_vs_oracle(oracle_mod):
+  """Silhouette mode of k_vsd (cus, cou_bb_proj) vs the oracle raster: exact
+  counts and bboxes, including empty / behind-camera / off-screen poses."""
+  from bop_toolkit_amd import _lib, pose_error
+  from bop_toolkit_amd._lib import _d, _i32, ptr
+  n = 24
+  rng, pts, faces, Rg, tg, Re, te_, K = _scene(23, n)
+  te_[3] = [0.0, 0.0, -300.0]  # behind the camera: empty est mask
+  te_[4] = [5000.0, 0.0, 800.0]  # off-screen
+  tg[5] = [0.0, 0.0, 70.0]  # very close: guard band
+  ctx = _lib.Context(0)
+  ctx.add_object(4, pts, faces)
+  fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+  ids = np.full(n, 4, np.int32)
+  pe = np.concatenate([Re.reshape(n, 9), te_], 1)
+  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
+  fi = np.zeros(n, np.int32)
+  cam = np.array([[fx, fy, cx, cy]], np.float64)
+  out = np.empty((n, 10))
+  ctx.call("bopx_cover_batch", n, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(fi, _i32), 1,
+           640, 480, ptr(cam, _d), ptr(out, _d))
+  for i in range(n):
+    de = oracle_mod.render_depth(pts, faces, Re[i], te_[i], fx, fy, cx, cy, 640, 480)
+    dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, 640, 480)
+    ref = _cover_ref(de, dg)
+    assert np.array_equal(out[i], ref), (i, out[i], ref)
+    # foreign-renderer path on the same maps
+    from bop_toolkit_amd._lib import _f
+    o2 = np.empty(10)
+    ctx.call("bopx_cover_from_depths", 640, 480, ptr(np.ascontiguousarray(de), _f),
+             ptr(np.ascontiguousarray(dg), _f), ptr(o2, _d))
+    assert np.array_equal(o2, ref), i
+    if ref[0] > 0:
+      assert pose_error.cus_from_cover(out[i]) == 1.0 - ref[1] / ref[0]
+  ctx.close()
+
+
+def test_drop_in_cus_cou_bb_proj(oracle_mod):
+  """pose_error.cus / cou_bb_proj with the HIP renderer and with a foreign
+  (oracle) renderer agree with the reference formulas bit for bit."""
+  from bop_toolkit_amd import misc, pose_error
+  from bop_toolkit_amd.renderer import create_renderer
+  rng, pts, faces, Rg, tg, Re, te_, K = _scene(29, 8)
+  ren = create_renderer(640, 480, "hip", mode="depth")
+  ren.add_object_arrays(6, pts, faces)
+
+  class Foreign:
+    def render_object(self, obj_id, R, t, fx, fy, cx, cy):
+      return {"depth": oracle_mod.render_depth(pts, faces, R, t, fx, fy, cx, cy, 640, 480)}
+
+  fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+  for i in range(8):
+    de = oracle_mod.render_depth(pts, faces, Re[i], te_[i], fx, fy, cx, cy, 640, 480)
+    dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, 640, 480)
+    me, mg = de > 0, dg > 0
+    union = float(np.logical_or(me, mg).sum())
+    cus_ref = 1.0 - np.logical_and(me, mg).sum() / union if union > 0 else 1.0
+    ys, xs = me.nonzero()
+    bbe = misc.calc_2d_bbox(xs, ys)
+    ys, xs = mg.nonzero()
+    bbg = misc.calc_2d_bbox(xs, ys)
+    cou_ref = 1.0 - misc.iou(bbe, bbg)
+    for r in (ren, Foreign()):
+      assert pose_error.cus(Re[i], te_[i], Rg[i], tg[i], K, r, 6) == cus_ref
+      assert pose_error.cou_bb_proj(Re[i], te_[i], Rg[i], tg[i], K, r, 6) == cou_ref
