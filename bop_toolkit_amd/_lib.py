@@ -55,6 +55,10 @@ SIGNATURES = {
     "bopx_cover_batch": (_I, [_CTX, _I64, _i32, _d, _d, _i32, _I64, _I, _I, _d, _d]),
     "bopx_cover_from_depths": (_I, [_CTX, _I, _I, _f, _f, _d]),
     "bopx_cover_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
+    "bopx_gt_info_batch": (_I, [_CTX, _I64, _i32, _d, _i32, _f, _I64, _I, _I, _d, _D, _I, _I,
+                                _d, _u8]),
+    "bopx_gt_info_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _I, _I, _P, _D, _I, _I, _P, _P,
+                                    _P]),
     "bopx_render_depth": (_I, [_CTX, _I, _d, _d, _D, _D, _D, _D, _I, _I, _f]),
     "bopx_dist_im": (_I, [_CTX, _I, _I, _f, _D, _D, _D, _D, _d]),
     "bopx_visib_mask": (_I, [_CTX, _I64, _d, _d, _u8, _D, _I, _I, _u8]),

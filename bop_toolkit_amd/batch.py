@@ -126,6 +126,21 @@ class BatchEvaluator:
                   _stream(self.device))
     return out
 
+  def gt_info(self, slots, pose, frame_idx, frames, cam, delta, canvas_scale=3, masks=False,
+              delta_flags=0):
+    """GT-side statistics (calc_gt_info.py / calc_gt_masks.py): float64 [n, 11]
+    = px_count_all, px_count_visib, silhouette bbox (x0, y0, x1, y1), visible
+    bbox, px_count_valid; with masks=True also uint8 [n, 2, H, W] (0/255:
+    silhouette, visible part). canvas_scale 3 = calc_gt_info's enlarged canvas."""
+    n = slots.numel()
+    H, W = int(frames.shape[-2]), int(frames.shape[-1])
+    out = self._out(n, 11)
+    mk = torch.empty((n, 2, H, W), dtype=torch.uint8, device=self.device) if masks else None
+    self.ctx.call("bopx_gt_info_batch_dev", n, _p(slots), _p(pose), _p(frame_idx), _p(frames),
+                  W, H, _p(cam), float(delta), int(delta_flags), int(canvas_scale), _p(out),
+                  _p(mk), _stream(self.device))
+    return out, mk
+
   def render(self, slots, pose, frame_idx, cam, n_frames, width, height, frames=None):
     """Min-composite depth renders of many instances into n_frames frames
     (instances sharing a frame occlude each other). Returns float32 frames."""

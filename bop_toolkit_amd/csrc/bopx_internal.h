@@ -37,6 +37,8 @@ constexpr int kMaxTaus = 16;
 constexpr int kVsdMaxTiles = 2048;  // k_vsd keeps 16-bit per-lane tau counters
 constexpr int kCostCover = 2;  // k_vsd mode: silhouette union/inter + bboxes (cus, cou_bb_proj)
 constexpr int kCoverCols = 10;  // union, inter, est bbox x0 y0 x1 y1, gt bbox x0 y0 x1 y1
+constexpr int kCostGtInfo = 3;  // k_vsd mode: one (gt) pose, silhouette + visibility stats
+constexpr int kGtInfoCols = 11;  // all, visib, obj bbox x0 y0 x1 y1, visib bbox, valid
 constexpr int kTileW = BOPX_TILE_W;  // VSD screen tile (LDS-resident q pair)
 constexpr int kTileH = BOPX_TILE_H;
 constexpr int kTileStride = kTileW + 1;  // LDS row pitch of a q tile (dwords)
@@ -72,6 +74,9 @@ struct VsdArgs {
   double delta64;
   int n_tau;
   int normalized;
+  int img_w, img_h;  // test-depth frame size (= width/height except GT-info mode)
+  int ox, oy;        // image origin inside the raster canvas (GT-info mode)
+  uint8_t* masks;    // GT-info mode, optional: n x 2 x img_h x img_w (mask, mask_visib)
   int ablate;  // BOPX_VSD_ABLATE, read only by -DBOPX_VSD_DIAG=1 builds (kern_vsd.hip)
   double taus[kMaxTaus];
 };

@@ -171,14 +171,17 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   const gptr<const uint32_t> g_mtri = (gptr<const uint32_t>)o.mlet_tri;
   const gptr<const float> g_mlet = (gptr<const float>)o.mlet;
   const int64_t fidx = a.frame_idx[b];
-  const gptr<const float> frame = (gptr<const float>)(a.frames + fidx * (int64_t)W * H);
+  // test depth: img_w x img_h frames; the raster canvas (W x H) may be larger
+  // with the image at (ox, oy) (GT-info mode, calc_gt_info.py:66-73)
+  const int IW = a.img_w, IH = a.img_h, ox = a.ox, oy = a.oy;
+  const gptr<const float> frame = (gptr<const float>)(a.frames + fidx * (int64_t)IW * IH);
   const double fx = a.cam[4 * fidx + 0], fy = a.cam[4 * fidx + 1];
   const double cx = a.cam[4 * fidx + 2], cy = a.cam[4 * fidx + 3];
   Cam32 c32;
   c32.fx = (float)fx;
   c32.fy = (float)fy;
-  c32.cx = (float)cx;
-  c32.cy = (float)cy;
+  c32.cx = (float)(cx + (double)ox);  // the renderer receives cx + offset (float64)
+  c32.cy = (float)(cy + (double)oy);
   if (tid < 12) {
     s_pose[0][tid] = (float)a.pose_est[12 * b + tid];
     s_pose[1][tid] = (float)a.pose_gt[12 * b + tid];
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   for (int j = 0; j < kRectsPerThread; ++j) {
     const int i = tid + j * kVsdThreads;
     rect[j] = make_short4(1, 1, 0, 0);
-    if (i < 2 * nm) {
+    if (i < 2 * nm && !(COST == kCostGtInfo && i < nm)) {  // GT-info: gt pose only
       const int r = i >= nm, m = i - r * nm;
       rect[j] = meshlet_rect(g_mlet + 8 * (int64_t)m, s_pose[r], c32, W, H);
       if (rect[j].x <= rect[j].z && rect[j].y <= rect[j].w) {
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   __syncthreads();
   const int rx0 = s_roi[0], ry0 = s_roi[1], rx1 = s_roi[2], ry1 = s_roi[3];
 
-  uint32_t c_union = 0, c_inter = 0;
+  uint32_t c_union = 0, c_inter = 0, c_valid = 0;
   // cover mode: est / gt silhouette bboxes (x0, y0, x1, y1), empty = (INT_MAX, INT_MAX, -1, -1)
   int bb[8] = {INT32_MAX, INT32_MAX, -1, -1, INT32_MAX, INT32_MAX, -1, -1};
   // step cost: two 16-bit per-tau counters per register (a lane evaluates at
@@ -237,9 +240,10 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         s_next = 0;
       }
       // float64 distance coefficients of the tile's columns / rows (misc.py:137-138)
-      if (tid < kTileW) s_pX[tid] = ((double)(tx0 + tid) - cx) / fx;
+      if (tid < kTileW) s_pX[tid] = ((double)(tx0 + tid - ox) - cx) / fx;
       if (tid >= kVsdThreads - kTileH)
-        s_pY[tid - (kVsdThreads - kTileH)] = ((double)(ty0 + tid - (kVsdThreads - kTileH)) - cy) / fy;
+        s_pY[tid - (kVsdThreads - kTileH)] =
+            ((double)(ty0 + tid - (kVsdThreads - kTileH) - oy) - cy) / fy;
       __syncthreads();
       VSD_STAMP(0);
 #pragma unroll
@@ -417,9 +421,35 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
           }
           continue;
         }
+        if constexpr (COST == kCostGtInfo) {  // calc_gt_info.py:113-158, calc_gt_masks.py:104-125
+          ++c_union;  // px_count_all (whole canvas silhouette)
+          const int x = col - ox, y = row - oy;
+          bb[0] = min(bb[0], x);
+          bb[1] = min(bb[1], y);
+          bb[2] = max(bb[2], x);
+          bb[3] = max(bb[3], y);
+          if (x < 0 || y < 0 || x >= IW || y >= IH) continue;
+          const double pX = s_pX[p % kTileW], pY = s_pY[p / kTileW];
+          const double dist_g = dist_of(pX, pY, 1.0f / __uint_as_float(qg));
+          const double dist_t = dist_of(pX, pY, frame[(int64_t)y * IW + x]);
+          c_valid += dist_t > 0.0;
+          const bool vis = visib19(dist_t, dist_g, a.delta32, a.delta_f64, a.delta64);
+          uint8_t* mk = a.masks ? a.masks + (2 * b) * (int64_t)IW * IH + (int64_t)y * IW + x
+                                : nullptr;
+          if (mk) mk[0] = 255u;
+          if (vis) {
+            ++c_inter;  // px_count_visib
+            bb[4] = min(bb[4], x);
+            bb[5] = min(bb[5], y);
+            bb[6] = max(bb[6], x);
+            bb[7] = max(bb[7], y);
+            if (mk) mk[(int64_t)IW * IH] = 255u;
+          }
+          continue;
+        }
         const float de = qe ? 1.0f / __uint_as_float(qe) : 0.0f;
         const float dg = qg ? 1.0f / __uint_as_float(qg) : 0.0f;
-        const float dtest = frame[(int64_t)row * W + col];
+        const float dtest = frame[(int64_t)row * IW + col];
         const double pX = s_pX[p % kTileW];
         const double pY = s_pY[p / kTileW];
         const double dist_t = dist_of(pX, pY, dtest);
@@ -474,7 +504,8 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       s_lin[wave][k] = lin[k];
     }
   }
-  if constexpr (COST == kCostCover) {
+  if constexpr (COST == kCostCover || COST == kCostGtInfo) {
+    c_valid = wave_sum_u32(c_valid);
 #pragma unroll
     for (int k = 0; k < 8; ++k)
       for (int off = 32; off > 0; off >>= 1) {
@@ -484,6 +515,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
     if (lane == 0)
 #pragma unroll
       for (int k = 0; k < 8; ++k) s_cnt[wave][2 + k] = (uint32_t)bb[k];
+    if (lane == 0) s_cnt[wave][10] = c_valid;
   }
   __syncthreads();
   VSD_STAMP(7);
@@ -495,10 +527,16 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       un += s_cnt[w][0];
       in += s_cnt[w][1];
     }
-    if constexpr (COST == kCostCover) {
-      double* out = a.out + b * (int64_t)kCoverCols;
+    if constexpr (COST == kCostCover || COST == kCostGtInfo) {
+      // cover: union, inter, 8 bbox values; GT info: all, visib, 8 bbox values, valid
+      double* out = a.out + b * (int64_t)(COST == kCostCover ? kCoverCols : kGtInfoCols);
       out[0] = (double)un;
       out[1] = (double)in;
+      if (COST == kCostGtInfo) {
+        uint64_t valid = 0;
+        for (int w = 0; w < kVsdWaves; ++w) valid += s_cnt[w][10];
+        out[10] = (double)valid;
+      }
       for (int k = 0; k < 8; ++k) {
         int v = (int)s_cnt[0][2 + k];
         for (int w = 1; w < kVsdWaves; ++w) {
@@ -544,8 +582,10 @@ hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s) {
     hipLaunchKernelGGL(k_vsd<0>, grid, block, 0, s, a);
   else if (cost_type == 1)
     hipLaunchKernelGGL(k_vsd<1>, grid, block, 0, s, a);
-  else
+  else if (cost_type == kCostCover)
     hipLaunchKernelGGL(k_vsd<kCostCover>, grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL(k_vsd<kCostGtInfo>, grid, block, 0, s, a);
   return hipGetLastError();
 }
 

@@ -558,8 +558,8 @@ static int fill_vsd_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height, d
   if (cost_type != BOPX_COST_STEP && cost_type != BOPX_COST_TLINEAR)
     return fail(c, BOPX_E_INVALID, "Unknown pixel matching cost.");
   if (int r = check_taus(c, taus, n_tau)) return r;
-  a.width = width;
-  a.height = height;
+  a.width = a.img_w = width;
+  a.height = a.img_h = height;
   a.delta32 = (float)delta;
   a.delta64 = delta;
   a.delta_f64 = (flags & BOPX_DELTA_F64) ? 1 : 0;
@@ -666,9 +666,111 @@ static int cover_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height) {
           ((height + bopx::kTileH - 1) / bopx::kTileH) > bopx::kVsdMaxTiles)
     return fail(c, BOPX_E_UNSUPPORTED, "image %dx%d exceeds the fused kernel's %d tiles",
                 width, height, bopx::kVsdMaxTiles);
-  a.width = width;
-  a.height = height;
+  a.width = a.img_w = width;
+  a.height = a.img_h = height;
   a.n_tau = 0;
+  return BOPX_OK;
+}
+
+// ------------------------------------------------------------------- GT info
+static int gt_info_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height, double delta,
+                        int flags, int canvas_scale) {
+  if (canvas_scale != 1 && canvas_scale != 3)
+    return fail(c, BOPX_E_INVALID, "canvas_scale must be 1 or 3");
+  if (width <= 0 || height <= 0 || (int64_t)width * canvas_scale > 32767 ||
+      (int64_t)height * canvas_scale > 32767)
+    return fail(c, BOPX_E_INVALID, "bad image size %dx%d", width, height);
+  a.img_w = width;
+  a.img_h = height;
+  a.width = width * canvas_scale;
+  a.height = height * canvas_scale;
+  a.ox = canvas_scale == 3 ? width : 0;
+  a.oy = canvas_scale == 3 ? height : 0;
+  a.delta32 = (float)delta;
+  a.delta64 = delta;
+  a.delta_f64 = (flags & BOPX_DELTA_F64) ? 1 : 0;
+  a.n_tau = 0;
+  return BOPX_OK;
+}
+
+int bopx_gt_info_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pose,
+                           const int32_t* frame_idx, const float* frames, int width, int height,
+                           const double* cam, double delta, int flags, int canvas_scale,
+                           double* out, uint8_t* masks, void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (int r = set_dev(c)) return r;
+  bopx::VsdArgs a{};
+  if (int r = gt_info_args(c, a, width, height, delta, flags, canvas_scale)) return r;
+  hipStream_t s = pick_stream(c, stream);
+  if (masks && n > 0)
+    HIPCHK(c, hipMemsetAsync(masks, 0, (size_t)n * 2 * width * height, s));
+  a.objs = c->d_desc;
+  a.slots = slots;
+  a.pose_est = pose;
+  a.pose_gt = pose;
+  a.frame_idx = frame_idx;
+  a.frames = frames;
+  a.cam = cam;
+  a.out = out;
+  a.masks = masks;
+  a.n = n;
+  HIPCHK(c, bopx::launch_vsd(a, bopx::kCostGtInfo, s));
+  return BOPX_OK;
+}
+
+int bopx_gt_info_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double* pose,
+                       const int32_t* frame_idx, const float* frames, int64_t n_frames,
+                       int width, int height, const double* cam, double delta, int flags,
+                       int canvas_scale, double* out, uint8_t* masks) {
+  if (!c) return BOPX_E_INVALID;
+  if (n < 0 || n_frames < 0) return fail(c, BOPX_E_INVALID, "negative size");
+  if (n == 0) return BOPX_OK;
+  if (!obj_ids || !pose || !frame_idx || !frames || !cam || !out)
+    return fail(c, BOPX_E_INVALID, "NULL buffer");
+  for (int64_t i = 0; i < n; ++i)
+    if (frame_idx[i] < 0 || frame_idx[i] >= n_frames)
+      return fail(c, BOPX_E_INVALID, "frame_idx[%lld] = %d out of range", (long long)i,
+                  frame_idx[i]);
+  if (int r = set_dev(c)) return r;
+  bopx::VsdArgs a{};
+  if (int r = gt_info_args(c, a, width, height, delta, flags, canvas_scale)) return r;
+  std::vector<int32_t> slots;
+  if (int r = map_slots(c, n, obj_ids, slots, false, true)) return r;
+  const size_t fpx = (size_t)width * height, cols = bopx::kGtInfoCols;
+  const size_t mbytes = masks ? 2 * fpx * (size_t)n : 0;
+  if (int r = ws_reserve(c, carve_size({4 * (size_t)n, 96 * (size_t)n, 4 * (size_t)n,
+                                        4 * fpx * (size_t)n_frames, 32 * (size_t)n_frames,
+                                        8 * cols * (size_t)n, mbytes})))
+    return r;
+  Carve cv{(char*)c->ws.p};
+  int32_t* d_s = cv.take<int32_t>(n);
+  double* d_p = cv.take<double>(12 * n);
+  int32_t* d_fi = cv.take<int32_t>(n);
+  float* d_fr = cv.take<float>(fpx * n_frames);
+  double* d_cam = cv.take<double>(4 * n_frames);
+  double* d_out = cv.take<double>(cols * n);
+  uint8_t* d_m = masks ? cv.take<uint8_t>(mbytes) : nullptr;
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_s, slots.data(), 4 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_p, pose, 96 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_fi, frame_idx, 4 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_fr, frames, 4 * fpx * n_frames, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_cam, cam, 32 * n_frames, hipMemcpyHostToDevice, s));
+  if (d_m) HIPCHK(c, hipMemsetAsync(d_m, 0, mbytes, s));
+  a.objs = c->d_desc;
+  a.slots = d_s;
+  a.pose_est = d_p;
+  a.pose_gt = d_p;
+  a.frame_idx = d_fi;
+  a.frames = d_fr;
+  a.cam = d_cam;
+  a.out = d_out;
+  a.masks = d_m;
+  a.n = n;
+  HIPCHK(c, bopx::launch_vsd(a, bopx::kCostGtInfo, s));
+  HIPCHK(c, hipMemcpyAsync(out, d_out, 8 * cols * n, hipMemcpyDeviceToHost, s));
+  if (d_m) HIPCHK(c, hipMemcpyAsync(masks, d_m, mbytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
   return BOPX_OK;
 }
 

@@ -1,0 +1,166 @@
+"""GT-side counterparts of scripts/calc_gt_info.py and scripts/calc_gt_masks.py
+(SURVEY.md §8f-3): the same raster + bop19 visibility as VSD, one fused
+launch per batch of GT instances (k_vsd GT-info mode) instead of one OpenGL
+render and three full-frame NumPy passes per instance.
+
+    python -m bop_toolkit_amd.gt_side info  --dataset lmo --dataset_split test
+    python -m bop_toolkit_amd.gt_side masks --dataset lmo --dataset_split test
+
+Outputs are the reference's: scene_gt_info.json (px_count_all /_valid /_visib,
+visib_fract, bbox_obj, bbox_visib per GT, calc_gt_info.py:113-168) and the
+mask / mask_visib PNGs (0/255, calc_gt_masks.py:104-125). calc_gt_info uses
+a canvas three times the image with the image in its centre, so silhouettes of
+objects truncated by the image border are counted whole (calc_gt_info.py:66-73,
+104-107); calc_gt_masks renders at image size. The reference's
+calc_gt_masks.py processes a hard-coded `scene_ids = [0]` (calc_gt_masks.py:56);
+here every present scene is processed unless --scene_ids narrows it.
+"""
+import argparse
+import os
+
+import numpy as np
+
+from . import dataset_params, inout, misc
+
+INFO_KEYS = ("px_count_all", "px_count_valid", "px_count_visib", "visib_fract", "bbox_obj",
+             "bbox_visib")
+
+
+def info_from_row(row):
+  """One scene_gt_info entry from a k_vsd GT-info row."""
+  n_all, n_visib, n_valid = int(row[0]), int(row[1]), int(row[10])
+  bb = [int(v) for v in row[2:10]]
+  bbox_obj, bbox_visib = [-1, -1, -1, -1], [-1, -1, -1, -1]
+  if n_visib > 0:  # both boxes only when something is visible (calc_gt_info.py:139-151)
+    bbox_obj = [bb[0], bb[1], bb[2] - bb[0], bb[3] - bb[1]]
+    bbox_visib = [bb[4], bb[5], bb[6] - bb[4], bb[7] - bb[5]]
+  return {"px_count_all": n_all, "px_count_valid": n_valid, "px_count_visib": n_visib,
+          "visib_fract": float(n_visib / float(n_all) if n_all > 0 else 0.0),
+          "bbox_obj": bbox_obj, "bbox_visib": bbox_visib}
+
+
+def _depth_path(dp_split, scene_id, im_id):
+  path = dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id)
+  return path if os.path.exists(path) else path.replace(".tif", ".png")
+
+
+def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_batch=128):
+  """Per image id: list of (row, masks or None) per GT instance, in GT order;
+  images are evaluated in batches of im_batch frames."""
+  from . import runtime
+  scene_camera = inout.load_scene_camera(dp_split["scene_camera_tpath"].format(scene_id=scene_id))
+  scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+  im_ids = sorted(scene_gt.keys())
+  res = {}
+  dev = ev.device
+  for i0 in range(0, len(im_ids), im_batch):
+    ims = im_ids[i0:i0 + im_batch]
+    frames, cam, obj, pose, fidx, owner = [], [], [], [], [], []
+    for k, im_id in enumerate(ims):
+      d = inout.load_depth(_depth_path(dp_split, scene_id, im_id))
+      d *= scene_camera[im_id]["depth_scale"]  # float32 in place, calc_gt_info.py:99-100
+      frames.append(d)
+      K = scene_camera[im_id]["cam_K"]
+      cam.append((K[0, 0], K[1, 1], K[0, 2], K[1, 2]))
+      for gt in scene_gt[im_id]:
+        obj.append(gt["obj_id"])
+        pose.append(np.concatenate([gt["cam_R_m2c"].reshape(9), gt["cam_t_m2c"].reshape(3)]))
+        fidx.append(k)
+        owner.append(im_id)
+      res[im_id] = []
+    if not obj:
+      continue
+    T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+    rows, mk = ev.gt_info(ev.slots(obj), T(np.stack(pose), torch.float64),
+                          T(np.array(fidx, np.int32), torch.int32),
+                          T(np.stack(frames), torch.float32), T(np.array(cam), torch.float64),
+                          delta, canvas_scale, masks, runtime.delta_flags(delta))
+    rows = rows.cpu().numpy()
+    mk = mk.cpu().numpy() if mk is not None else None
+    for j, im_id in enumerate(owner):
+      res[im_id].append((rows[j], None if mk is None else mk[j]))
+  return res
+
+
+def _setup(p):
+  import torch
+  from .batch import BatchEvaluator
+  dp_split = dataset_params.get_split_params(p["datasets_path"], p["dataset"],
+                                             p["dataset_split"], p["dataset_split_type"])
+  dp_model = dataset_params.get_model_params(p["datasets_path"], p["dataset"],
+                                             "cad" if p["dataset"] == "tless" else None)
+  ev = BatchEvaluator(p.get("device", 0))
+  misc.log("Initializing renderer...")
+  for obj_id in dp_model["obj_ids"]:
+    path = dp_model["model_tpath"].format(obj_id=obj_id)
+    if os.path.exists(path):
+      m = inout.load_ply(path)
+      ev.add_object(obj_id, m["pts"], m["faces"])
+  scene_ids = p.get("scene_ids") or dataset_params.get_present_scene_ids(dp_split)
+  return torch, ev, dp_split, scene_ids
+
+
+def calc_gt_info(p):
+  """scene_gt_info.json of every scene (calc_gt_info.py:75-175); returns paths."""
+  torch, ev, dp_split, scene_ids = _setup(p)
+  written = []
+  for scene_id in scene_ids:
+    misc.log("Calculating GT info - dataset: {} ({}, {}), scene: {}".format(
+        p["dataset"], p["dataset_split"], p["dataset_split_type"], scene_id))
+    stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 3, False)
+    info = {im_id: [info_from_row(r) for r, _ in lst] for im_id, lst in stats.items()}
+    path = dp_split["scene_gt_info_tpath"].format(scene_id=scene_id)
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    inout.save_json(path, info)
+    written.append(path)
+  return written
+
+
+def calc_gt_masks(p):
+  """mask / mask_visib PNGs of every GT instance (calc_gt_masks.py:58-125)."""
+  from PIL import Image
+  torch, ev, dp_split, scene_ids = _setup(p)
+  written = []
+  for scene_id in scene_ids:
+    if not os.path.exists(dp_split["scene_gt_tpath"].format(scene_id=scene_id)):
+      print("Skip scene {} (GT file not found).".format(scene_id))
+      continue
+    misc.log("Calculating masks - dataset: {} ({}, {}), scene: {}".format(
+        p["dataset"], p["dataset_split"], p["dataset_split_type"], scene_id))
+    stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 1, True)
+    for im_id, lst in stats.items():
+      for gt_id, (_, mk) in enumerate(lst):
+        for plane, key in enumerate(("mask_tpath", "mask_visib_tpath")):
+          path = dp_split[key].format(scene_id=scene_id, im_id=im_id, gt_id=gt_id)
+          os.makedirs(os.path.dirname(path), exist_ok=True)
+          Image.fromarray(mk[plane]).save(path)
+          written.append(path)
+  return written
+
+
+def parse_args(argv=None):
+  ap = argparse.ArgumentParser()
+  ap.add_argument("task", choices=["info", "masks"])
+  ap.add_argument("--dataset", default="lmo")
+  ap.add_argument("--dataset_split", default="test")
+  ap.add_argument("--dataset_split_type", default=None)
+  ap.add_argument("--delta", type=float, default=15)
+  ap.add_argument("--renderer_type", default="hip")
+  ap.add_argument("--datasets_path", default=os.environ.get("BOP_PATH", "/path/to/bop"))
+  ap.add_argument("--scene_ids", default="")
+  a = ap.parse_args(argv)
+  delta = int(a.delta) if float(a.delta).is_integer() else a.delta  # reference: int 15
+  p = {"dataset": a.dataset, "dataset_split": a.dataset_split,
+       "dataset_split_type": a.dataset_split_type, "delta": delta,
+       "renderer_type": a.renderer_type, "datasets_path": a.datasets_path,
+       "scene_ids": [int(x) for x in a.scene_ids.split(",") if x]}
+  return a.task, p
+
+
+def main(argv=None):
+  task, p = parse_args(argv)
+  (calc_gt_info if task == "info" else calc_gt_masks)(p)
+
+
+if __name__ == "__main__":
+  main()

@@ -142,6 +142,22 @@ int bopx_cover_batch(bopx_ctx* ctx, int64_t n, const int32_t* obj_ids,
 int bopx_cover_from_depths(bopx_ctx* ctx, int width, int height, const float* depth_est,
                            const float* depth_gt, double* out);
 
+/* ---- GT-side statistics: calc_gt_info.py:95-160, calc_gt_masks.py:95-125 -- */
+/* For n GT instances (obj_ids, pose n x 12 [R | t]) in test frames
+ * (frames n_frames x height x width float32 depth in mm, cam n_frames x 4):
+ * the instance is rasterised on a canvas canvas_scale (1 or 3) times the image
+ * (3 = calc_gt_info's enlarged canvas, the image in its centre; 1 =
+ * calc_gt_masks), compared with the test depth (bop19 visibility, tolerance
+ * delta). out n x 11 float64: px_count_all (whole canvas silhouette),
+ * px_count_visib, silhouette bbox (x0, y0, x1, y1 in image coordinates),
+ * visible-part bbox (x0, y0, x1, y1; x1 = -1 when empty), px_count_valid.
+ * masks (optional, NULL = none): n x 2 x height x width uint8, 255 inside the
+ * silhouette (plane 0) and the visible part (plane 1), 0 elsewhere. */
+int bopx_gt_info_batch(bopx_ctx* ctx, int64_t n, const int32_t* obj_ids, const double* pose,
+                       const int32_t* frame_idx, const float* frames, int64_t n_frames,
+                       int width, int height, const double* cam, double delta, int flags,
+                       int canvas_scale, double* out, uint8_t* masks);
+
 /* ---- renderer plugin (renderer.py:62-74) ---------------------------------- */
 /* Depth (eye Z in model units, 0 = background) of one object in one pose;
  * out: height x width float32. */
@@ -187,6 +203,10 @@ int bopx_cover_batch_dev(bopx_ctx* ctx, int64_t n, const int32_t* slots,
                          const double* pose_est, const double* pose_gt,
                          const int32_t* frame_idx, int width, int height, const double* cam,
                          double* out, void* stream);
+int bopx_gt_info_batch_dev(bopx_ctx* ctx, int64_t n, const int32_t* slots, const double* pose,
+                           const int32_t* frame_idx, const float* frames, int width,
+                           int height, const double* cam, double delta, int flags,
+                           int canvas_scale, double* out, uint8_t* masks, void* stream);
 /* Composite render of many (object, pose) instances into frames:
  * frames (n_frames x h x w f32, device) must be pre-filled with +inf bit
  * patterns by bopx_depth_clear_dev; instances are min-composited (z-buffer);

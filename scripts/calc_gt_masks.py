@@ -1,0 +1,10 @@
+"""Drop-in for the reference's scripts/calc_gt_masks.py (bop_toolkit_amd.gt_side masks)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from bop_toolkit_amd.gt_side import main  # noqa: E402
+
+if __name__ == "__main__":
+  main(["masks"] + sys.argv[1:])

@@ -12,12 +12,15 @@ validity rules, and scripts/eval_bop19_pose.py (which spawns the other two
 scores_bop19.json). They pin tuple enumeration, n_top, gates, the per-tau VSD
 split, the JSON layout, error values, matching, recall and the BOP19 average
 recalls of bop_toolkit_amd (tests/test_e2e_errors.py, tests/test_scores.py).
+scripts/calc_gt_info.py and scripts/calc_gt_masks.py run on a copy of the
+dataset; their scene_gt_info.json and masks go to expected_gt/
+(tests/test_gt_side.py).
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_e2e.py
 
 Harness stubs, installed by a generated sitecustomize.py in
 every reference interpreter: imageio/png are absent here, so `imageio`
-is a module whose imread is backed by Pillow and `png` an empty module;
+is a module whose imread/imwrite are backed by Pillow and `png` an empty module;
 NumPy 2 removed np.float, which the reference's inout uses, so it is set to
 float. The reference's OpenGL renderers cannot run here: the vispy slot
 (`bop_toolkit_lib.renderer_vispy`, honoured by renderer.create_renderer) is
@@ -154,6 +157,7 @@ np.float = float  # removed in NumPy 2, used by the reference's inout
 from PIL import Image
 imageio = types.ModuleType("imageio")
 imageio.imread = lambda p: np.asarray(Image.open(p))
+imageio.imwrite = lambda p, im, **kw: Image.fromarray(np.asarray(im)).save(p)
 sys.modules["imageio"] = imageio
 sys.modules["png"] = types.ModuleType("png")
 
@@ -178,6 +182,16 @@ class RendererVispy:  # fills the vispy slot of renderer.create_renderer
 mod = types.ModuleType("bop_toolkit_lib.renderer_vispy")
 mod.RendererVispy = RendererVispy
 sys.modules["bop_toolkit_lib.renderer_vispy"] = mod
+
+# calc_gt_info.py / calc_gt_masks.py hard-code their dataset ('gist', a local
+# path) in the script body: point the split/model lookups at the golden copy.
+import os as _os
+if _os.environ.get("BOPX_GT_REDIRECT"):
+  _path, _name, _split = _os.environ["BOPX_GT_REDIRECT"].split(":")
+  from bop_toolkit_lib import dataset_params as _dp
+  _gsp, _gmp = _dp.get_split_params, _dp.get_model_params
+  _dp.get_split_params = lambda p, n, s, t=None: _gsp(_path, _name, _split, t)
+  _dp.get_model_params = lambda p, n, t=None: _gmp(_path, _name, t)
 """
 
 # (error folder, extra arguments) of the standalone eval_calc_scores runs
@@ -197,6 +211,33 @@ SCORE_RUNS = [
 def run_ref(script, args, env):
   subprocess.run([sys.executable, os.path.join(REF, "scripts", script)] + args, env=env,
                  check=True, stdout=subprocess.DEVNULL)
+
+
+def gt_side(env, datasets, tmp):
+  """calc_gt_info.py and calc_gt_masks.py on a copy of the dataset: scene 0 is
+  a copy of scene 2 (calc_gt_masks.py processes scene_ids = [0] only) and
+  models/ a copy of models_eval/ (the scripts use the default model type)."""
+  import shutil as sh
+  root = os.path.join(tmp, "gt")
+  sh.copytree(datasets, root)
+  split = os.path.join(root, "lmo", "test")
+  sh.copytree(os.path.join(split, "%06d" % SCENE), os.path.join(split, "000000"))
+  sh.copytree(os.path.join(root, "lmo", "models_eval"), os.path.join(root, "lmo", "models"))
+  genv = dict(env, BOPX_GT_REDIRECT="%s:lmo:test" % root)
+  run_ref("calc_gt_info.py", [], genv)
+  run_ref("calc_gt_masks.py", [], genv)
+  out = os.path.join(OUT, "expected_gt")
+  os.makedirs(out)
+  sh.copy(os.path.join(split, "%06d" % SCENE, "scene_gt_info.json"),
+          os.path.join(out, "scene_gt_info_%06d.json" % SCENE))
+  from PIL import Image
+  masks = {}
+  for kind in ("mask", "mask_visib"):
+    d = os.path.join(split, "000000", kind)
+    for fn in sorted(os.listdir(d)):
+      m = np.asarray(Image.open(os.path.join(d, fn)))
+      masks["%s_%s" % (kind, os.path.splitext(fn)[0])] = np.packbits(m > 0)
+  np.savez_compressed(os.path.join(out, "masks_scene0.npz"), **masks)
 
 
 def main():
@@ -241,6 +282,7 @@ def main():
                                                    os.path.join(ev19, name)))
           os.makedirs(os.path.dirname(dst), exist_ok=True)
           shutil.copy(os.path.join(root, fn), dst)
+    gt_side(env, datasets, tmp)
   with open(os.path.join(OUT, "runs.json"), "w") as f:
     json.dump({"result": RESULT, "runs": RUNS, "score_runs": SCORE_RUNS,
                "depth_scale": DEPTH_SCALE}, f, indent=1)
