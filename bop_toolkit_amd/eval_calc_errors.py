@@ -213,12 +213,11 @@ def evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, mode
   if et == "vsd":
     ims = sorted({recs[ri]["im_id"] for ri, _, _, _ in todo})
     frame_of = {im: k for k, im in enumerate(ims)}
-    depths = []
+    depths = inout.load_depths(dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id)
+                               for im_id in ims)
     cam = np.empty((len(ims), 4), np.float64)
     for k, im_id in enumerate(ims):
-      d = inout.load_depth(dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id))
-      d *= scene_camera[im_id]["depth_scale"]  # float32 in place, eval_calc_errors.py:242-243
-      depths.append(d)
+      depths[k] *= scene_camera[im_id]["depth_scale"]  # float32 in place, :242-243
       K = scene_camera[im_id]["cam_K"]
       cam[k] = (K[0, 0], K[1, 1], K[0, 2], K[1, 2])
     frames = T(np.stack(depths), torch.float32)

@@ -55,11 +55,10 @@ def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_ba
   dev = ev.device
   for i0 in range(0, len(im_ids), im_batch):
     ims = im_ids[i0:i0 + im_batch]
-    frames, cam, obj, pose, fidx, owner = [], [], [], [], [], []
+    frames = inout.load_depths(_depth_path(dp_split, scene_id, im_id) for im_id in ims)
+    cam, obj, pose, fidx, owner = [], [], [], [], []
     for k, im_id in enumerate(ims):
-      d = inout.load_depth(_depth_path(dp_split, scene_id, im_id))
-      d *= scene_camera[im_id]["depth_scale"]  # float32 in place, calc_gt_info.py:99-100
-      frames.append(d)
+      frames[k] *= scene_camera[im_id]["depth_scale"]  # float32 in place, calc_gt_info.py:99-100
       K = scene_camera[im_id]["cam_K"]
       cam.append((K[0, 0], K[1, 1], K[0, 2], K[1, 2]))
       for gt in scene_gt[im_id]:

@@ -204,3 +204,16 @@ def load_bop_results(path, version="bop19"):
           "t": np.array([float(x) for x in e[5].split()], np.float64).reshape((3, 1)),
           "time": float(e[6])})
   return results
+
+
+def load_depths(paths, workers=None):
+  """load_depth of many files, decoded in a thread pool (Pillow's PNG/TIFF
+  decoders release the GIL), in input order."""
+  from concurrent.futures import ThreadPoolExecutor
+  paths = list(paths)
+  if len(paths) <= 1:
+    return [load_depth(p) for p in paths]
+  import os
+  n = workers or min(16, os.cpu_count() or 1, len(paths))
+  with ThreadPoolExecutor(n) as pool:
+    return list(pool.map(load_depth, paths))
