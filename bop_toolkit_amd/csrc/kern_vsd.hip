@@ -367,11 +367,9 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
             }
             for (int p = lane; p < wn; p += 64) {
               const RRow rec = s_rec[wave][s_own[wave][p]];
-              r_walk_row(rec, wb + p - (int)(rec.meta >> 19),
-                         [&](int pose, int col, int row, float q) {
-                           if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], 1ull);
-                           atomicMax(&s_dep[pose][row * kTileStride + col], __float_as_uint(q));
-                         });
+              const int fr = r_walk_row_max(rec, wb + p - (int)(rec.meta >> 19),
+                                            s_dep[(rec.meta >> 18) & 1u]);
+              if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
             }
           }
           VSD_STAMP(11);
