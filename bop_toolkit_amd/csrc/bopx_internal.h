@@ -74,6 +74,7 @@ struct VsdArgs {
   double delta64;
   int n_tau;
   int normalized;
+  int max_nm;        // most meshlets of a registered object (sizes the rect registers)
   int img_w, img_h;  // test-depth frame size (= width/height except GT-info mode)
   int ox, oy;        // image origin inside the raster canvas (GT-info mode)
   uint8_t* masks;    // GT-info mode, optional: n x 2 x img_h x img_w (mask, mask_visib)

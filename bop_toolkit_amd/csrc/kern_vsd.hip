@@ -136,9 +136,13 @@ constexpr int kPixPerWave = kTileW * kTileH / kVsdThreads * 64;  // covered-pixe
 static_assert(sizeof(RRow) * 64 * kVsdWaves >= 2 * kPixPerWave * kVsdWaves,
               "pixel lists overlay the raster records");
 constexpr int kGroup = BOPX_VSD_GROUP;  // (pose, meshlet) entries staged together per wave step
-constexpr int kRectsPerThread = 2 * kMaxMeshlets / kVsdThreads;
+constexpr int kRectsPerThread = 2 * kMaxMeshlets / kVsdThreads;  // worst case (RPT)
 
-template <int COST>  // 0 = step, 1 = tlinear, kCostCover = silhouette overlap only
+// COST: 0 = step, 1 = tlinear, kCostCover = silhouette overlap, kCostGtInfo = GT stats.
+// RPT: meshlet rectangles held per thread (1, 2 or 4): the launch picks the
+// smallest that covers 2 x the most meshlets of any registered object, so
+// objects of up to 16k triangles keep 6 fewer VGPRs live through the tile loop.
+template <int COST, int RPT>
 // Two workgroups per CU: 2 * kVsdThreads / 256 waves per SIMD (caps VGPRs at 128).
 __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdArgs a) {
   // q = 1/Z bits, 0 = empty; rows padded by one dword so lanes that walk the
@@ -193,9 +197,9 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   __syncthreads();
 
   // 1. per-pose meshlet rectangles (kept in registers: entry tid + 256 j) + ROI.
-  short4 rect[kRectsPerThread];
+  short4 rect[RPT];
 #pragma unroll
-  for (int j = 0; j < kRectsPerThread; ++j) {
+  for (int j = 0; j < RPT; ++j) {
     const int i = tid + j * kVsdThreads;
     rect[j] = make_short4(1, 1, 0, 0);
     if (i < 2 * nm && !(COST == kCostGtInfo && i < nm)) {  // GT-info: gt pose only
@@ -247,7 +251,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       __syncthreads();
       VSD_STAMP(0);
 #pragma unroll
-      for (int j = 0; j < kRectsPerThread; ++j) {
+      for (int j = 0; j < RPT; ++j) {
         const short4 rc = rect[j];
         if (rc.x <= tx1 && rc.z >= tx0 && rc.y <= ty1 && rc.w >= ty0 && rc.x <= rc.z &&
             rc.y <= rc.w)
@@ -573,17 +577,28 @@ hipError_t read_vsd_stats(unsigned long long* out, int reset) {
   return e == hipSuccess ? hipMemcpyToSymbol(HIP_SYMBOL(g_vsd_time), z, sizeof(z)) : e;
 }
 
-hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s) {
-  if (a.n <= 0) return hipSuccess;
+template <int RPT>
+static void launch_vsd_rpt(const VsdArgs& a, int cost_type, hipStream_t s) {
   dim3 grid((unsigned)a.n), block(kVsdThreads);
   if (cost_type == 0)
-    hipLaunchKernelGGL(k_vsd<0>, grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_vsd<0, RPT>), grid, block, 0, s, a);
   else if (cost_type == 1)
-    hipLaunchKernelGGL(k_vsd<1>, grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_vsd<1, RPT>), grid, block, 0, s, a);
   else if (cost_type == kCostCover)
-    hipLaunchKernelGGL(k_vsd<kCostCover>, grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_vsd<kCostCover, RPT>), grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL(k_vsd<kCostGtInfo>, grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_vsd<kCostGtInfo, RPT>), grid, block, 0, s, a);
+}
+
+hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s) {
+  if (a.n <= 0) return hipSuccess;
+  const int need = 2 * a.max_nm;
+  if (need <= kVsdThreads)
+    launch_vsd_rpt<1>(a, cost_type, s);
+  else if (need <= 2 * kVsdThreads)
+    launch_vsd_rpt<2>(a, cost_type, s);
+  else
+    launch_vsd_rpt<kRectsPerThread>(a, cost_type, s);
   return hipGetLastError();
 }
 

@@ -54,6 +54,7 @@ struct bopx_ctx {
   size_t desc_cap = 0;
   int max_nf = 0;
   int max_ns = 0;  // most symmetries of a live object (MSSD/MSPD grid)
+  int max_nm = 0;  // most meshlets of a live object (k_vsd rect registers)
   DevBuf ws;  // scratch for host-buffer calls
 };
 
@@ -123,7 +124,7 @@ static size_t carve_size(std::initializer_list<size_t> bytes) {
 
 int sync_desc(bopx_ctx* c) {
   std::vector<ObjDesc> h(c->objs.size());
-  int max_nf = 0, max_ns = 0;
+  int max_nf = 0, max_ns = 0, max_nm = 0;
   for (size_t i = 0; i < c->objs.size(); ++i) {
     const Object& o = c->objs[i];
     ObjDesc d{};
@@ -142,11 +143,13 @@ int sync_desc(bopx_ctx* c) {
       d.ns = (int)o.ns;
       max_nf = std::max(max_nf, (int)o.nf);
       max_ns = std::max(max_ns, (int)o.ns);
+      max_nm = std::max(max_nm, (int)o.nm);
     }
     h[i] = d;
   }
   c->max_nf = max_nf;
   c->max_ns = max_ns;
+  c->max_nm = max_nm;
   if (h.size() > c->desc_cap) {
     if (c->d_desc) HIPCHK(c, hipFree(c->d_desc));
     size_t cap = std::max<size_t>(64, h.size() * 2);
@@ -586,6 +589,7 @@ int bopx_vsd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doubl
                             cost_type))
     return r;
   a.objs = c->d_desc;
+  a.max_nm = c->max_nm;
   a.slots = slots;
   a.pose_est = pe;
   a.pose_gt = pg;
@@ -643,6 +647,7 @@ int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double*
   HIPCHK(c, hipMemcpyAsync(d_cam, cam, 32 * n_frames, hipMemcpyHostToDevice, s));
   HIPCHK(c, hipMemcpyAsync(d_dia, diameters, 8 * n, hipMemcpyHostToDevice, s));
   a.objs = c->d_desc;
+  a.max_nm = c->max_nm;
   a.slots = d_s;
   a.pose_est = d_pe;
   a.pose_gt = d_pg;
@@ -705,6 +710,7 @@ int bopx_gt_info_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const d
   if (masks && n > 0)
     HIPCHK(c, hipMemsetAsync(masks, 0, (size_t)n * 2 * width * height, s));
   a.objs = c->d_desc;
+  a.max_nm = c->max_nm;
   a.slots = slots;
   a.pose_est = pose;
   a.pose_gt = pose;
@@ -758,6 +764,7 @@ int bopx_gt_info_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const dou
   HIPCHK(c, hipMemcpyAsync(d_cam, cam, 32 * n_frames, hipMemcpyHostToDevice, s));
   if (d_m) HIPCHK(c, hipMemsetAsync(d_m, 0, mbytes, s));
   a.objs = c->d_desc;
+  a.max_nm = c->max_nm;
   a.slots = d_s;
   a.pose_est = d_p;
   a.pose_gt = d_p;
@@ -782,6 +789,7 @@ int bopx_cover_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const dou
   bopx::VsdArgs a{};
   if (int r = cover_args(c, a, width, height)) return r;
   a.objs = c->d_desc;
+  a.max_nm = c->max_nm;
   a.slots = slots;
   a.pose_est = pe;
   a.pose_gt = pg;
@@ -829,6 +837,7 @@ int bopx_cover_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const doubl
   HIPCHK(c, hipMemcpyAsync(d_fi, frame_idx, 4 * n, hipMemcpyHostToDevice, s));
   HIPCHK(c, hipMemcpyAsync(d_cam, cam, 32 * n_frames, hipMemcpyHostToDevice, s));
   a.objs = c->d_desc;
+  a.max_nm = c->max_nm;
   a.slots = d_s;
   a.pose_est = d_pe;
   a.pose_gt = d_pg;
