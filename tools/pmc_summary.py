@@ -19,7 +19,7 @@ import os
 import sys
 from collections import defaultdict
 
-SHORT = {"k_vsd<0>": "k_vsd", "k_sym_error<0>": "k_sym_error<MSSD>",
+SHORT = {"k_vsd<0>": "k_vsd", "k_vsd<0,": "k_vsd", "k_sym_error<0>": "k_sym_error<MSSD>",
          "k_sym_error<1>": "k_sym_error<MSPD>"}
 
 
