@@ -105,6 +105,8 @@ def evaluate(p, device=0, calc_errors=True):
     for error in p["errors"]:
       if calc_errors:
         ece.run(ece.parse_args(errors_argv(p, error, result_filename)), device)
+      if ece._dist()[0] != 0:  # scores are host bookkeeping on rank 0
+        continue
       if error["type"] == "vsd":
         signs = [misc.get_error_signature("vsd", error["n_top"],
                                           vsd_delta=error["vsd_deltas"][dataset], vsd_tau=tau)
@@ -126,6 +128,8 @@ def evaluate(p, device=0, calc_errors=True):
       average_recalls[error["type"]] = np.mean(recalls)
       misc.log("Recall scores: {}".format(" ".join(map(str, recalls))))
       misc.log("Average recall: {}".format(average_recalls[error["type"]]))
+    if ece._dist()[0] != 0:
+      continue
     misc.log("Evaluation of {} took {}s.".format(result_filename, time.time() - t0))
     final = {"bop19_average_recall_{}".format(e["type"]): average_recalls[e["type"]]
              for e in p["errors"]}
@@ -142,7 +146,9 @@ def evaluate(p, device=0, calc_errors=True):
 
 
 def main(argv=None):
-  evaluate(parse_args(argv), int(os.environ.get("LOCAL_RANK", os.environ.get("BOPX_DEVICE", 0))))
+  from . import shard
+  _, _, local = shard.init_from_env()  # torchrun: errors sharded, scores on rank 0
+  evaluate(parse_args(argv), local)
 
 
 if __name__ == "__main__":

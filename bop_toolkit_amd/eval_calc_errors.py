@@ -176,14 +176,13 @@ def _pose12(R, t):
                          np.asarray(t, np.float64).reshape(3)])
 
 
-def evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, models_info,
-             symmetric_ids):
-  """errors dict per record; the gated-in tuples of the scene are evaluated
-  as one GPU batch."""
+def plan(p, recs, models_info):
+  """Host gates of every (record, GT) pair: errs with the filled values and
+  None placeholders, and the todo list [(record, gt_id, R_g, t_g)] for the GPU."""
   et = p["error_type"]
   n_tau = len(p["vsd_taus"])
   errs = [dict() for _ in recs]
-  todo = []  # (record, gt_id, R_g, t_g)
+  todo = []
   for ri, r in enumerate(recs):
     for gt_id, gt in r["gts"]:
       R_g, t_g = gt["cam_R_m2c"], gt["cam_t_m2c"]
@@ -198,10 +197,25 @@ def evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, mode
         e_te = pose_error.te(r["t"], t_g)
         errs[ri][gt_id] = {"re": [e_re], "te": [e_te], "rete": [e_re, e_te]}[et]
       else:
-        errs[ri][gt_id] = None  # filled from the batch below
+        errs[ri][gt_id] = None  # filled from the GPU batch
         todo.append((ri, gt_id, R_g, t_g))
-  if not todo:
-    return errs
+  return errs, todo
+
+
+def row_to_errors(et, row):
+  """Error list of one tuple from its raw batch row (VSD: n_tau values, CUS:
+  the silhouette-overlap row, others: one value)."""
+  if et == "vsd":
+    return [float(v) for v in row]
+  if et == "cus":
+    return [pose_error.cus_from_cover(row)]
+  return [float(row[0])]
+
+
+def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, models_info,
+                   symmetric_ids, todo):
+  """Raw float64 rows [len(todo), C] of the GPU evaluation of todo."""
+  et = p["error_type"]
   dev = ev.device
   n = len(todo)
   obj = np.array([recs[ri]["obj_id"] for ri, _, _, _ in todo], np.int32)
@@ -210,41 +224,34 @@ def evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, mode
   T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
   slots = ev.slots(obj)
   d_pe, d_pg = T(pe, torch.float64), T(pg, torch.float64)
-  if et == "vsd":
-    ims = sorted({recs[ri]["im_id"] for ri, _, _, _ in todo})
-    frame_of = {im: k for k, im in enumerate(ims)}
-    depths = inout.load_depths(dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id)
-                               for im_id in ims)
-    cam = np.empty((len(ims), 4), np.float64)
-    for k, im_id in enumerate(ims):
-      depths[k] *= scene_camera[im_id]["depth_scale"]  # float32 in place, :242-243
-      K = scene_camera[im_id]["cam_K"]
-      cam[k] = (K[0, 0], K[1, 1], K[0, 2], K[1, 2])
-    frames = T(np.stack(depths), torch.float32)
-    fidx = np.array([frame_of[recs[ri]["im_id"]] for ri, _, _, _ in todo], np.int32)
-    dia = np.array([models_info[o]["diameter"] for o in obj], np.float64)
-    delta = p["vsd_deltas"][dataset]
-    from . import runtime
-    out = ev.vsd(slots, d_pe, d_pg, T(fidx, torch.int32), frames, T(cam, torch.float64), delta,
-                 p["vsd_taus"], T(dia, torch.float64),
-                 normalized_by_diameter=p["vsd_normalized_by_diameter"], cost_type="step",
-                 delta_flags=runtime.delta_flags(delta))
-  elif et == "cus":
+  if et in ("vsd", "cus"):
     ims = sorted({recs[ri]["im_id"] for ri, _, _, _ in todo})
     frame_of = {im: k for k, im in enumerate(ims)}
     cam = np.array([[K[0, 0], K[1, 1], K[0, 2], K[1, 2]]
                     for K in (scene_camera[im]["cam_K"] for im in ims)], np.float64)
-    fidx = np.array([frame_of[recs[ri]["im_id"]] for ri, _, _, _ in todo], np.int32)
-    W, H = dp_split["im_size"]
-    cov = ev.cover(slots, d_pe, d_pg, T(fidx, torch.int32), T(cam, torch.float64), W, H)
-    out = [pose_error.cus_from_cover(row) for row in cov.cpu().numpy()]
-  elif et in ("mspd", "proj"):
+    fidx = T(np.array([frame_of[recs[ri]["im_id"]] for ri, _, _, _ in todo], np.int32),
+             torch.int32)
+    if et == "cus":
+      W, H = dp_split["im_size"]
+      return ev.cover(slots, d_pe, d_pg, fidx, T(cam, torch.float64), W, H)
+    depths = inout.load_depths(dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id)
+                               for im_id in ims)
+    for k, im_id in enumerate(ims):
+      depths[k] *= scene_camera[im_id]["depth_scale"]  # float32 in place, :242-243
+    dia = np.array([models_info[o]["diameter"] for o in obj], np.float64)
+    delta = p["vsd_deltas"][dataset]
+    from . import runtime
+    return ev.vsd(slots, d_pe, d_pg, fidx, T(np.stack(depths), torch.float32),
+                  T(cam, torch.float64), delta, p["vsd_taus"], T(dia, torch.float64),
+                  normalized_by_diameter=p["vsd_normalized_by_diameter"], cost_type="step",
+                  delta_flags=runtime.delta_flags(delta))
+  if et in ("mspd", "proj"):
     K = np.stack([scene_camera[recs[ri]["im_id"]]["cam_K"].reshape(9) for ri, _, _, _ in todo])
     fn = ev.mspd if et == "mspd" else ev.proj
-    out = fn(slots, d_pe, d_pg, T(K, torch.float64))
-  elif et == "mssd":
-    out = ev.mssd(slots, d_pe, d_pg)
-  elif et in ("ad", "add", "adi"):
+    return fn(slots, d_pe, d_pg, T(K, torch.float64)).view(n, 1)
+  if et == "mssd":
+    return ev.mssd(slots, d_pe, d_pg).view(n, 1)
+  if et in ("ad", "add", "adi"):
     use_adi = np.array([et == "adi" or (et == "ad" and int(o) in symmetric_ids) for o in obj])
     out = torch.empty(n, dtype=torch.float64, device=dev)
     for flag, fn in ((False, ev.add), (True, ev.adi)):
@@ -252,11 +259,59 @@ def evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, mode
       if len(idx):
         ii = T(idx, torch.int64)
         out[ii] = fn(slots[ii], d_pe[ii], d_pg[ii])
-  else:
-    raise ValueError("Unknown pose error function.")
-  vals = out if isinstance(out, list) else out.cpu().numpy().tolist()
-  for (ri, gt_id, _, _), v in zip(todo, vals):
-    errs[ri][gt_id] = v if isinstance(v, list) else [v]
+    return out.view(n, 1)
+  raise ValueError("Unknown pose error function.")
+
+
+def _dist():
+  import torch.distributed as dist
+  if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    return dist.get_rank(), dist.get_world_size()
+  return 0, 1
+
+
+def shard_todo(recs, todo, world, costs=None):
+  """Images of the scene over ranks (LPT on the number of tuples per image, or
+  on `costs` per todo entry); returns one index array into todo per rank."""
+  from . import shard
+  ims = sorted({recs[ri]["im_id"] for ri, _, _, _ in todo})
+  col = {im: k for k, im in enumerate(ims)}
+  frame = np.array([col[recs[ri]["im_id"]] for ri, _, _, _ in todo])
+  w = np.ones(len(todo)) if costs is None else np.asarray(costs, np.float64)
+  parts = shard.lpt_shard(shard.image_costs(frame, w, len(ims)), world)
+  return [np.nonzero(np.isin(frame, part))[0] for part in parts]
+
+
+def evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, models_info,
+             symmetric_ids, batch_fn=None):
+  """errors dict per record. The gated-in tuples of the scene are evaluated as
+  one GPU batch; under torch.distributed (world > 1) the scene's images are
+  split over the ranks (LPT) and the rows gathered to rank 0 (RCCL), which
+  alone returns the errors (None elsewhere)."""
+  et = p["error_type"]
+  errs, todo = plan(p, recs, models_info)
+  rank, world = _dist()
+  if todo:
+    batch_fn = batch_fn or evaluate_batch
+    if world == 1:
+      rows = batch_fn(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
+                      models_info, symmetric_ids, todo)
+    else:
+      from . import shard
+      mine = shard_todo(recs, todo, world)[rank]
+      local = batch_fn(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
+                       models_info, symmetric_ids, [todo[i] for i in mine]) if len(mine) else None
+      width = len(p["vsd_taus"]) if et == "vsd" else (10 if et == "cus" else 1)
+      dev = ev.device if ev is not None else torch.device("cpu")
+      if local is None:
+        local = torch.zeros((0, width), dtype=torch.float64, device=dev)
+      rows = shard.gather_rows(local, torch.as_tensor(mine, dtype=torch.int64, device=dev),
+                               len(todo))
+  if rank != 0:
+    return None
+  if todo:
+    for (ri, gt_id, _, _), row in zip(todo, rows.cpu().numpy()):
+      errs[ri][gt_id] = row_to_errors(et, row)
   return errs
 
 
@@ -310,6 +365,8 @@ def run(p, device=0):
       ests_counter += n_ests
       errs = evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
                       models_info, sym_ids) if recs else []
+      if errs is None:  # another rank writes
+        continue
       scene_errs = [{"im_id": r["im_id"], "obj_id": r["obj_id"], "est_id": r["est_id"],
                      "score": r["score"], "errors": e} for r, e in zip(recs, errs)]
 
@@ -342,7 +399,9 @@ def main(argv=None):
   for k, v in p.items():
     log("- {}: {}".format(k, v))
   log("-----------")
-  run(p, int(os.environ.get("LOCAL_RANK", os.environ.get("BOPX_DEVICE", 0))))
+  from . import shard
+  _, _, local = shard.init_from_env()  # torchrun: scenes' images split over the GPUs
+  run(p, local)
 
 
 if __name__ == "__main__":

@@ -44,13 +44,25 @@ def _depth_path(dp_split, scene_id, im_id):
   return path if os.path.exists(path) else path.replace(".tif", ".png")
 
 
-def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_batch=128):
+def my_images(scene_gt, rank, world):
+  """This rank's image ids of a scene (LPT on the GT count per image)."""
+  from . import shard
+  im_ids = sorted(scene_gt.keys())
+  if world == 1:
+    return im_ids
+  part = shard.lpt_shard([len(scene_gt[i]) + 1 for i in im_ids], world)[rank]
+  return [im_ids[k] for k in part]
+
+
+def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_batch=128,
+                rank=0, world=1):
   """Per image id: list of (row, masks or None) per GT instance, in GT order;
-  images are evaluated in batches of im_batch frames."""
+  images are evaluated in batches of im_batch frames. With world > 1 only this
+  rank's images (my_images) are evaluated."""
   from . import runtime
   scene_camera = inout.load_scene_camera(dp_split["scene_camera_tpath"].format(scene_id=scene_id))
   scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
-  im_ids = sorted(scene_gt.keys())
+  im_ids = my_images(scene_gt, rank, world)
   res = {}
   dev = ev.device
   for i0 in range(0, len(im_ids), im_batch):
@@ -88,7 +100,8 @@ def _setup(p):
                                              p["dataset_split"], p["dataset_split_type"])
   dp_model = dataset_params.get_model_params(p["datasets_path"], p["dataset"],
                                              "cad" if p["dataset"] == "tless" else None)
-  ev = BatchEvaluator(p.get("device", 0))
+  import os as _os
+  ev = BatchEvaluator(int(_os.environ.get("LOCAL_RANK", p.get("device", 0))))
   misc.log("Initializing renderer...")
   for obj_id in dp_model["obj_ids"]:
     path = dp_model["model_tpath"].format(obj_id=obj_id)
@@ -99,15 +112,47 @@ def _setup(p):
   return torch, ev, dp_split, scene_ids
 
 
+def _gather_info(torch, ev, stats, scene_gt, rank, world):
+  """{im_id: [row]} of the whole scene on rank 0 (RCCL gather of the rows)."""
+  if world == 1:
+    return {im: [r for r, _ in lst] for im, lst in stats.items()}
+  from . import shard
+  ims = sorted(scene_gt.keys())
+  first = np.cumsum([0] + [len(scene_gt[i]) for i in ims])
+  pos = {im: int(first[k]) for k, im in enumerate(ims)}
+  ids, rows = [], []
+  for im, lst in stats.items():
+    for g, (r, _) in enumerate(lst):
+      ids.append(pos[im] + g)
+      rows.append(r)
+  dev = ev.device
+  table = shard.gather_rows(
+      torch.as_tensor(np.array(rows, np.float64).reshape(-1, 11), device=dev),
+      torch.as_tensor(np.array(ids, np.int64), device=dev), int(first[-1]))
+  if rank != 0:
+    return None
+  table = table.cpu().numpy()
+  return {im: [table[pos[im] + g] for g in range(len(scene_gt[im]))] for im in ims}
+
+
 def calc_gt_info(p):
-  """scene_gt_info.json of every scene (calc_gt_info.py:75-175); returns paths."""
+  """scene_gt_info.json of every scene (calc_gt_info.py:75-175); returns paths.
+  Under torchrun the images of each scene are split over the GPUs and rank 0
+  writes the file."""
+  from . import shard
+  rank, world, _ = shard.init_from_env()
   torch, ev, dp_split, scene_ids = _setup(p)
   written = []
   for scene_id in scene_ids:
     misc.log("Calculating GT info - dataset: {} ({}, {}), scene: {}".format(
         p["dataset"], p["dataset_split"], p["dataset_split_type"], scene_id))
-    stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 3, False)
-    info = {im_id: [info_from_row(r) for r, _ in lst] for im_id, lst in stats.items()}
+    stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 3, False, rank=rank,
+                        world=world)
+    scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+    rows = _gather_info(torch, ev, stats, scene_gt, rank, world)
+    if rows is None:
+      continue
+    info = {im_id: [info_from_row(r) for r in lst] for im_id, lst in rows.items()}
     path = dp_split["scene_gt_info_tpath"].format(scene_id=scene_id)
     os.makedirs(os.path.dirname(path), exist_ok=True)
     inout.save_json(path, info)
@@ -116,8 +161,11 @@ def calc_gt_info(p):
 
 
 def calc_gt_masks(p):
-  """mask / mask_visib PNGs of every GT instance (calc_gt_masks.py:58-125)."""
+  """mask / mask_visib PNGs of every GT instance (calc_gt_masks.py:58-125).
+  Under torchrun every rank writes the masks of its own images."""
   from PIL import Image
+  from . import shard
+  rank, world, _ = shard.init_from_env()
   torch, ev, dp_split, scene_ids = _setup(p)
   written = []
   for scene_id in scene_ids:
@@ -126,7 +174,8 @@ def calc_gt_masks(p):
       continue
     misc.log("Calculating masks - dataset: {} ({}, {}), scene: {}".format(
         p["dataset"], p["dataset_split"], p["dataset_split_type"], scene_id))
-    stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 1, True)
+    stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 1, True, rank=rank,
+                        world=world)
     for im_id, lst in stats.items():
       for gt_id, (_, mk) in enumerate(lst):
         for plane, key in enumerate(("mask_tpath", "mask_visib_tpath")):

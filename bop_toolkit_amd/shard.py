@@ -84,3 +84,19 @@ def gather_rows(rows, ids, n_total, group=None):
   if not bool(filled.all()):
     raise RuntimeError("gather_rows: %d tuple rows missing" % int((~filled).sum()))
   return table
+
+
+def init_from_env():
+  """One process per GPU under torchrun (RANK / WORLD_SIZE / LOCAL_RANK):
+  bind the local GPU and join the RCCL group. Returns (rank, world, local)."""
+  import os
+  world = int(os.environ.get("WORLD_SIZE", 1))
+  local = int(os.environ.get("LOCAL_RANK", os.environ.get("BOPX_DEVICE", 0)))
+  if world <= 1:
+    return 0, 1, local
+  import torch
+  import torch.distributed as dist
+  torch.cuda.set_device(local)
+  if not dist.is_initialized():
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+  return dist.get_rank(), world, local

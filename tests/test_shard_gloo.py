@@ -67,3 +67,55 @@ def test_gather_bitwise_equals_single(tmp_path, world):
   table = np.load(out)
   full = np.sin(np.arange(n_img * 6)[:, None] * np.arange(1, 13)[None, :])
   assert np.array_equal(table, full)
+
+
+def _stub_rows(ev, torch_, p, dataset, dp_split, scene_camera, scene_id, recs, models_info,
+               sym_ids, todo):
+  """Stand-in for the GPU batch: a deterministic function of (record, gt)."""
+  width = len(p["vsd_taus"])
+  return torch.tensor([[ri * 1000.0 + gt_id + 0.1 * k for k in range(width)]
+                       for ri, gt_id, _, _ in todo], dtype=torch.float64)
+
+
+def _caller_errs(world_rank=None):
+  from bop_toolkit_amd import dataset_params, eval_calc_errors as ece, inout
+  e2e = os.path.join(os.path.dirname(__file__), "golden", "e2e")
+  p = ece.parse_args(["--error_type", "vsd", "--n_top", "-1", "--result_filenames",
+                      "synth_lmo-test.csv", "--results_path", os.path.join(e2e, "results"),
+                      "--datasets_path", os.path.join(e2e, "datasets")])
+  dp_split = dataset_params.get_split_params(p["datasets_path"], "lmo", "test")
+  dp_model = dataset_params.get_model_params(p["datasets_path"], "lmo", "eval")
+  targets = inout.load_json(os.path.join(dp_split["base_path"], p["targets_filename"]))
+  ests = inout.load_bop_results(os.path.join(p["results_path"], "synth_lmo-test.csv"))
+  t_org, e_org = ece.organize(targets, ests)
+  info = inout.load_json(dp_model["models_info_path"], keys_to_int=True)
+  scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=2))
+  recs, _ = ece.scene_records(p, 2, t_org[2], e_org, scene_gt)
+  return ece.evaluate(None, torch, p, "lmo", dp_split, None, 2, recs, info, set(),
+                      batch_fn=_stub_rows)
+
+
+def _caller_worker(rank, world, port, out_path):
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  errs = _caller_errs()
+  if rank == 0:
+    import json
+    with open(out_path, "w") as f:
+      json.dump([{str(k): v for k, v in e.items()} for e in errs], f)
+  else:
+    assert errs is None
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+def test_caller_sharded_equals_single(tmp_path):
+  """eval_calc_errors.evaluate under gloo world 2 (images of the scene split
+  by LPT, rows gathered to rank 0) == the single-process result."""
+  import json
+  out = str(tmp_path / "errs.json")
+  mp.spawn(_caller_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+  single = [{str(k): v for k, v in e.items()} for e in _caller_errs()]
+  assert json.load(open(out)) == single
+  assert sum(v[0] != 1.0 and v[0] < 1e6 for e in single for v in e.values()) > 10
