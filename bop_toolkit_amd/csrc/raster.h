@@ -233,32 +233,7 @@ __device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int 
            ((uint32_t)pose << 18) | ((uint32_t)first << 19);
 }
 
-// Walk row j of a record: plot(pose, tile col, tile row, q) per fragment.
-template <class Plot>
-__device__ __forceinline__ void r_walk_row(const RRow& r, int j, Plot plot) {
-  const int tc0 = r.meta & 63u, tr = (int)((r.meta >> 6) & 63u) + j;
-  const int w = (int)((r.meta >> 12) & 63u) + 1, pose = (r.meta >> 18) & 1u;
-  uint32_t e[3], sx[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int32_t dU = (int32_t)(r.duv[k] << 16) >> 16, dV = (int32_t)r.duv[k] >> 16;
-    e[k] = r.er[k] + (uint32_t)__mul24(256 * dU, j);  // |256 dU| < 2^23, j < 64
-    sx[k] = (uint32_t)(-256 * dV);
-  }
-  const float qy = r.gb * (float)(r.py0v + 256 * j);
-  float fdx = (float)r.px0u;  // integers below 2^24: += 256 is exact
-  for (int i = 0; i < w; ++i, fdx += 256.0f) {
-    if (((int32_t)e[0] > 0) & ((int32_t)e[1] > 0) & ((int32_t)e[2] > 0)) {
-      const float q = (r.iz0 + r.ga * fdx) + qy;
-      if (q > 0.0f) plot(pose, tc0 + i, tr, q);
-    }
-    e[0] += sx[0];
-    e[1] += sx[1];
-    e[2] += sx[2];
-  }
-}
-
-// Branch-free variant for the LDS z-buffer: every column of the row issues one
+// Walk row j of a record into the LDS z-buffer, branch-free: every column issues one
 // atomicMax, with 0 (a no-op on the 0-initialised buffer) where the pixel
 // centre is outside the triangle or q <= 0 / NaN. No exec-mask branches in the
 // loop body: the edge tests, the q plane and the LDS op form straight-line code.

@@ -372,3 +372,11 @@ def test_drop_in_cus_cou_bb_proj(oracle_mod):
     for r in (ren, Foreign()):
       assert pose_error.cus(Re[i], te_[i], Rg[i], tg[i], K, r, 6) == cus_ref
       assert pose_error.cou_bb_proj(Re[i], te_[i], Rg[i], tg[i], K, r, 6) == cou_ref
+
+
+def test_fused_vsd_bit_exact_large_meshes(oracle_mod):
+  """Objects with > 256 and > 512 meshlets: the launch sizes the per-thread
+  meshlet-rectangle registers to 2 and 4 (RPT), both paths bit-exact."""
+  from bop_toolkit_amd import synth
+  _fused_vs_oracle(oracle_mod, 15, 6, 640, 480, synth.YCBV_K, 100, 150)  # 30k tris: RPT 2
+  _fused_vs_oracle(oracle_mod, 16, 6, 640, 480, synth.LMO_K, 150, 200)   # 60k tris: RPT 4
