@@ -5,24 +5,31 @@
 //   images (misc.py:143-163) -> 2 visibility masks (visibility.py:9-75) ->
 //   inter/union counts -> per-tau step (or truncated-linear) cost.
 //
-// Here ONE launch evaluates a whole batch: one 256-thread workgroup per tuple.
-//  1. The object's meshlets (64 triangles each) are culled per pose: the 8
-//     corners of each meshlet AABB are projected (float32, same arithmetic as
-//     the vertices) into a conservative pixel rectangle kept in LDS. Their
-//     union is the tuple's region of interest (ROI): pixels outside both
+// Here ONE launch evaluates a whole batch: one 512-thread workgroup (8 waves)
+// per tuple, two workgroups per CU.
+//  1. The object's meshlets (<= 64 triangles / 64 vertices each) are culled per
+//     pose: the 8 corners of each meshlet AABB are projected (float32, the
+//     vertex arithmetic) into a conservative pixel rectangle kept in registers.
+//     Their union is the tuple's region of interest (ROI): pixels outside both
 //     silhouettes cannot change VSD (masks need d_model > 0, visibility.py:37).
 //  2. The ROI is swept in 64x64 screen tiles. Per tile, both q-buffers
-//     (est, gt; q = 1/Z, 0 = empty) live in LDS (2 x 16 KiB); the meshlets
-//     whose rectangle touches the tile are listed, and each wave rasterises one
-//     meshlet per step (lane = triangle) with exact integer edge functions and
-//     an LDS atomicMax on the float bits (order-independent z-buffer, raster.h).
-//  3. The tile's pixels are then evaluated in place: test depth is read from
-//     HBM (coalesced rows), the three float64 distances and the float32
-//     visibility tests follow the reference operation order exactly
-//     (-ffp-contract=off), and integer counters (union, inter, per-tau) stay
-//     in registers. Pixels covered by neither pose are skipped.
-//  4. Counters are reduced across the workgroup; one thread writes
-//     e_k = (cnt_k + comp) / union (1.0 when union == 0).
+//     (est, gt; q = 1/Z, 0 = empty) live in LDS; the (pose, meshlet) entries
+//     whose rectangle touches the tile are listed and pulled by the waves in
+//     groups of two (dynamic balance). Per group: vertex blocks transformed
+//     once into LDS (lane = vertex), bbox test + ballot compaction of the
+//     triangles that touch the tile, set-up on full waves (lane = triangle),
+//     then (triangle, row) items dealt out one per lane and walked with exact
+//     integer edge functions and an LDS atomicMax on the float bits
+//     (order-independent z-buffer, raster.h).
+//  3. Each wave compacts the tile's covered pixels of its rows into a list and
+//     evaluates it with full lanes: test depth from HBM, the three float64
+//     distances and the float32 visibility tests in the reference operation
+//     order (-ffp-contract=off), integer counters (union, inter, per-tau) in
+//     registers.
+//  4. Counters are reduced across the workgroup in a fixed order; one thread
+//     writes e_k = (cnt_k + comp) / union (1.0 when union == 0).
+// The same kernel has a silhouette mode (cus / cou_bb_proj) and a GT-info mode
+// (calc_gt_info / calc_gt_masks) that reuse steps 1-2 and replace step 3.
 // Results are bit-identical to the reference given identical depth maps.
 #include <algorithm>
 

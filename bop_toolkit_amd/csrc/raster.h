@@ -2,12 +2,13 @@
 //
 // Replaces the OpenGL depth pass of renderer_vispy.py:433-538 /
 // renderer_py.py:422-555 (eye-Z depth, pixel-centre sampling, no culling,
-// GL_LESS z-test, background 0). The arithmetic follows raster spec v2 of
+// GL_LESS z-test, background 0). The arithmetic follows raster spec v4 of
 // DESIGN.md §4 exactly, so results are bit-identical to the CPU twin
 // (oracle/bopx_oracle.c: oracle_render_depth) whatever the tiling, culling or
 // triangle order:
 //   * vertex: float32, no FMA contraction (built with -ffp-contract=off),
-//     snapped to 1/256 px with round-half-even (v_rndne_f32), iz = 1/Z;
+//     iz = 1/Z (one IEEE division), u = (fx X) iz + cx, snapped to 1/256 px
+//     with round-half-even (v_rndne_f32);
 //   * exact integer edge functions with the top-left fill rule (watertight:
 //     a pixel centre on a shared edge belongs to exactly one triangle).
 //     Triangles whose fixed-point extent is < 2^15 (128 px) step their edge
