@@ -80,7 +80,10 @@ def make_dataset(rng, root):
   for im in range(N_IM):
     objs = list(rng.choice(OBJ_IDS, 5, replace=False))
     objs.append(objs[0])  # two instances of one object
-    Rg, tg = synth.gt_poses(rng, len(objs), z_range=(600.0, 1100.0), xy=(120.0, 90.0))
+    # image 3: objects near and across the image border (truncated silhouettes:
+    # calc_gt_info's enlarged canvas, clipped ROIs)
+    xy = (420.0, 320.0) if im == 3 else (120.0, 90.0)
+    Rg, tg = synth.gt_poses(rng, len(objs), z_range=(600.0, 1100.0), xy=xy)
     depth = np.zeros((H, W), np.float32)
     inst, renders = [], []
     for j, o in enumerate(objs):
