@@ -35,20 +35,49 @@ FP64_PEAK_TF = 78.6
 FP32_PEAK_TF = 157.3
 
 
+# BASELINE.json configs (index): per-GPU shard of the workload each names.
+# Default: configs[3], the metric's configuration (BOP19 set, 100k est / 8 GPUs).
+CONFIGS = {
+    1: {"objects": 8, "n_lat": 50, "n_lon": 100, "syms": [1, 2, 4, 8], "continuous": False,
+        "tuples": 10000, "K": "LMO_K", "W": 640, "H": 480, "errors": ("mssd", "mspd"),
+        "what": "configs[1]: MSSD+MSPD, 8 LM-O-like objs, S<=8, 10k est/GPU"},
+    2: {"objects": 21, "n_lat": 50, "n_lon": 100, "syms": [1, 2, 4, 8], "continuous": True,
+        "tuples": 50000, "K": "YCBV_K", "W": 640, "H": 480, "errors": ("vsd",),
+        "what": "configs[2]: VSD (10 taus) with HIP raster, 21 YCB-V-like objs, 50k est/GPU"},
+    3: {"objects": 21, "n_lat": 50, "n_lon": 100, "syms": [1, 2, 4, 8], "continuous": True,
+        "tuples": 12500, "K": "YCBV_K", "W": 640, "H": 480, "errors": ("vsd", "mssd", "mspd"),
+        "what": "BASELINE configs[3] per-GPU shard: BOP19 error set (VSD 10 taus + MSSD + MSPD)"},
+    4: {"objects": 30, "n_lat": 100, "n_lon": 150, "syms": [1, 2, 4, 8, 16, 32, 64],
+        "continuous": False, "tuples": 25000, "K": "TLESS_K", "W": 720, "H": 540,
+        "errors": ("vsd", "mssd", "mspd"),
+        "what": "configs[4] per-GPU shard: T-LESS-like BOP19 set, ~15k verts, S<=64"},
+}
+
+
 def parse():
   ap = argparse.ArgumentParser()
   ap.add_argument("--gpus", type=int, default=1)
   ap.add_argument("--steps", type=int, default=10)
   ap.add_argument("--warmup", type=int, default=2)
-  ap.add_argument("--tuples", type=int, default=12500, help="tuples per GPU")
-  ap.add_argument("--objects", type=int, default=21)
-  ap.add_argument("--n-lat", type=int, default=50)
-  ap.add_argument("--n-lon", type=int, default=100)
+  ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS),
+                  help="BASELINE.json configs index (3 = the metric's workload)")
+  ap.add_argument("--tuples", type=int, default=None, help="tuples per GPU")
+  ap.add_argument("--objects", type=int, default=None)
+  ap.add_argument("--n-lat", type=int, default=None)
+  ap.add_argument("--n-lon", type=int, default=None)
   ap.add_argument("--cpu-seconds", type=float, default=10.0,
                   help="target wall time of the CPU-baseline sample")
   ap.add_argument("--no-cpu-baseline", action="store_true")
   ap.add_argument("--seed", type=int, default=20250220 + 4)
-  return ap.parse_args()
+  args = ap.parse_args()
+  cfg = CONFIGS[args.config]
+  for k in ("tuples", "objects", "n_lat", "n_lon"):
+    if getattr(args, k) is None:
+      setattr(args, k, cfg[k])
+  global W, H
+  W, H = cfg["W"], cfg["H"]
+  args.cfg = cfg
+  return args
 
 
 def build_objects(ev, args, torch):
@@ -61,10 +90,11 @@ def build_objects(ev, args, torch):
     p = torch.as_tensor(pts, device=ev.device)
     dia = float(torch.cdist(p, p, compute_mode="donot_use_mm_for_euclid_dist").max())
     info = {"diameter": dia}
-    if o == args.objects - 1:
+    if o == args.objects - 1 and args.cfg["continuous"]:
       info["symmetries_continuous"] = [{"axis": [0, 0, 1], "offset": [0, 0, 0]}]
     else:
-      n_disc = [1, 2, 4, 8][o % 4]
+      pat = args.cfg["syms"]
+      n_disc = pat[o % len(pat)]
       info["symmetries_discrete"] = [
           np.concatenate([np.concatenate([synth.rot_z(2 * np.pi * j / n_disc), np.zeros((3, 1))],
                                          1), [[0, 0, 0, 1]]]).reshape(-1).tolist()
@@ -91,7 +121,7 @@ def build_workload(ev, objs, args, rank, torch):
   pe = np.concatenate([Re.reshape(n, 9), te], 1)
   pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
   frame_idx = np.repeat(np.arange(n_img, dtype=np.int32), per_img)
-  K = synth.YCBV_K
+  K = getattr(synth, args.cfg["K"])
   cam = np.tile([K[0, 0], K[1, 1], K[0, 2], K[1, 2]], (n_img, 1)).astype(np.float64)
   dev = ev.device
   t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
@@ -152,11 +182,10 @@ def roi_pixels(objs, obj, poses, K):
   return area
 
 
-def algorithmic_cost(objs, host, n):
+def algorithmic_cost(objs, host, n, K):
   """Compulsory HBM bytes and VALU flops per launch (SURVEY.md §8d formulas)."""
-  from bop_toolkit_amd import synth
   obj = host["obj"]
-  roi = roi_pixels(objs, obj, [host["pe"], host["pg"]], synth.YCBV_K)
+  roi = roi_pixels(objs, obj, [host["pe"], host["pg"]], K)
   used = np.unique(obj)
   V = np.array([len(objs[o]["pts"]) for o in obj], np.float64)
   F = np.array([len(objs[o]["faces"]) for o in obj], np.float64)
@@ -239,20 +268,22 @@ def main():
   out_mspd = torch.empty(n, dtype=torch.float64, device=ev.device)
   rows = torch.empty((n, N_TAU + 2), dtype=torch.float64, device=ev.device)
   gids = torch.arange(rank * n, (rank + 1) * n, dtype=torch.int64, device=ev.device)
-  ktime = {"vsd": 0.0, "mssd": 0.0, "mspd": 0.0}
+  ktime = {k: 0.0 for k in args.cfg["errors"]}
   marks = []  # per timed step: HIP events bracketing each kernel on the launch stream
 
   def step(timed):
     e = {k: [torch.cuda.Event(enable_timing=True) for _ in range(2)] for k in ktime} \
         if timed else None
-    if e: e["vsd"][0].record()
-    ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"], d["frames"], d["cam"], DELTA,
-           TAUS, d["diameters"], out=out_vsd)
-    if e: e["vsd"][1].record(); e["mssd"][0].record()
-    ev.mssd(d["slots"], d["pose_est"], d["pose_gt"], out=out_mssd)
-    if e: e["mssd"][1].record(); e["mspd"][0].record()
-    ev.mspd(d["slots"], d["pose_est"], d["pose_gt"], d["K"], out=out_mspd)
-    if e: e["mspd"][1].record(); marks.append(e)
+    run = {
+        "vsd": lambda: ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"],
+                              d["frames"], d["cam"], DELTA, TAUS, d["diameters"], out=out_vsd),
+        "mssd": lambda: ev.mssd(d["slots"], d["pose_est"], d["pose_gt"], out=out_mssd),
+        "mspd": lambda: ev.mspd(d["slots"], d["pose_est"], d["pose_gt"], d["K"], out=out_mspd)}
+    for k in ktime:
+      if e: e[k][0].record()
+      run[k]()
+      if e: e[k][1].record()
+    if e: marks.append(e)
     if world > 1:
       rows[:, :N_TAU] = out_vsd
       rows[:, N_TAU] = out_mssd
@@ -285,12 +316,13 @@ def main():
   if rank == 0:
     steps = args.steps
     total = n * world * steps
-    cost = algorithmic_cost(objs, d["host"], n)
+    from bop_toolkit_amd import synth
+    cost = algorithmic_cost(objs, d["host"], n, getattr(synth, args.cfg["K"]))
     kt = {k: v / steps for k, v in ktime.items()}
     roof = None
     kernels = {}
     if kt:
-      for k in ("vsd", "mssd", "mspd"):
+      for k in kt:
         b, f32, f64 = cost[k]
         t_valu = f64 / (FP64_PEAK_TF * 1e12) + f32 / (FP32_PEAK_TF * 1e12)
         kernels[k] = {"ms": kt[k] * 1e3, "alg_GBps": b / kt[k] / 1e9,
@@ -299,7 +331,7 @@ def main():
       b, f32, f64 = cost[dom]
       ach = b / kt[dom] / 1e9
       t_valu = f64 / (FP64_PEAK_TF * 1e12) + f32 / (FP32_PEAK_TF * 1e12)
-      traffic = load_traffic() if dom == "vsd" else None
+      traffic = load_traffic() if dom == "vsd" and args.config == 3 else None
       roof = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
               "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": traffic,
               "kernel": "k_vsd" if dom == "vsd" else "k_sym_error<%s>" % dom.upper(),
@@ -307,18 +339,21 @@ def main():
                           "note": "VALU-bound by SURVEY.md §8d flop/byte; fp64 %.1f TF + "
                                   "fp32 %.1f TF peaks" % (FP64_PEAK_TF, FP32_PEAK_TF)}}
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and len(args.cfg["errors"]) == 3:
       cpu = cpu_baseline(objs, d, n, args.cpu_seconds)
     line = {
-        "metric": "pose-error tuples/sec (VSD+MSSD+MSPD) at 640x480, ~5k-vert meshes",
+        "metric": "pose-error tuples/sec (%s) at %dx%d, ~%dk-vert meshes" % (
+            "+".join(e.upper() for e in args.cfg["errors"]), W, H,
+            round(len(objs[0]["pts"]) / 1000)),
         "value": total / elapsed, "unit": "tuples/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": elapsed / steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64+f32", "data": "synthetic",
-        "config": {"workload": "BASELINE configs[3] per-GPU shard: BOP19 error set (VSD 10 taus "
-                               "+ MSSD + MSPD), %d objs V=%d F=%d S in {1,2,4,8,314}, "
-                               "%dx%d YCB-V K, %d tuples/GPU" % (
-                                   args.objects, len(objs[0]["pts"]), len(objs[0]["faces"]), W,
-                                   H, n),
+        "config": {"workload": "%s, %d objs V=%d F=%d S in {%s}, %dx%d %s, %d tuples/GPU" % (
+                                   args.cfg["what"], args.objects, len(objs[0]["pts"]),
+                                   len(objs[0]["faces"]),
+                                   ",".join(map(str, sorted(set(
+                                       len(o["syms"]) for o in objs)))), W, H,
+                                   args.cfg["K"].split("_")[0], n),
                    "global_batch": n * world, "parallelism": "image-sharded x%d" % world,
                    "roi_mean_px": round(cost["roi_mean"], 1)},
         "roofline": roof, "kernels": kernels, "cpu_baseline": cpu}
