@@ -65,11 +65,29 @@ __device__ unsigned long long g_vsd_time[16];
     }                                                             \
   } while (0)
 
+// Correctly rounded float64 sqrt for s = 0 or s >= 2^-767 (finite): the
+// rsq + Goldschmidt sequence of the device library's sqrt, without its input
+// scaling (taken only below 2^-767) and inf/zero class fix-ups. Arguments here
+// come from float32 depths: s = (pX d)^2 + (pY d)^2 + d^2 >= d^2 >= 2^-298 when
+// d != 0, so the result is bit-identical to sqrt(s).
+__device__ __forceinline__ double sqrt_depth(double s) {
+  const double y = __builtin_amdgcn_rsq(s);
+  double g = s * y, h = y * 0.5;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, s);
+  g = fma(d, h, g);
+  d = fma(-g, g, s);
+  g = fma(d, h, g);
+  return s > 0.0 ? g : s;
+}
+
 // float64 distance of a float32 depth at pixel (pX, pY) (misc.py:158-161).
 __device__ __forceinline__ double dist_of(double pX, double pY, float depth) {
   const double d = (double)depth;
   const double a = pX * d, b = pY * d;
-  return sqrt((a * a + b * b) + d * d);
+  return sqrt_depth((a * a + b * b) + d * d);
 }
 
 // visibility._estimate_visib_mask, bop19 (visibility.py:34-37).
