@@ -6,8 +6,8 @@
 //   vtx   : float32x4    (x, y, z, 0) per vertex     (rasteriser, GL-like fp32)
 //   faces : uint32 x3 per triangle, re-ordered into meshlets of 64 triangles
 //           sorted by the Morton code of the triangle centroid
-//   mlet  : float32 x8 per meshlet: min xyz, 0, max xyz, 0 (object-space AABB
-//           of the meshlet's float32 vertices; used for conservative culling)
+//   mlet  : float32 x24 per meshlet: the 8 corners (xyz) of an oriented
+//           bounding box of the meshlet's float32 vertices (conservative culling)
 //   syms  : float64 x12 per symmetry [R row-major | t]
 #pragma once
 #include <hip/hip_runtime.h>
@@ -48,7 +48,7 @@ struct ObjDesc {
   const double* pts;         // 3*nv, SoA
   const float4* vtx;         // nv
   const uint32_t* faces;     // 3*nf (meshlet order)
-  const float* mlet;         // 8*nm: object-space AABB per meshlet
+  const float* mlet;         // 24*nm: object-space OBB corners per meshlet
   const int4* mlet_info;     // nm: {first triangle, #triangles, first vertex slot, #vertices}
   const float4* mlet_vtx;    // nm x 64: meshlet-local vertex blocks, fixed stride
                              // (vertices shared by neighbouring meshlets are duplicated)

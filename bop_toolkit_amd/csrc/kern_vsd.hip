@@ -98,17 +98,16 @@ __device__ __forceinline__ bool visib19(double dt, double dm, float delta32, int
   return (le || dt == 0.0) && dm > 0.0;
 }
 
-// Conservative pixel rectangle of one meshlet AABB under a pose. Any corner with
-// Z <= 0 (or a non-finite projection) gives the whole image.
+// Conservative pixel rectangle of one meshlet bounding box (8 object-space
+// corners, runtime.cpp obb_corners) under a pose. Any corner with Z <= 0 (or a
+// non-finite projection) gives the whole image.
 __device__ __forceinline__ short4 meshlet_rect(gptr<const float> mb, const float* Rf,
                                                const Cam32& c, int W, int H) {
   float umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
   bool full = false;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const float x = (k & 1) ? mb[4] : mb[0];
-    const float y = (k & 2) ? mb[5] : mb[1];
-    const float z = (k & 4) ? mb[6] : mb[2];
+    const float x = mb[3 * k], y = mb[3 * k + 1], z = mb[3 * k + 2];
     const float X = ((Rf[0] * x + Rf[1] * y) + Rf[2] * z) + Rf[9];
     const float Y = ((Rf[3] * x + Rf[4] * y) + Rf[5] * z) + Rf[10];
     const float Z = ((Rf[6] * x + Rf[7] * y) + Rf[8] * z) + Rf[11];
@@ -229,7 +228,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
     rect[j] = make_short4(1, 1, 0, 0);
     if (i < 2 * nm && !(COST == kCostGtInfo && i < nm)) {  // GT-info: gt pose only
       const int r = i >= nm, m = i - r * nm;
-      rect[j] = meshlet_rect(g_mlet + 8 * (int64_t)m, s_pose[r], c32, W, H);
+      rect[j] = meshlet_rect(g_mlet + 24 * (int64_t)m, s_pose[r], c32, W, H);
       if (rect[j].x <= rect[j].z && rect[j].y <= rect[j].w) {
         atomicMin(&s_roi[0], (int)rect[j].x);
         atomicMin(&s_roi[1], (int)rect[j].y);

@@ -288,6 +288,80 @@ int bopx_synchronize(bopx_ctx* c) {
 
 void* bopx_stream(bopx_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+// Oriented bounding box of a meshlet's vertices (principal axes of their
+// covariance, Jacobi rotations), appended as 8 float32 corners (x, y, z each).
+// A surface patch is thin along its normal, so its projected OBB is much
+// tighter than that of an object-space AABB: fewer (meshlet, tile) entries in
+// k_vsd. The box is inflated by 1e-4 of its extent (+1e-3) so float32 rounding
+// of the corners cannot make it non-conservative.
+static void jacobi3(double a[3][3], double v[3][3]) {
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) v[i][j] = i == j;
+  for (int sweep = 0; sweep < 32; ++sweep) {
+    const double off = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
+    if (off < 1e-30) break;
+    for (int p = 0; p < 2; ++p)
+      for (int q = p + 1; q < 3; ++q) {
+        if (std::fabs(a[p][q]) < 1e-300) continue;
+        const double th = (a[q][q] - a[p][p]) / (2.0 * a[p][q]);
+        const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1.0));
+        const double c = 1.0 / std::sqrt(t * t + 1.0), sn = t * c;
+        for (int k = 0; k < 3; ++k) {  // A <- A J
+          const double akp = a[k][p], akq = a[k][q];
+          a[k][p] = c * akp - sn * akq;
+          a[k][q] = sn * akp + c * akq;
+        }
+        for (int k = 0; k < 3; ++k) {  // A <- J^T A
+          const double apk = a[p][k], aqk = a[q][k];
+          a[p][k] = c * apk - sn * aqk;
+          a[q][k] = sn * apk + c * aqk;
+        }
+        for (int k = 0; k < 3; ++k) {  // V <- V J
+          const double vkp = v[k][p], vkq = v[k][q];
+          v[k][p] = c * vkp - sn * vkq;
+          v[k][q] = sn * vkp + c * vkq;
+        }
+      }
+  }
+}
+
+static void obb_corners(const std::vector<float4>& vtx, const std::vector<uint32_t>& ids,
+                        std::vector<float>& out) {
+  const size_t n = ids.size();
+  double mean[3] = {0, 0, 0};
+  for (uint32_t v : ids) {
+    mean[0] += vtx[v].x;
+    mean[1] += vtx[v].y;
+    mean[2] += vtx[v].z;
+  }
+  for (int k = 0; k < 3; ++k) mean[k] /= (double)std::max<size_t>(n, 1);
+  double cov[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, ax[3][3];
+  for (uint32_t v : ids) {
+    const double d[3] = {vtx[v].x - mean[0], vtx[v].y - mean[1], vtx[v].z - mean[2]};
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) cov[i][j] += d[i] * d[j];
+  }
+  jacobi3(cov, ax);  // columns of ax: orthonormal principal axes
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (uint32_t v : ids) {
+    const double d[3] = {vtx[v].x - mean[0], vtx[v].y - mean[1], vtx[v].z - mean[2]};
+    for (int k = 0; k < 3; ++k) {
+      const double t = d[0] * ax[0][k] + d[1] * ax[1][k] + d[2] * ax[2][k];
+      lo[k] = std::min(lo[k], t);
+      hi[k] = std::max(hi[k], t);
+    }
+  }
+  double ext = 0;
+  for (int k = 0; k < 3; ++k) ext = std::max(ext, hi[k] - lo[k]);
+  const double pad = 1e-4 * ext + 1e-3;
+  for (int k = 0; k < 3; ++k) lo[k] -= pad, hi[k] += pad;
+  for (int c = 0; c < 8; ++c) {
+    const double t[3] = {(c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2]};
+    for (int i = 0; i < 3; ++i)
+      out.push_back((float)(mean[i] + t[0] * ax[i][0] + t[1] * ax[i][1] + t[2] * ax[i][2]));
+  }
+}
+
 int bopx_add_object(bopx_ctx* c, int obj_id, const double* pts, int64_t nv,
                     const uint32_t* faces, int64_t nf) {
   if (!c) return BOPX_E_INVALID;
@@ -354,7 +428,6 @@ int bopx_add_object(bopx_ctx* c, int obj_id, const double* pts, int64_t nv,
       const int32_t tri0 = (int32_t)f, vtx0 = (int32_t)mvtx.size();
       const size_t tslot0 = mtri.size();
       touched.clear();
-      float bl[3] = {INFINITY, INFINITY, INFINITY}, bh[3] = {-INFINITY, -INFINITY, -INFINITY};
       while (f < nf && f - tri0 < bopx::kMeshletTris) {
         int fresh = 0;
         for (int j = 0; j < 3; ++j) fresh += local[fsorted[3 * f + j]] < 0;
@@ -368,21 +441,16 @@ int bopx_add_object(bopx_ctx* c, int obj_id, const double* pts, int64_t nv,
             mvtx.push_back(vtx[v]);
           }
           pk |= (uint32_t)local[v] << (8 * j);
-          const float* p = &vtx[v].x;
-          for (int k = 0; k < 3; ++k) bl[k] = std::min(bl[k], p[k]), bh[k] = std::max(bh[k], p[k]);
         }
         mtri.push_back(pk);
         ++f;
       }
+      obb_corners(vtx, touched, mlet);
       for (uint32_t v : touched) local[v] = -1;
       const float4 pad = mvtx[vtx0];
       while (mvtx.size() - vtx0 < (size_t)bopx::kMeshletVerts) mvtx.push_back(pad);
       while (mtri.size() - tslot0 < (size_t)bopx::kMeshletTris) mtri.push_back(0xFFFFFFFFu);
       minfo.push_back(make_int4(tri0, (int32_t)(f - tri0), vtx0, (int32_t)touched.size()));
-      for (int k = 0; k < 3; ++k) mlet.push_back(bl[k]);
-      mlet.push_back(0.f);
-      for (int k = 0; k < 3; ++k) mlet.push_back(bh[k]);
-      mlet.push_back(0.f);
     }
     o.nm = (int64_t)minfo.size();
   }
