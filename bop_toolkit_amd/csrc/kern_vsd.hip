@@ -124,9 +124,12 @@ __device__ __forceinline__ short4 meshlet_rect(gptr<const float> mb, const float
   }
   if (full || !(umin == umin) || !(vmin == vmin) || !(umax == umax) || !(vmax == vmax))
     return make_short4(0, 0, (short)(W - 1), (short)(H - 1));
-  // pixel col is sampled at col + 0.5; one pixel of margin for rounding.
-  const float fx0 = floorf(umin - 0.5f) - 1.0f, fx1 = ceilf(umax - 0.5f) + 1.0f;
-  const float fy0 = floorf(vmin - 0.5f) - 1.0f, fy1 = ceilf(vmax - 0.5f) + 1.0f;
+  // Column c is sampled at c + 0.5 and covered only if that centre is inside a
+  // triangle, i.e. within [min, max] of the snapped vertex u (snap error
+  // 1/512 px). The corners bound the vertices exactly; their float32
+  // projection and the vertices' differ by ~1e-3 px at most: 1/16 px of slack.
+  const float fx0 = ceilf(umin - 0.5f - 0.0625f), fx1 = floorf(umax - 0.5f + 0.0625f);
+  const float fy0 = ceilf(vmin - 0.5f - 0.0625f), fy1 = floorf(vmax - 0.5f + 0.0625f);
   if (fx1 < 0.0f || fy1 < 0.0f || fx0 > (float)(W - 1) || fy0 > (float)(H - 1))
     return make_short4(1, 1, 0, 0);  // empty
   const int x0 = (int)fmaxf(fx0, 0.0f), y0 = (int)fmaxf(fy0, 0.0f);
