@@ -8,7 +8,7 @@
 // Here ONE launch evaluates a whole batch: one 512-thread workgroup (8 waves)
 // per tuple, two workgroups per CU.
 //  1. The object's meshlets (<= 64 triangles / 64 vertices each) are culled per
-//     pose: the 8 corners of each meshlet AABB are projected (float32, the
+//     pose: the 8 corners of each meshlet OBB are projected (float32, the
 //     vertex arithmetic) into a conservative pixel rectangle kept in registers.
 //     Their union is the tuple's region of interest (ROI): pixels outside both
 //     silhouettes cannot change VSD (masks need d_model > 0, visibility.py:37).
