@@ -240,6 +240,10 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       }
     }
   }
+  // Both q tiles start at 0 once per tuple; afterwards the pixel pass zeroes
+  // every pixel it reads (the only ones the raster can have written), so the
+  // tiles are clean for the next tile without a separate clearing pass.
+  for (int i = tid; i < 2 * kTileStride * kTileH; i += kVsdThreads) (&s_dep[0][0])[i] = 0u;
   __syncthreads();
   const int rx0 = s_roi[0], ry0 = s_roi[1], rx1 = s_roi[2], ry1 = s_roi[3];
 
@@ -263,9 +267,8 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
     for (int t = 0; t < ntx * nty; ++t) {
       const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
       const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
-      // 2a. clear both q tiles, list the (pose, meshlet) entries touching the tile.
-      uint32_t* dep_flat = &s_dep[0][0];
-      for (int i = tid; i < 2 * kTileStride * kTileH; i += kVsdThreads) dep_flat[i] = 0u;
+      // 2a. list the (pose, meshlet) entries touching the tile (the q tiles are
+      // already zero, see the pixel pass).
       if (tid == 0) {
         s_nlist = 0;
         s_next = 0;
@@ -432,6 +435,8 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         const int row = ty0 + p / kTileW, col = tx0 + p % kTileW;
         const int ps = (p / kTileW) * kTileStride + p % kTileW;
         const uint32_t qe = s_dep[0][ps], qg = s_dep[1][ps];
+        s_dep[0][ps] = 0u;  // clean for the next tile (rows are wave-private here)
+        s_dep[1][ps] = 0u;
         if VSD_DIAG(4) atomicAdd(&g_vsd_stats[6], 1ull);
         if constexpr (COST == kCostCover) {  // silhouettes only (cus, cou_bb_proj)
           ++c_union;
