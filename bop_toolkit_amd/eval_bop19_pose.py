@@ -100,8 +100,7 @@ def evaluate(p, device=0, calc_errors=True):
     dataset = str(result_name.split("_")[1].split("-")[0])
     ests = inout.load_bop_results(os.path.join(p["results_path"], result_filename))
     avg_time = average_time_per_image(ests)
-    cache = ecs._Cache()
-    average_recalls = {}
+    jobs, owner = [], []
     for error in p["errors"]:
       if calc_errors:
         ece.run(ece.parse_args(errors_argv(p, error, result_filename)), device)
@@ -113,23 +112,28 @@ def evaluate(p, device=0, calc_errors=True):
                  for tau in error["vsd_taus"]]
       else:
         signs = [misc.get_error_signature(error["type"], error["n_top"])]
-      recalls = []
       for sign in dict.fromkeys(signs):
         error_dir_path = os.path.join(result_name, sign)
-        for th in error["correct_th"]:
-          sp = ecs.parse_args([
-              "--error_dir_paths={}".format(error_dir_path),
-              "--eval_path={}".format(p["eval_path"]),
-              "--targets_filename={}".format(p["targets_filename"]),
-              "--visib_gt_min={}".format(p["visib_gt_min"]),
-              "--correct_th_{}={}".format(error["type"], ",".join(map(str, th)))])
-          scores, _ = ecs.score_error_dir(sp, error_dir_path, cache=cache)
-          recalls.append(scores["recall"])
-      average_recalls[error["type"]] = np.mean(recalls)
-      misc.log("Recall scores: {}".format(" ".join(map(str, recalls))))
-      misc.log("Average recall: {}".format(average_recalls[error["type"]]))
+        sps = [ecs.parse_args([
+            "--error_dir_paths={}".format(error_dir_path),
+            "--eval_path={}".format(p["eval_path"]),
+            "--targets_filename={}".format(p["targets_filename"]),
+            "--visib_gt_min={}".format(p["visib_gt_min"]),
+            "--correct_th_{}={}".format(error["type"], ",".join(map(str, th)))])
+            for th in error["correct_th"]]
+        jobs.append((error_dir_path, sps))
+        owner.append(error["type"])
     if ece._dist()[0] != 0:
       continue
+    # every (folder, threshold) setting is independent: folders in parallel
+    folder_scores = ecs.score_folders(jobs)
+    average_recalls = {}
+    for error in p["errors"]:
+      recalls = [s["recall"] for o, fs in zip(owner, folder_scores) if o == error["type"]
+                 for s in fs]
+      average_recalls[error["type"]] = np.mean(recalls)
+      misc.log("Recall scores ({}): {}".format(error["type"], " ".join(map(str, recalls))))
+      misc.log("Average recall: {}".format(average_recalls[error["type"]]))
     misc.log("Evaluation of {} took {}s.".format(result_filename, time.time() - t0))
     final = {"bop19_average_recall_{}".format(e["type"]): average_recalls[e["type"]]
              for e in p["errors"]}

@@ -80,15 +80,42 @@ def valid_gts(im_gt, im_gt_info, im_targets, visib_gt_min):
 
 
 class _Cache:
-  """Per-dataset inputs shared by all thresholds of one evaluation."""
+  """Per-dataset inputs shared by all thresholds of one evaluation, and the
+  parsed (normalised, grouped) errors files of the most recent errors folder:
+  eval_bop19_pose scores every folder at 10 thresholds in a row."""
 
   def __init__(self):
     self.d = {}
+    self._folder = None
+    self._errs = {}
 
   def get(self, key, fn):
     if key not in self.d:
       self.d[key] = fn()
     return self.d[key]
+
+  def errors(self, folder, path, fn):
+    if folder != self._folder:
+      self._folder, self._errs = folder, {}
+    st = os.stat(path)
+    key = (path, st.st_mtime_ns, st.st_size)
+    if key not in self._errs:
+      self._errs[key] = fn()
+    return self._errs[key]
+
+
+def _load_errors(path, models_info, by_dia, width_factor):
+  """errors_*.json of a scene, normalised (eval_calc_scores.py:221-233) and
+  grouped per (image, object) in match order."""
+  scene_errs = inout.load_json(path, keys_to_int=True)
+  if by_dia:
+    for err in scene_errs:
+      dia = float(models_info[err["obj_id"]]["diameter"])
+      err["errors"] = {g: [e / dia for e in v] for g, v in err["errors"].items()}
+  if width_factor is not None:
+    for err in scene_errs:
+      err["errors"] = {g: [width_factor * e for e in v] for g, v in err["errors"].items()}
+  return pose_matching.group_scene_errs(scene_errs)
 
 
 def score_error_dir(p, error_dir_path, correct_th=None, cache=None, do_print=True):
@@ -121,19 +148,16 @@ def score_error_dir(p, error_dir_path, correct_th=None, cache=None, do_print=Tru
     ipath = dp_split["scene_gt_info_tpath"].format(scene_id=scene_id)
     scene_gt_info = cache.get(("gti", ipath), lambda: inout.load_json(ipath, keys_to_int=True))
     gt_curr = {im: scene_gt[im] for im in scene_targets}
-    gt_valid = {im: valid_gts(scene_gt[im], scene_gt_info[im], tg, p["visib_gt_min"])
-                for im, tg in scene_targets.items()}
-    scene_errs = inout.load_json(p["error_tpath"].format(
-        eval_path=p["eval_path"], error_dir_path=error_dir_path, scene_id=scene_id),
-        keys_to_int=True)
-    if err_type in p["normalized_by_diameter"]:
-      for err in scene_errs:
-        dia = float(models_info[err["obj_id"]]["diameter"])
-        err["errors"] = {g: [e / dia for e in v] for g, v in err["errors"].items()}
-    if err_type in p["normalized_by_im_width"]:
-      factor = 640.0 / float(dp_split["im_size"][0])
-      for err in scene_errs:
-        err["errors"] = {g: [factor * e for e in v] for g, v in err["errors"].items()}
+    gt_valid = cache.get(("valid", ipath, tpath, p["visib_gt_min"]), lambda: {
+        im: valid_gts(scene_gt[im], scene_gt_info[im], tg, p["visib_gt_min"])
+        for im, tg in scene_targets.items()})
+    epath = p["error_tpath"].format(eval_path=p["eval_path"], error_dir_path=error_dir_path,
+                                    scene_id=scene_id)
+    by_dia = err_type in p["normalized_by_diameter"]
+    factor = (640.0 / float(dp_split["im_size"][0])
+              if err_type in p["normalized_by_im_width"] else None)
+    scene_errs = cache.errors(error_dir_path, epath,
+                              lambda: _load_errors(epath, models_info, by_dia, factor))
     matches += pose_matching.match_poses_scene(scene_id, gt_curr, gt_valid, scene_errs, th,
                                                n_top)
   scores = score.calc_localization_scores(dp_split["scene_ids"], dp_model["obj_ids"], matches,
@@ -142,6 +166,31 @@ def score_error_dir(p, error_dir_path, correct_th=None, cache=None, do_print=Tru
   inout.save_json(p["out_scores_tpath"].format(**fmt), scores)
   inout.save_json(p["out_matches_tpath"].format(**fmt), matches)
   return scores, score_sign
+
+
+def _score_job(job):
+  error_dir_path, sps, do_print = job
+  cache = _Cache()
+  return [score_error_dir(sp, error_dir_path, cache=cache, do_print=do_print)[0] for sp in sps]
+
+
+def score_folders(jobs, workers=None, do_print=True):
+  """Scores of several errors folders, each at several settings: jobs is a
+  list of (error_dir_path, [params per setting]); returns the scores dicts in
+  the same nesting and order. Folders are independent (the reference scores
+  every setting in its own interpreter, eval_bop19_pose.py:150-213), so with
+  more than one worker they are scored in a pool of spawned processes
+  (host-only modules: no GPU state is inherited). workers: default
+  $BOPX_SCORE_WORKERS, else min(#folders, CPUs, 16)."""
+  if workers is None:
+    workers = int(os.environ.get("BOPX_SCORE_WORKERS", "0")) or \
+        min(len(jobs), os.cpu_count() or 1, 16)
+  args = [(path, sps, do_print) for path, sps in jobs]
+  if workers <= 1 or len(jobs) <= 1:
+    return [_score_job(a) for a in args]
+  import multiprocessing as mp
+  with mp.get_context("spawn").Pool(workers) as pool:
+    return pool.map(_score_job, args, chunksize=1)
 
 
 def main(argv=None):

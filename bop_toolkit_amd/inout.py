@@ -108,23 +108,41 @@ def save_ply(path, pts, faces):
     f.write(farr.tobytes())
 
 
+def _make_dumps():
+  """json.dumps(o, sort_keys=True) without the per-call encoder set-up: one C
+  encoder (the one json.dumps itself builds for every call) reused for every
+  element. Same bytes: same separators, float repr, ASCII escaping, NaN/inf."""
+  from json import encoder as je
+  if getattr(je, "c_make_encoder", None) is None:
+    return json.JSONEncoder(sort_keys=True).encode
+
+  def default(o):
+    raise TypeError("Object of type {} is not JSON serializable".format(type(o).__name__))
+
+  enc = je.c_make_encoder(None, default, je.encode_basestring_ascii, None, ": ", ", ", True,
+                          False, True)
+
+  def dumps(o):
+    if isinstance(o, str):
+      return je.encode_basestring_ascii(o)
+    return "".join(enc(o, 0))
+  return dumps
+
+
+_dumps = _make_dumps()
+
+
 def save_json(path, content):
   """JSON with one top-level element per line and sorted keys
   (inout.py:85-113), the format of the errors_*.json hand-off files."""
   with open(path, "w") as f:
     if isinstance(content, dict):
       items = sorted(content.items(), key=lambda x: x[0])
-      f.write("{\n")
-      for i, (k, v) in enumerate(items):
-        f.write('  "{}": {}'.format(k, json.dumps(v, sort_keys=True)))
-        f.write(",\n" if i != len(items) - 1 else "\n")
-      f.write("}")
+      body = ",\n".join('  "{}": {}'.format(k, _dumps(v)) for k, v in items)
+      f.write("{\n" + body + ("\n}" if items else "}"))
     elif isinstance(content, list):
-      f.write("[\n")
-      for i, e in enumerate(content):
-        f.write("  {}".format(json.dumps(e, sort_keys=True)))
-        f.write(",\n" if i != len(content) - 1 else "\n")
-      f.write("]")
+      body = ",\n".join("  " + _dumps(e) for e in content)
+      f.write("[\n" + body + ("\n]" if content else "]"))
     else:
       json.dump(content, f, sort_keys=True)
 

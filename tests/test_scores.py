@@ -8,6 +8,7 @@ import json
 import os
 import shutil
 
+import numpy as np
 import pytest
 
 from bop_toolkit_amd import eval_bop19_pose as e19
@@ -74,6 +75,60 @@ def test_match_poses_greedy_rules():
   # rete-style: every element must be lowest so far
   e2 = [{"est_id": 0, "score": 1.0, "errors": {0: [1.0, 4.0], 1: [2.0, 3.0]}}]
   assert pose_matching.match_poses(e2, [5.0, 5.0])[0]["gt_id"] == 0
+
+
+def _match_scene_plain(scene_gt, valid, errs, th, n_top):
+  """Unoptimised restatement of pose_matching.py:93-160 (flat list, fresh sort
+  and the all-elements rule for every group) to check the scalar fast path."""
+  out = []
+  for im_id, im_gts in scene_gt.items():
+    recs = [[-1, -1, -1, -1] for _ in im_gts]  # est_id, score, error, error_norm
+    for obj_id in set(g["obj_id"] for g in im_gts):
+      group = [e for e in errs if e["im_id"] == im_id and e["obj_id"] == obj_id]
+      for m in pose_matching.match_poses(group, th, n_top, valid[im_id]):
+        recs[m["gt_id"]] = [m["est_id"], m["score"], m["error"], m["error_norm"]]
+    out += recs
+  return out
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_match_scene_fast_path_equals_plain(seed):
+  rng = np.random.default_rng(seed)
+  scene_gt, valid, errs = {}, {}, []
+  for im in range(30):
+    objs = rng.integers(1, 5, int(rng.integers(1, 6)))
+    scene_gt[im] = [{"obj_id": int(o)} for o in objs]
+    valid[im] = [bool(v) for v in rng.random(len(objs)) < 0.8]
+    for o in set(objs.tolist()):
+      gts = [g for g in range(len(objs)) if objs[g] == o]
+      for k in range(int(rng.integers(0, 4))):
+        vals = np.round(rng.random(len(gts)), 1)  # ties in errors and scores
+        errs.append({"im_id": im, "obj_id": o, "est_id": k, "score": float(rng.integers(0, 3)),
+                     "errors": {g: [float(v)] for g, v in zip(gts, vals)}})
+  for n_top in (-1, 0, 1, 2):
+    for th in ([0.35], [0.75]):
+      fast = pose_matching.match_poses_scene(1, scene_gt, valid, errs, th, n_top)
+      grouped = pose_matching.match_poses_scene(
+          1, scene_gt, valid, pose_matching.group_scene_errs(errs), th, n_top)
+      plain = _match_scene_plain(scene_gt, valid, errs, th, n_top)
+      got = [[r["est_id"], r["score"], r["error"], r["error_norm"]] for r in fast]
+      assert got == plain
+      assert grouped == fast
+
+
+def test_save_json_layout(tmp_path):
+  """Fast writer = the reference's per-element json.dumps(sort_keys=True)."""
+  content = [{"b": [float("inf"), 0.1 + 0.2, -0.0], "a": {3: True, 10: None}, "s": "x\u00e9"},
+             {"errors": {12: [1e-300], 0: [0.5]}, "score": 0.25}]
+  path = tmp_path / "x.json"
+  inout.save_json(str(path), content)
+  want = "[\n" + ",\n".join("  " + json.dumps(e, sort_keys=True) for e in content) + "\n]"
+  assert path.read_text() == want
+  for empty, text in (([], "[\n]"), ({}, "{\n}")):
+    inout.save_json(str(path), empty)
+    assert path.read_text() == text
+  inout.save_json(str(path), {2: [1, 2], 1: "a"})
+  assert path.read_text() == '{\n  "1": "a",\n  "2": [1, 2]\n}'
 
 
 def test_ap_and_recall():

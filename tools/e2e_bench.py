@@ -1,0 +1,203 @@
+#!/usr/bin/env python
+"""End-to-end timing of the BOP19 evaluation pipeline on a synthetic dataset.
+
+Writes a YCB-V-layout dataset (21 superellipsoid objects of 5,002 vertices,
+test scenes 48.., 6 objects per image, 16-bit depth PNGs with depth_scale 0.1
+rendered by the HIP rasteriser plus background, occluder, noise and holes) and
+a BOP19 results CSV, then times the drop-in pipeline as a user runs it:
+
+  1. calc_gt_info (scene_gt_info.json; gt_side.calc_gt_info),
+  2. eval_bop19_pose: VSD / MSSD / MSPD error files (eval_calc_errors.run)
+     and the 120 score settings (eval_calc_scores.score_error_dir),
+
+and prints one JSON line with the per-phase wall times and the end-to-end
+tuples/s. --profile adds a cProfile of phase 2 (host hot spots) to
+gpurun_out/e2e_profile.txt. Needs a GPU.
+
+    python tools/e2e_bench.py --images 2000 [--root /tmp/bopx_e2e] [--profile]
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+W, H = 640, 480
+DEPTH_SCALE = 0.1
+PER_IMG = 6
+SCENES = list(range(48, 60))
+
+
+def make_dataset(root, n_im, seed, torch):
+  from PIL import Image
+  from concurrent.futures import ThreadPoolExecutor
+  from bop_toolkit_amd import inout, misc, synth
+  from bop_toolkit_amd.batch import BatchEvaluator
+  rng = np.random.default_rng(seed)
+  ds = os.path.join(root, "datasets", "ycbv")
+  mdir = os.path.join(ds, "models_eval")
+  os.makedirs(mdir)
+  ev = BatchEvaluator(0)
+  info = {}
+  for o in range(1, 22):
+    axes = tuple(rng.uniform(30.0, 100.0, 3))
+    pts, faces = synth.superellipsoid(50, 100, axes, float(rng.uniform(0.5, 1.0)))
+    n_disc = [1, 2, 4, 8][o % 4]
+    e = synth.models_info_entry(pts, n_disc, continuous=(o == 21))
+    info[str(o)] = {k: (float(v) if not isinstance(v, list) else v) for k, v in e.items()}
+    inout.save_ply(os.path.join(mdir, "obj_%06d.ply" % o), pts, faces)
+    ev.add_object(o, pts.astype(np.float64), faces)
+  with open(os.path.join(mdir, "models_info.json"), "w") as f:
+    json.dump(info, f)
+  shutil.copytree(mdir, os.path.join(ds, "models"))
+
+  obj = np.stack([rng.choice(np.arange(1, 22), PER_IMG, replace=False)
+                  for _ in range(n_im)]).reshape(-1).astype(np.int32)
+  n = len(obj)
+  Rg, tg = synth.gt_poses(rng, n)
+  Re, te = synth.perturb(rng, Rg, tg)
+  K = synth.YCBV_K
+  dev = ev.device
+  T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+  fidx = np.repeat(np.arange(n_im, dtype=np.int32), PER_IMG)
+  cam = np.tile([K[0, 0], K[1, 1], K[0, 2], K[1, 2]], (n_im, 1)).astype(np.float64)
+  frames = ev.render(ev.slots(obj), T(np.concatenate([Rg.reshape(n, 9), tg], 1), torch.float64),
+                     T(fidx, torch.int32), T(cam, torch.float64), n_im, W, H)
+  g = torch.Generator(device=dev)
+  g.manual_seed(seed)
+  frames = torch.where(frames > 0, frames, torch.full_like(frames, 1600.0))
+  ys = torch.arange(H, device=dev).view(1, H, 1)
+  xs = torch.arange(W, device=dev).view(1, 1, W)
+  x0 = torch.randint(0, W - 120, (n_im, 1, 1), device=dev, generator=g)
+  y0 = torch.randint(0, H - 120, (n_im, 1, 1), device=dev, generator=g)
+  sz = torch.randint(40, 120, (n_im, 1, 1), device=dev, generator=g)
+  occ = (xs >= x0) & (xs < x0 + sz) & (ys >= y0) & (ys < y0 + sz)
+  frames = torch.where(occ, torch.full_like(frames, 450.0), frames)
+  frames = frames + 2.0 * torch.randn(frames.shape, device=dev, generator=g)
+  frames[torch.rand(frames.shape, device=dev, generator=g) < 0.1] = 0.0
+  png = torch.round(frames / DEPTH_SCALE).clamp_(0, 65535).to(torch.int32).cpu().numpy()
+  png = png.astype(np.uint16)
+
+  scene_of = np.array([SCENES[i * len(SCENES) // n_im] for i in range(n_im)])
+  targets, lines = [], ["scene_id,im_id,obj_id,score,R,t,time"]
+  jobs = []
+  for s in sorted(set(scene_of.tolist())):
+    sdir = os.path.join(ds, "test", "%06d" % s)
+    os.makedirs(os.path.join(sdir, "depth"))
+    cams, gts = {}, {}
+    for im in np.nonzero(scene_of == s)[0]:
+      jobs.append((os.path.join(sdir, "depth", "%06d.png" % im), im))
+      cams[str(im)] = {"cam_K": K.reshape(-1).tolist(), "depth_scale": DEPTH_SCALE}
+      rows = range(im * PER_IMG, (im + 1) * PER_IMG)
+      gts[str(im)] = [{"cam_R_m2c": Rg[j].reshape(-1).tolist(), "cam_t_m2c": tg[j].tolist(),
+                       "obj_id": int(obj[j])} for j in rows]
+      for j in rows:
+        targets.append({"im_id": int(im), "inst_count": 1, "obj_id": int(obj[j]),
+                        "scene_id": s})
+        lines.append("%d,%d,%d,%r,%s,%s,0.5" % (
+            s, im, obj[j], float(rng.random()), " ".join(repr(float(x)) for x in Re[j].ravel()),
+            " ".join(repr(float(x)) for x in te[j])))
+    with open(os.path.join(sdir, "scene_camera.json"), "w") as f:
+      json.dump(cams, f)
+    with open(os.path.join(sdir, "scene_gt.json"), "w") as f:
+      json.dump(gts, f)
+  with ThreadPoolExecutor(16) as pool:
+    list(pool.map(lambda j: Image.fromarray(png[j[1]]).save(j[0]), jobs))
+  with open(os.path.join(ds, "test_targets_bop19.json"), "w") as f:
+    json.dump(targets, f)
+  os.makedirs(os.path.join(root, "results"))
+  result = "synth_ycbv-test.csv"
+  with open(os.path.join(root, "results", result), "w") as f:
+    f.write("\n".join(lines) + "\n")
+  del ev
+  return n, result, sorted(set(scene_of.tolist()))
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument("--images", type=int, default=2000)
+  ap.add_argument("--root", default="/tmp/bopx_e2e")
+  ap.add_argument("--seed", type=int, default=7)
+  ap.add_argument("--profile", action="store_true")
+  a = ap.parse_args()
+  import torch
+  if os.path.exists(a.root):
+    shutil.rmtree(a.root)
+  t0 = time.perf_counter()
+  n, result, scenes = make_dataset(a.root, a.images, a.seed, torch)
+  t_gen = time.perf_counter() - t0
+  datasets = os.path.join(a.root, "datasets")
+  os.environ["BOP_PATH"] = datasets
+
+  from bop_toolkit_amd import eval_bop19_pose, eval_calc_errors as ece, eval_calc_scores as ecs
+  from bop_toolkit_amd import gt_side, misc
+  misc.log = lambda s: None  # keep stdout to the JSON line
+  phases = {}
+
+  def timed(name, fn):
+    def wrap(*args, **kw):
+      t = time.perf_counter()
+      try:
+        return fn(*args, **kw)
+      finally:
+        phases[name] = phases.get(name, 0.0) + time.perf_counter() - t
+    return wrap
+
+  t0 = time.perf_counter()
+  gt_side.calc_gt_info({"dataset": "ycbv", "dataset_split": "test", "dataset_split_type": None,
+                        "delta": 15, "renderer_type": "hip", "datasets_path": datasets,
+                        "scene_ids": scenes})
+  torch.cuda.synchronize()
+  phases["calc_gt_info"] = time.perf_counter() - t0
+
+  run0, score0 = ece.run, ecs.score_error_dir
+  err_t = {}
+
+  def run_wrap(p, device=0):
+    t = time.perf_counter()
+    out = run0(p, device)
+    err_t[p["error_type"]] = time.perf_counter() - t
+    return out
+  ece.run = run_wrap
+  ecs.score_error_dir = timed("scores", score0)
+  p = eval_bop19_pose.parse_args([
+      "--result_filenames", result, "--results_path", os.path.join(a.root, "results"),
+      "--eval_path", os.path.join(a.root, "eval")])
+  prof = None
+  if a.profile:
+    import cProfile
+    prof = cProfile.Profile()
+    prof.enable()
+  t0 = time.perf_counter()
+  final = eval_bop19_pose.evaluate(p)
+  t_eval = time.perf_counter() - t0
+  if prof is not None:
+    import io
+    import pstats
+    prof.disable()
+    s = io.StringIO()
+    pstats.Stats(prof, stream=s).sort_stats("cumulative").print_stats(45)
+    pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(30)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "e2e_profile.txt"), "w") as f:
+      f.write(s.getvalue())
+  scores = final[os.path.splitext(result)[0]]
+  print(json.dumps({
+      "what": "end-to-end BOP19 evaluation (calc_gt_info + eval_bop19_pose), synthetic YCB-V "
+              "layout, 21 objs V=5002, 640x480 PNG depth, 1 GPU",
+      "images": a.images, "tuples": n, "gen_s": round(t_gen, 2),
+      "calc_gt_info_s": round(phases["calc_gt_info"], 2),
+      "errors_s": {k: round(v, 2) for k, v in err_t.items()},
+      "scores_s": round(phases.get("scores", 0.0), 2), "eval_bop19_s": round(t_eval, 2),
+      "eval_tuples_per_s": n / t_eval,
+      "ar": {k: round(float(v), 4) for k, v in scores.items()}}))
+
+
+if __name__ == "__main__":
+  main()
