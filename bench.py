@@ -289,7 +289,7 @@ def main():
       rows[:, N_TAU] = out_mssd
       rows[:, N_TAU + 1] = out_mspd
       # per-tuple error rows -> rank 0, ordered by global tuple id (RCCL)
-      shard.gather_rows(rows, gids, world * n)
+      shard.gather_rows(rows, gids, world * n, counts=[n] * world)
 
   for _ in range(args.warmup):
     step(False)

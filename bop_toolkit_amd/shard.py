@@ -45,23 +45,30 @@ def image_costs(frame_of_tuple, per_tuple_cost, n_images):
   return np.bincount(np.asarray(frame_of_tuple), weights=per_tuple_cost, minlength=n_images)
 
 
-def gather_rows(rows, ids, n_total, group=None):
+def gather_rows(rows, ids, n_total, group=None, counts=None):
   """Gather per-tuple rows from every rank to rank 0.
 
   rows: [n_local, C] float64 tensor on this rank's device (or CPU for gloo);
   ids:  [n_local] int64 tensor of global tuple ids.
+  counts: the n_local of every rank when the caller knows them (a fixed shard
+  per rank, e.g. bench.py); otherwise one all_gather of the counts first.
   Returns the [n_total, C] table ordered by global id on rank 0, None elsewhere.
-  One all_gather of the counts, one padded all_gather of [id | row] blocks.
+  One padded all_gather of [id | row] blocks, scattered by id on rank 0.
   """
   import torch
   import torch.distributed as dist
   world = dist.get_world_size(group)
   rank = dist.get_rank(group)
   dev = rows.device
-  n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
-  counts = [torch.zeros_like(n) for _ in range(world)]
-  dist.all_gather(counts, n, group=group)
-  counts = [int(c.item()) for c in counts]
+  if counts is None:
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
+    cl = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(cl, n, group=group)
+    counts = [int(c.item()) for c in cl]
+  counts = [int(c) for c in counts]
+  if len(counts) != world or counts[rank] != rows.shape[0]:
+    raise ValueError("gather_rows: counts %r do not match this rank's %d rows"
+                     % (counts, rows.shape[0]))
   width = rows.shape[1] + 1
   pad = max(counts)
   block = torch.zeros((pad, width), dtype=torch.float64, device=dev)
@@ -74,15 +81,16 @@ def gather_rows(rows, ids, n_total, group=None):
     dist.all_gather(list(out.view(world, pad, width).unbind(0)), block, group=group)
   if rank != 0:
     return None
+  if pad * world != sum(counts):  # drop the padding rows
+    keep = torch.cat([torch.arange(r * pad, r * pad + c, device=dev)
+                      for r, c in enumerate(counts)])
+    out = out.index_select(0, keep)
+  gid = out[:, 0].to(torch.int64)
+  if out.shape[0] != n_total or not bool(
+      (torch.bincount(gid, minlength=n_total)[:n_total] == 1).all()):
+    raise RuntimeError("gather_rows: tuple ids are not a permutation of 0..%d" % (n_total - 1))
   table = torch.empty((n_total, rows.shape[1]), dtype=torch.float64, device=dev)
-  filled = torch.zeros(n_total, dtype=torch.bool, device=dev)
-  for r, c in enumerate(counts):
-    seg = out[r * pad:r * pad + c]
-    gid = seg[:, 0].to(torch.int64)
-    table[gid] = seg[:, 1:]
-    filled[gid] = True
-  if not bool(filled.all()):
-    raise RuntimeError("gather_rows: %d tuple rows missing" % int((~filled).sum()))
+  table[gid] = out[:, 1:]
   return table
 
 
