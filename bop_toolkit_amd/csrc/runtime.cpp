@@ -735,10 +735,7 @@ int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double*
 static int cover_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height) {
   if (width <= 0 || height <= 0 || width > 32767 || height > 32767)
     return fail(c, BOPX_E_INVALID, "bad image size %dx%d", width, height);
-  if ((int64_t)((width + bopx::kTileW - 1) / bopx::kTileW) *
-          ((height + bopx::kTileH - 1) / bopx::kTileH) > bopx::kVsdMaxTiles)
-    return fail(c, BOPX_E_UNSUPPORTED, "image %dx%d exceeds the fused kernel's %d tiles",
-                width, height, bopx::kVsdMaxTiles);
+  // no tile limit: the 16-bit per-tau counters behind kVsdMaxTiles are VSD-only
   a.width = a.img_w = width;
   a.height = a.img_h = height;
   a.n_tau = 0;

@@ -149,14 +149,38 @@ def get_score_signature(correct_th, visib_gt_min):
       "_min-visib={:.3f}".format(visib_gt_min)
 
 
+def calc_pts_diameter2(pts):
+  """Same value as calc_pts_diameter (misc.py:296-306 is the all-pairs variant)."""
+  return calc_pts_diameter(pts)
+
+
+def ensure_dir(path):
+  """Create a directory (and parents) if missing (misc.py:34-40)."""
+  import os
+  if not os.path.exists(path):
+    os.makedirs(path)
+
+
+def clip_pt_to_im(pt, im_size):
+  """Clip a 2D point to the image frame (misc.py:191-199)."""
+  return [min(max(pt[0], 0), im_size[0] - 1), min(max(pt[1], 0), im_size[1] - 1)]
+
+
+def calc_3d_bbox(xs, ys, zs):
+  """(x, y, z, w, h, d) of a 3D point set (misc.py:221-233)."""
+  lo = [xs.min(), ys.min(), zs.min()]
+  hi = [xs.max(), ys.max(), zs.max()]
+  return [lo[0], lo[1], lo[2], hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]]
+
+
 def calc_2d_bbox(xs, ys, im_size=None, clip=False):
   """(x, y, w, h) of a point set, w = max - min (misc.py:202-218)."""
   lo = [xs.min(), ys.min()]
   hi = [xs.max(), ys.max()]
   if clip:
     assert im_size is not None
-    lo = [min(max(lo[0], 0), im_size[0] - 1), min(max(lo[1], 0), im_size[1] - 1)]
-    hi = [min(max(hi[0], 0), im_size[0] - 1), min(max(hi[1], 0), im_size[1] - 1)]
+    lo = clip_pt_to_im(lo, im_size)
+    hi = clip_pt_to_im(hi, im_size)
   return [lo[0], lo[1], hi[0] - lo[0], hi[1] - lo[1]]
 
 
