@@ -65,6 +65,21 @@ __device__ __forceinline__ void proj_mat(const double* K, const double* R, const
 #define BOPX_SYM_CHUNK 64
 #endif
 constexpr int kSymChunk = BOPX_SYM_CHUNK;  // <= 64: a unit's symmetries fit wave 0
+// Vertices staged in LDS per round (two barriers each). MSSD: large rounds keep
+// the barrier count low when a unit has few symmetries (S = 1: one d2 per
+// vertex); MSPD stages 5 values per vertex, where a smaller LDS footprint (more
+// resident blocks) measured faster (profiles/: 1024 -> 0.79 ms MSSD, 256 ->
+// 1.21 ms MSPD).
+#ifndef BOPX_SYM_STAGE_MSSD
+#define BOPX_SYM_STAGE_MSSD 1024
+#endif
+#ifndef BOPX_SYM_STAGE_MSPD
+#define BOPX_SYM_STAGE_MSPD 256
+#endif
+template <int MODE>
+constexpr int kSymStage = MODE ? BOPX_SYM_STAGE_MSPD : BOPX_SYM_STAGE_MSSD;
+static_assert(kSymStage<0> % kPoseThreads == 0 && kSymStage<1> % kPoseThreads == 0,
+              "whole staging passes");
 
 __global__ void k_sym_init(double* __restrict__ out, int64_t n) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -91,9 +106,9 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
                                                             const double* __restrict__ Km,
                                                             double* __restrict__ out, int nch) {
   __shared__ double s_red[kPoseThreads];
-  // A block of vertices staged for every symmetry of the unit: x, y, z and,
-  // for MSPD, the estimate's projection u_e, v_e.
-  __shared__ double s_v[5][kPoseThreads];
+  // A block of kSymStage vertices staged for every symmetry of the unit: x, y, z
+  // and, for MSPD, the estimate's projection u_e, v_e.
+  __shared__ double s_v[MODE ? 5 : 3][kSymStage<MODE>];
   const int64_t b = blockIdx.x / nch;
   const int c = blockIdx.x % nch;
   const int tid = threadIdx.x;
@@ -120,7 +135,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
   const gptr<const double> py = px + nv;
   const gptr<const double> pz = py + nv;
   double m0 = -INFINITY, m1 = -INFINITY, m2 = -INFINITY, m3 = -INFINITY;
-  if (MODE == 0) {
+  if constexpr (MODE == 0) {
     double E[12], A[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) E[i] = pe[12 * b + i];
@@ -136,14 +151,16 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
       const double dx = aff(A, 0, x, y, z), dy = aff(A, 1, x, y, z), dz = aff(A, 2, x, y, z);
       return fma(dz, dz, fma(dy, dy, dx * dx));
     };
-    for (int v0 = 0; v0 < nv; v0 += kPoseThreads) {
-      const int nb = min(kPoseThreads, nv - v0);
+    for (int v0 = 0; v0 < nv; v0 += kSymStage<MODE>) {
+      const int nb = min(kSymStage<MODE>, nv - v0);
       __syncthreads();
-      if (tid < nb) {
-        s_v[0][tid] = px[v0 + tid];
-        s_v[1][tid] = py[v0 + tid];
-        s_v[2][tid] = pz[v0 + tid];
-      }
+#pragma unroll
+      for (int i = tid; i < kSymStage<MODE>; i += kPoseThreads)
+        if (i < nb) {
+          s_v[0][i] = px[v0 + i];
+          s_v[1][i] = py[v0 + i];
+          s_v[2][i] = pz[v0 + i];
+        }
       __syncthreads();
       if (g < ng) {
         int j = g;
@@ -167,22 +184,24 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
     auto d2 = [&](int j) {
       const double x = s_v[0][j], y = s_v[1][j], z = s_v[2][j];
       const double izg = rcp64(aff(A, 2, x, y, z));
-      const double du = s_v[3][j] - aff(A, 0, x, y, z) * izg;
-      const double dv = s_v[4][j] - aff(A, 1, x, y, z) * izg;
+      const double du = fma(-aff(A, 0, x, y, z), izg, s_v[3][j]);
+      const double dv = fma(-aff(A, 1, x, y, z), izg, s_v[4][j]);
       return fma(dv, dv, du * du);
     };
-    for (int v0 = 0; v0 < nv; v0 += kPoseThreads) {
-      const int nb = min(kPoseThreads, nv - v0);
+    for (int v0 = 0; v0 < nv; v0 += kSymStage<MODE>) {
+      const int nb = min(kSymStage<MODE>, nv - v0);
       __syncthreads();
-      if (tid < nb) {
-        const double x = px[v0 + tid], y = py[v0 + tid], z = pz[v0 + tid];
-        const double ize = rcp64(aff(Pe, 2, x, y, z));
-        s_v[0][tid] = x;
-        s_v[1][tid] = y;
-        s_v[2][tid] = z;
-        s_v[3][tid] = aff(Pe, 0, x, y, z) * ize;
-        s_v[4][tid] = aff(Pe, 1, x, y, z) * ize;
-      }
+#pragma unroll
+      for (int i = tid; i < kSymStage<MODE>; i += kPoseThreads)
+        if (i < nb) {
+          const double x = px[v0 + i], y = py[v0 + i], z = pz[v0 + i];
+          const double ize = rcp64(aff(Pe, 2, x, y, z));
+          s_v[0][i] = x;
+          s_v[1][i] = y;
+          s_v[2][i] = z;
+          s_v[3][i] = aff(Pe, 0, x, y, z) * ize;
+          s_v[4][i] = aff(Pe, 1, x, y, z) * ize;
+        }
       __syncthreads();
       if (g < ng) {
         int j = g;
@@ -227,7 +246,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_mean_error(const ObjDesc* __re
     E[i] = pe[12 * b + i];
     G[i] = pg[12 * b + i];
   }
-  if (MODE == 0) {
+  if constexpr (MODE == 0) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
 #pragma unroll
