@@ -380,3 +380,12 @@ def test_fused_vsd_bit_exact_large_meshes(oracle_mod):
   from bop_toolkit_amd import synth
   _fused_vs_oracle(oracle_mod, 15, 6, 640, 480, synth.YCBV_K, 100, 150)  # 30k tris: RPT 2
   _fused_vs_oracle(oracle_mod, 16, 6, 640, 480, synth.LMO_K, 150, 200)   # 60k tris: RPT 4
+
+
+def test_fused_vsd_bit_exact_large_images(oracle_mod):
+  """ITODD-like 1280x960 (delta 5, dataset_params.py) and HOPE-like 1920x1080
+  frames: many tiles per tuple, bit-exact."""
+  K_itodd = np.array([[2992.0, 0.0, 640.5], [0.0, 2992.0, 480.5], [0.0, 0.0, 1.0]])
+  K_hope = np.array([[1390.0, 0.0, 960.0], [0.0, 1390.0, 540.0], [0.0, 0.0, 1.0]])
+  _fused_vs_oracle(oracle_mod, 17, 4, 1280, 960, K_itodd, 30, 60, delta=5.0)
+  _fused_vs_oracle(oracle_mod, 18, 4, 1920, 1080, K_hope, 30, 60)
