@@ -254,9 +254,17 @@ def main():
   rank = int(os.environ.get("RANK", 0))
   world = int(os.environ.get("WORLD_SIZE", 1))
   local = int(os.environ.get("LOCAL_RANK", 0))
+  # BOPX_DIST_BACKEND=gloo: rehearsal of the multi-rank flow with several ranks
+  # on one GPU (host collectives); the measured configuration is RCCL, one GPU per rank.
+  backend = os.environ.get("BOPX_DIST_BACKEND", "nccl")
+  if backend == "gloo":
+    local %= torch.cuda.device_count()
   torch.cuda.set_device(local)
   if world > 1:
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if backend == "nccl":
+      dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+      dist.init_process_group(backend)
   from bop_toolkit_amd import shard
   from bop_toolkit_amd.batch import BatchEvaluator
   ev = BatchEvaluator(local)
@@ -299,7 +307,10 @@ def main():
       rows[:, N_TAU] = out_mssd
       rows[:, N_TAU + 1] = out_mspd
       # per-tuple error rows -> rank 0, ordered by global tuple id (RCCL)
-      shard.gather_rows(rows, gids, world * n, counts=[n] * world)
+      if backend == "nccl":
+        shard.gather_rows(rows, gids, world * n, counts=[n] * world)
+      else:
+        shard.gather_rows(rows.cpu(), gids.cpu(), world * n, counts=[n] * world)
 
   for _ in range(args.warmup):
     step(False)
@@ -319,7 +330,8 @@ def main():
     for k in ktime:
       ktime[k] += e[k][0].elapsed_time(e[k][1]) * 1e-3
   if world > 1:
-    tt = torch.tensor([elapsed], dtype=torch.float64, device=ev.device)
+    tt = torch.tensor([elapsed], dtype=torch.float64,
+                      device=ev.device if backend == "nccl" else "cpu")
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = float(tt.item())
 
@@ -341,7 +353,9 @@ def main():
       b, f32, f64 = cost[dom]
       ach = b / kt[dom] / 1e9
       t_valu = f64 / (FP64_PEAK_TF * 1e12) + f32 / (FP32_PEAK_TF * 1e12)
-      traffic = load_traffic() if dom == "vsd" and args.config == 3 else None
+      # PMC bytes were collected on the default configs[3] shard (tools/pmc.sh)
+      traffic = load_traffic() if (dom == "vsd" and args.config == 3 and
+                                   args.tuples == CONFIGS[3]["tuples"]) else None
       roof = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
               "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": traffic,
               "kernel": "k_vsd" if dom == "vsd" else "k_sym_error<%s>" % dom.upper(),
