@@ -38,6 +38,9 @@ FP32_PEAK_TF = 157.3
 # BASELINE.json configs (index): per-GPU shard of the workload each names.
 # Default: configs[3], the metric's configuration (BOP19 set, 100k est / 8 GPUs).
 CONFIGS = {
+    0: {"objects": 1, "n_lat": 25, "n_lon": 40, "syms": [1], "continuous": False,
+        "tuples": 100, "K": "LMO_K", "W": 640, "H": 480, "errors": ("add", "adi"),
+        "what": "configs[0]: ADD/ADI, 1 LM-O-like obj ~1k verts, 100 est/gt pairs"},
     1: {"objects": 8, "n_lat": 50, "n_lon": 100, "syms": [1, 2, 4, 8], "continuous": False,
         "tuples": 10000, "K": "LMO_K", "W": 640, "H": 480, "errors": ("mssd", "mspd"),
         "what": "configs[1]: MSSD+MSPD, 8 LM-O-like objs, S<=8, 10k est/GPU"},
@@ -111,7 +114,7 @@ def build_workload(ev, objs, args, rank, torch):
   plane + occluder + noise + 10 % holes, rounded to integer mm (uint16 PNG)."""
   from bop_toolkit_amd import synth
   rng = np.random.default_rng(args.seed + 1000 * (rank + 1))
-  per_img = 6
+  per_img = min(6, len(objs))
   n_img = (args.tuples + per_img - 1) // per_img
   n = n_img * per_img
   obj = np.stack([rng.choice(len(objs), per_img, replace=False) for _ in range(n_img)]).reshape(-1)
@@ -199,7 +202,11 @@ def algorithmic_cost(objs, host, n, K):
   mspd_bytes = mssd_bytes + n * 72
   mssd_f64 = (V * (18 + 28 * S)).sum()
   mspd_f64 = (V * (20 + 27 * S)).sum()
-  return {"vsd": (vsd_bytes, vsd_f32, vsd_f64), "mssd": (mssd_bytes, 0.0, mssd_f64),
+  pts_bytes = n * (192 + 4 + 8) + sum(24 * len(objs[o]["pts"]) for o in used)
+  add_f64 = (46 * V).sum()
+  adi_f64 = (36 * V + 9 * V * V).sum()  # brute-force NN
+  return {"add": (pts_bytes, 0.0, add_f64), "adi": (pts_bytes, 0.0, adi_f64),
+          "vsd": (vsd_bytes, vsd_f32, vsd_f64), "mssd": (mssd_bytes, 0.0, mssd_f64),
           "mspd": (mspd_bytes, 0.0, mspd_f64), "roi_mean": float(roi.mean())}
 
 
@@ -246,6 +253,21 @@ def cpu_baseline(objs, d, n, seconds):
                     "oracle/bopx_oracle.c, reference per-tuple algorithm in C" % (m, m, t1)}
 
 
+def cpu_baseline_point(objs, d, n):
+  """configs[0] on the host: the oracle's ADD and brute-force ADI (C restatement
+  of pose_error.py:147-184), one tuple after the other on one core."""
+  from oracle import oracle
+  h = d["host"]
+  t0 = time.perf_counter()
+  for i in range(n):
+    pts = objs[h["obj"][i]]["pts"]
+    oracle.add(pts, h["pe"][i], h["pg"][i])
+    oracle.adi(pts, h["pe"][i], h["pg"][i])
+  dt = time.perf_counter() - t0
+  return {"value": n / dt, "unit": "tuples/s", "cores": 1, "kind": "port",
+          "sample": "all %d tuples, ADD + ADI, %.2f s; oracle/bopx_oracle.c" % (n, dt)}
+
+
 def main():
   args = parse()
   import torch
@@ -290,7 +312,9 @@ def main():
         "vsd": lambda: ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"],
                               d["frames"], d["cam"], DELTA, TAUS, d["diameters"], out=out_vsd),
         "mssd": lambda: ev.mssd(d["slots"], d["pose_est"], d["pose_gt"], out=out_mssd),
-        "mspd": lambda: ev.mspd(d["slots"], d["pose_est"], d["pose_gt"], d["K"], out=out_mspd)}
+        "mspd": lambda: ev.mspd(d["slots"], d["pose_est"], d["pose_gt"], d["K"], out=out_mspd),
+        "add": lambda: ev.add(d["slots"], d["pose_est"], d["pose_gt"], out=out_mssd),
+        "adi": lambda: ev.adi(d["slots"], d["pose_est"], d["pose_gt"], out=out_mspd)}
     main = torch.cuda.current_stream(ev.device)
     if side is not None:
       side.wait_stream(main)  # previous step's rows consumed before they are rewritten
@@ -358,13 +382,16 @@ def main():
                                    args.tuples == CONFIGS[3]["tuples"]) else None
       roof = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
               "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": traffic,
-              "kernel": "k_vsd" if dom == "vsd" else "k_sym_error<%s>" % dom.upper(),
+              "kernel": {"vsd": "k_vsd", "mssd": "k_sym_error<MSSD>", "mspd": "k_sym_error<MSPD>",
+                         "add": "k_mean_error<ADD>", "adi": "k_adi"}[dom],
               "binding": {"roof": "valu", "frac": round(t_valu / kt[dom], 4),
                           "note": "VALU-bound by SURVEY.md §8d flop/byte; fp64 %.1f TF + "
                                   "fp32 %.1f TF peaks" % (FP64_PEAK_TF, FP32_PEAK_TF)}}
     cpu = None
     if world == 1 and not args.no_cpu_baseline and len(args.cfg["errors"]) == 3:
       cpu = cpu_baseline(objs, d, n, args.cpu_seconds)
+    elif world == 1 and not args.no_cpu_baseline and args.cfg["errors"] == ("add", "adi"):
+      cpu = cpu_baseline_point(objs, d, n)
     line = {
         "metric": "pose-error tuples/sec (%s) at %dx%d, ~%dk-vert meshes" % (
             "+".join(e.upper() for e in args.cfg["errors"]), W, H,
