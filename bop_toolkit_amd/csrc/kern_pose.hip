@@ -164,13 +164,11 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
       __syncthreads();
       if (g < ng) {
         int j = g;
-        for (; j + 3 * ng < nb; j += 4 * ng) {
-          m0 = fmax(m0, d2(j));
-          m1 = fmax(m1, d2(j + ng));
-          m2 = fmax(m2, d2(j + 2 * ng));
-          m3 = fmax(m3, d2(j + 3 * ng));
-        }
-        for (; j < nb; j += ng) m0 = fmax(m0, d2(j));
+        // A max tree over fresh arithmetic results: only the loop-carried m0
+        // needs the IEEE-mode canonicalisation before v_max_f64 (once per 4).
+        for (; j + 3 * ng < nb; j += 4 * ng)
+          m0 = fmax(m0, fmax(fmax(d2(j), d2(j + ng)), fmax(d2(j + 2 * ng), d2(j + 3 * ng))));
+        for (; j < nb; j += ng) m1 = fmax(m1, d2(j));
       }
     }
   } else {
@@ -205,10 +203,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
       __syncthreads();
       if (g < ng) {
         int j = g;
-        for (; j + ng < nb; j += 2 * ng) {
-          m0 = fmax(m0, d2(j));
-          m1 = fmax(m1, d2(j + ng));
-        }
+        for (; j + ng < nb; j += 2 * ng) m0 = fmax(m0, fmax(d2(j), d2(j + ng)));
         if (j < nb) m2 = fmax(m2, d2(j));
       }
     }
