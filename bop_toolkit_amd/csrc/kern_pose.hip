@@ -343,13 +343,19 @@ __global__ __launch_bounds__(kPoseThreads) void k_adi(const ObjDesc* __restrict_
         s_e[2][j] = aff(Ea, 2, x, y, z);
       }
       __syncthreads();
-      for (int j = 0; j < nj; ++j) {
-        const double ex = s_e[0][j], ey = s_e[1][j], ez = s_e[2][j];
+      auto d2 = [&](int j, int q) {
+        const double dx = s_e[0][j] - qx[q], dy = s_e[1][j] - qy[q], dz = s_e[2][j] - qz[q];
+        return fma(dz, dz, fma(dy, dy, dx * dx));
+      };
+      // pairs: one IEEE canonicalisation of the loop-carried minimum per two points
+      int j = 0;
+      for (; j + 1 < nj; j += 2) {
 #pragma unroll
-        for (int q = 0; q < kAdiQ; ++q) {
-          const double dx = ex - qx[q], dy = ey - qy[q], dz = ez - qz[q];
-          best[q] = fmin(best[q], fma(dz, dz, fma(dy, dy, dx * dx)));
-        }
+        for (int q = 0; q < kAdiQ; ++q) best[q] = fmin(best[q], fmin(d2(j, q), d2(j + 1, q)));
+      }
+      if (j < nj) {
+#pragma unroll
+        for (int q = 0; q < kAdiQ; ++q) best[q] = fmin(best[q], d2(j, q));
       }
     }
 #pragma unroll
