@@ -107,7 +107,7 @@ def _setup(p):
     path = dp_model["model_tpath"].format(obj_id=obj_id)
     if os.path.exists(path):
       m = inout.load_ply(path)
-      ev.add_object(obj_id, m["pts"], m["faces"])
+      ev.add_object(obj_id, m["pts"], m.get("faces"))
   scene_ids = p.get("scene_ids") or dataset_params.get_present_scene_ids(dp_split)
   return torch, ev, dp_split, scene_ids
 

@@ -1,8 +1,9 @@
 """Host I/O needed around the pose-error path (subset of bop_toolkit_lib/inout.py).
 
-load_ply reads the vertices and triangles of a BOP model (inout.py:401-583
-parses them with a per-vertex Python loop; here the binary body is decoded
-with one structured-dtype read). Other per-vertex attributes are skipped.
+load_ply reads a BOP model (inout.py:401-583 parses it with a per-vertex
+Python loop; here each element's body is decoded with one structured-dtype
+read): pts, faces, normals, colors, per-vertex and per-face texture
+coordinates and the texture file name, as float64 arrays like the reference.
 """
 import json
 
@@ -14,10 +15,13 @@ _PLY_TYPES = {
     "int": "i4", "int32": "i4", "uint": "u4", "uint32": "u4",
     "float": "f4", "float32": "f4", "double": "f8", "float64": "f8",
 }
+_FACE_CORNERS = 3  # only triangles (inout.py:416)
 
 
 def _read_header(f):
-  elements, fmt = [], None
+  """(format, elements, texture_file); elements: [{'name', 'count', 'props':
+  [(name, 'scalar', type, None) | (name, 'list', count type, item type)]}]."""
+  elements, fmt, texture_file = [], None, None
   line = f.readline().strip()
   if line != b"ply":
     raise ValueError("not a PLY file")
@@ -25,69 +29,114 @@ def _read_header(f):
     line = f.readline()
     if not line:
       raise ValueError("truncated PLY header")
-    tok = line.decode("ascii", "replace").split()
+    text = line.decode("utf8", "replace").rstrip("\n").rstrip("\r")
+    tok = text.split()
     if not tok:
       continue
-    if tok[0] == "format":
+    if text.startswith("comment TextureFile"):
+      texture_file = tok[-1]
+    elif tok[0] == "format":
       fmt = tok[1]
     elif tok[0] == "element":
       elements.append({"name": tok[1], "count": int(tok[2]), "props": []})
-    elif tok[0] == "property":
+    elif tok[0] == "property" and elements:
       if tok[1] == "list":
         elements[-1]["props"].append((tok[4], "list", _PLY_TYPES[tok[2]], _PLY_TYPES[tok[3]]))
       else:
         elements[-1]["props"].append((tok[2], "scalar", _PLY_TYPES[tok[1]], None))
     elif tok[0] == "end_header":
-      return fmt, elements
+      return fmt, elements, texture_file
+
+
+def _binary_element(body, off, el):
+  """Structured array of one element (list properties of constant length,
+  taken from the first record) and the offset after it."""
+  n = el["count"]
+  fields, pos = [], off
+  for name, kind, t, it in el["props"]:
+    if kind == "scalar":
+      fields.append((name, "<" + t))
+      pos += np.dtype(t).itemsize
+    else:
+      cnt = int(np.frombuffer(body, "<" + t, count=1, offset=pos)[0]) if n else 0
+      fields.append(("n_" + name, "<" + t))
+      fields.append((name, "<" + it, (cnt,)))
+      pos += np.dtype(t).itemsize + cnt * np.dtype(it).itemsize
+  dt = np.dtype(fields)
+  if n == 0:
+    return np.zeros(0, dt), off
+  return np.frombuffer(body, dt, count=n, offset=off), off + n * dt.itemsize
+
+
+def _ascii_element(lines, pos, el):
+  """Dict name -> column(s) of one element from its text lines."""
+  n = el["count"]
+  rows = [l.split() for l in lines[pos:pos + n]]
+  cols, k = {}, 0
+  for name, kind, _, _ in el["props"]:
+    if kind == "scalar":
+      cols[name] = np.array([r[k] for r in rows], np.float64)
+      k += 1
+    else:
+      cnt = np.array([int(r[k]) for r in rows], np.int64) if n else np.zeros(0, np.int64)
+      c0 = int(cnt[0]) if n else 0
+      cols["n_" + name] = cnt
+      cols[name] = np.array([r[k + 1:k + 1 + c0] for r in rows], np.float64).reshape(n, c0)
+      k += 1 + c0
+  return cols, pos + n
 
 
 def load_ply(path):
-  """Returns {'pts': V x 3 float64, 'faces': F x 3 int64}."""
+  """{'pts': V x 3, 'faces': F x 3 (when F > 0), and when present 'normals',
+  'colors', 'texture_uv' (V x 2), 'texture_uv_face' (F x 6), 'texture_file'};
+  arrays are float64 as in the reference (inout.py:472-500). Non-triangular
+  faces: ValueError('Only triangular faces are supported.'); a texcoord list
+  not of 6 values: ValueError('Wrong number of UV face coordinates.')."""
   with open(path, "rb") as f:
-    fmt, elements = _read_header(f)
+    fmt, elements, texture_file = _read_header(f)
     body = f.read()
+  data = {}
   if fmt == "ascii":
-    return _load_ascii(body.decode("ascii").split("\n"), elements)
-  if fmt != "binary_little_endian":
+    lines = body.decode("utf8").splitlines()
+    pos = 0
+    for el in elements:
+      data[el["name"]], pos = _ascii_element(lines, pos, el)
+  elif fmt == "binary_little_endian":
+    off = 0
+    for el in elements:
+      data[el["name"]], off = _binary_element(body, off, el)
+  else:
     raise ValueError("unsupported PLY format %r" % fmt)
-  off, pts, faces = 0, None, None
-  for el in elements:
-    n = el["count"]
-    if all(p[1] == "scalar" for p in el["props"]):
-      dt = np.dtype([(p[0], "<" + p[2]) for p in el["props"]])
-      arr = np.frombuffer(body, dt, count=n, offset=off)
-      off += n * dt.itemsize
-      if el["name"] == "vertex":
-        pts = np.stack([arr["x"], arr["y"], arr["z"]], 1).astype(np.float64)
-    elif el["name"] == "face" and len(el["props"]) == 1:
-      _, _, ct, it = el["props"][0]
-      cdt, idt = np.dtype("<" + ct), np.dtype("<" + it)
-      first = int(np.frombuffer(body, cdt, count=1, offset=off)[0]) if n else 3
-      dt = np.dtype([("n", cdt), ("i", idt, (first,))])
-      arr = np.frombuffer(body, dt, count=n, offset=off)
-      if n and not np.all(arr["n"] == first):
-        raise ValueError("mixed polygon sizes are not supported")
-      if first != 3 and n:
-        raise ValueError("only triangle meshes are supported")
-      faces = arr["i"].astype(np.int64)
-      off += n * dt.itemsize
-    else:
-      raise ValueError("unsupported PLY element layout %r" % el["name"])
-  return {"pts": pts, "faces": faces if faces is not None else np.zeros((0, 3), np.int64)}
 
+  model = {}
+  if texture_file is not None:
+    model["texture_file"] = texture_file
+  v = data.get("vertex")
+  names = set(v.dtype.names if isinstance(v, np.ndarray) else (v or {}))
+  col = lambda k: np.asarray(v[k], np.float64)
+  n_pts = len(col("x")) if v is not None and "x" in names else 0
+  model["pts"] = (np.stack([col("x"), col("y"), col("z")], 1) if n_pts
+                  else np.zeros((0, 3), np.float64))
+  if {"nx", "ny", "nz"} <= names:
+    model["normals"] = np.stack([col("nx"), col("ny"), col("nz")], 1)
+  if {"red", "green", "blue"} <= names:
+    model["colors"] = np.stack([col("red"), col("green"), col("blue")], 1)
+  if {"texture_u", "texture_v"} <= names:
+    model["texture_uv"] = np.stack([col("texture_u"), col("texture_v")], 1)
 
-def _load_ascii(lines, elements):
-  pos, pts, faces = 0, None, None
-  for el in elements:
-    rows = [l.split() for l in lines[pos:pos + el["count"]]]
-    pos += el["count"]
-    if el["name"] == "vertex":
-      names = [p[0] for p in el["props"]]
-      a = np.array(rows, np.float64)
-      pts = a[:, [names.index("x"), names.index("y"), names.index("z")]]
-    elif el["name"] == "face":
-      faces = np.array([[int(v) for v in r[1:4]] for r in rows], np.int64).reshape(-1, 3)
-  return {"pts": pts, "faces": faces if faces is not None else np.zeros((0, 3), np.int64)}
+  fc = data.get("face")
+  n_faces = next((el["count"] for el in elements if el["name"] == "face"), 0)
+  if fc is not None and n_faces > 0:
+    fnames = set(fc.dtype.names if isinstance(fc, np.ndarray) else fc)
+    key = "vertex_indices" if "vertex_indices" in fnames else "vertex_index"
+    if key not in fnames or np.any(np.asarray(fc["n_" + key]) != _FACE_CORNERS):
+      raise ValueError("Only triangular faces are supported.")
+    model["faces"] = np.asarray(fc[key], np.float64).reshape(n_faces, _FACE_CORNERS)
+    if "texcoord" in fnames:
+      if np.any(np.asarray(fc["n_texcoord"]) != 2 * _FACE_CORNERS):
+        raise ValueError("Wrong number of UV face coordinates.")
+      model["texture_uv_face"] = np.asarray(fc["texcoord"], np.float64).reshape(n_faces, 6)
+  return model
 
 
 def save_ply(path, pts, faces):

@@ -35,7 +35,7 @@ class RendererHIP(Renderer):
   def add_object(self, obj_id, model_path, **kwargs):
     """Load a PLY model (inout.load_ply) and upload it (renderer.py:47-53)."""
     model = inout.load_ply(model_path)
-    self.add_object_arrays(obj_id, model["pts"], model["faces"])
+    self.add_object_arrays(obj_id, model["pts"], model.get("faces"))
 
   def add_object_arrays(self, obj_id, pts, faces):
     """Register an in-memory mesh: pts V x 3, faces F x 3."""
