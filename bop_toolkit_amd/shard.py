@@ -75,10 +75,13 @@ def gather_rows(rows, ids, n_total, group=None, counts=None):
   block[:rows.shape[0], 0] = ids.to(torch.float64)
   block[:rows.shape[0], 1:] = rows
   out = torch.empty((world * pad, width), dtype=torch.float64, device=dev)
-  if dev.type == "cuda":  # RCCL: one contiguous all-gather
+  if dev.type == "cuda" and dist.get_backend(group) == "nccl":  # RCCL: one contiguous all-gather
     dist.all_gather_into_tensor(out, block, group=group)
-  else:  # gloo
-    dist.all_gather(list(out.view(world, pad, width).unbind(0)), block, group=group)
+  else:  # gloo (host collectives; device rows are staged through host memory)
+    host = out.cpu() if dev.type == "cuda" else out
+    dist.all_gather(list(host.view(world, pad, width).unbind(0)), block.cpu(), group=group)
+    if host is not out:
+      out.copy_(host)
   if rank != 0:
     return None
   if pad * world != sum(counts):  # drop the padding rows
@@ -104,7 +107,15 @@ def init_from_env():
     return 0, 1, local
   import torch
   import torch.distributed as dist
+  # BOPX_DIST_BACKEND=gloo: host collectives, ranks may share a GPU (rehearsal
+  # of the multi-rank flow on a one-GPU machine); default RCCL, one GPU per rank.
+  backend = os.environ.get("BOPX_DIST_BACKEND", "nccl")
+  if backend == "gloo":
+    local %= max(1, torch.cuda.device_count())
   torch.cuda.set_device(local)
   if not dist.is_initialized():
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if backend == "nccl":
+      dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+      dist.init_process_group(backend)
   return dist.get_rank(), world, local
