@@ -78,6 +78,7 @@ struct VsdArgs {
   int img_w, img_h;  // test-depth frame size (= width/height except GT-info mode)
   int ox, oy;        // image origin inside the raster canvas (GT-info mode)
   uint8_t* masks;    // GT-info mode, optional: n x 2 x img_h x img_w (mask, mask_visib)
+  const int32_t* order;  // optional launch order (launch_order_by_slot): block k takes tuple order[k]
   int ablate;  // BOPX_VSD_ABLATE, read only by -DBOPX_VSD_DIAG=1 builds (kern_vsd.hip)
   double taus[kMaxTaus];
 };
@@ -86,13 +87,17 @@ struct VsdArgs {
 // the launch; inputs are device pointers.
 hipError_t launch_sym_error(int mode, const ObjDesc* objs, int max_ns, int64_t n,
                             const int32_t* slots, const double* pe, const double* pg,
-                            const double* K, double* out,
+                            const double* K, double* out, const int32_t* order,
                             hipStream_t s);  // mode 0 = MSSD, 1 = MSPD; max_ns over objects
 hipError_t launch_mean_error(int mode, const ObjDesc* objs, int64_t n, const int32_t* slots,
                              const double* pe, const double* pg, const double* K, double* out,
-                             hipStream_t s);  // mode 0 = ADD, 1 = PROJ
+                             const int32_t* order, hipStream_t s);  // mode 0 = ADD, 1 = PROJ
 hipError_t launch_adi(const ObjDesc* objs, int64_t n, const int32_t* slots, const double* pe,
-                      const double* pg, double* out, hipStream_t s);
+                      const double* pg, double* out, const int32_t* order, hipStream_t s);
+// order: nullptr (block k takes tuple k) or a launch order from launch_order_by_slot
+constexpr int kOrderMaxSlots = 16383;  // LDS buckets of k_order_by_slot
+hipError_t launch_order_by_slot(const int32_t* slots, int64_t n, int ns, int32_t* order,
+                                hipStream_t s);
 hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s);  // or kCostCover
 hipError_t launch_cover_depths(int W, int H, const float* de, const float* dg,
                                long long* acc /* kCoverCols, device */, hipStream_t s);

@@ -104,12 +104,13 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
                                                             const double* __restrict__ pe,
                                                             const double* __restrict__ pg,
                                                             const double* __restrict__ Km,
-                                                            double* __restrict__ out, int nch) {
+                                                            double* __restrict__ out, int nch,
+                                                            const int32_t* __restrict__ order) {
   __shared__ double s_red[kPoseThreads];
   // A block of kSymStage vertices staged for every symmetry of the unit: x, y, z
   // and, for MSPD, the estimate's projection u_e, v_e.
   __shared__ double s_v[MODE ? 5 : 3][kSymStage<MODE>];
-  const int64_t b = blockIdx.x / nch;
+  const int64_t b = order ? (int64_t)order[blockIdx.x / nch] : (int64_t)(blockIdx.x / nch);
   const int c = blockIdx.x % nch;
   const int tid = threadIdx.x;
   const ObjDesc o = objs[slots[b]];
@@ -229,9 +230,10 @@ __global__ __launch_bounds__(kPoseThreads) void k_mean_error(const ObjDesc* __re
                                                              const double* __restrict__ pe,
                                                              const double* __restrict__ pg,
                                                              const double* __restrict__ Km,
-                                                             double* __restrict__ out) {
+                                                             double* __restrict__ out,
+                                                             const int32_t* __restrict__ order) {
   __shared__ double s_part[kPoseThreads / 64];
-  const int64_t b = blockIdx.x;
+  const int64_t b = order ? (int64_t)order[blockIdx.x] : (int64_t)blockIdx.x;
   const int tid = threadIdx.x;
   const ObjDesc o = objs[slots[b]];
   const int nv = o.nv;
@@ -293,10 +295,11 @@ __global__ __launch_bounds__(kPoseThreads) void k_adi(const ObjDesc* __restrict_
                                                       const int32_t* __restrict__ slots,
                                                       const double* __restrict__ pe,
                                                       const double* __restrict__ pg,
-                                                      double* __restrict__ out) {
+                                                      double* __restrict__ out,
+                                                      const int32_t* __restrict__ order) {
   __shared__ double s_e[3][kAdiTile];
   __shared__ double s_part[kPoseThreads / 64];
-  const int64_t b = blockIdx.x;
+  const int64_t b = order ? (int64_t)order[blockIdx.x] : (int64_t)blockIdx.x;
   const int tid = threadIdx.x;
   const ObjDesc o = objs[slots[b]];
   const int nv = o.nv;
@@ -374,7 +377,8 @@ __global__ __launch_bounds__(kPoseThreads) void k_adi(const ObjDesc* __restrict_
 
 hipError_t launch_sym_error(int mode, const ObjDesc* objs, int max_ns, int64_t n,
                             const int32_t* slots, const double* pe, const double* pg,
-                            const double* K, double* out, hipStream_t s) {
+                            const double* K, double* out, const int32_t* order,
+                            hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const int nch = (max(max_ns, 1) + kSymChunk - 1) / kSymChunk;
   if ((int64_t)nch * n > 0x7FFFFFFF) return hipErrorInvalidValue;
@@ -382,30 +386,91 @@ hipError_t launch_sym_error(int mode, const ObjDesc* objs, int max_ns, int64_t n
   hipLaunchKernelGGL(k_sym_init, gfix, bfix, 0, s, out, n);
   dim3 grid((unsigned)(n * nch)), block(kPoseThreads);
   if (mode == 0)
-    hipLaunchKernelGGL(k_sym_error<0>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch);
+    hipLaunchKernelGGL(k_sym_error<0>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch,
+                       order);
   else
-    hipLaunchKernelGGL(k_sym_error<1>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch);
+    hipLaunchKernelGGL(k_sym_error<1>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch,
+                       order);
   hipLaunchKernelGGL(k_sym_finish, gfix, bfix, 0, s, out, n);
   return hipGetLastError();
 }
 
 hipError_t launch_mean_error(int mode, const ObjDesc* objs, int64_t n, const int32_t* slots,
                              const double* pe, const double* pg, const double* K, double* out,
-                             hipStream_t s) {
+                             const int32_t* order, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   dim3 grid((unsigned)n), block(kPoseThreads);
   if (mode == 0)
-    hipLaunchKernelGGL(k_mean_error<0>, grid, block, 0, s, objs, slots, pe, pg, K, out);
+    hipLaunchKernelGGL(k_mean_error<0>, grid, block, 0, s, objs, slots, pe, pg, K, out, order);
   else
-    hipLaunchKernelGGL(k_mean_error<1>, grid, block, 0, s, objs, slots, pe, pg, K, out);
+    hipLaunchKernelGGL(k_mean_error<1>, grid, block, 0, s, objs, slots, pe, pg, K, out, order);
   return hipGetLastError();
 }
 
 hipError_t launch_adi(const ObjDesc* objs, int64_t n, const int32_t* slots, const double* pe,
-                      const double* pg, double* out, hipStream_t s) {
+                      const double* pg, double* out, const int32_t* order, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_adi, dim3((unsigned)n), dim3(kPoseThreads), 0, s, objs, slots, pe, pg,
-                     out);
+                     out, order);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Object-grouped launch order: order[k] = the tuple the k-th workgroup takes,
+// tuples grouped by slot (counting sort, one workgroup; slots outside [0, ns)
+// go last). Workgroups are dispatched in blockIdx order, so the resident ones
+// then work on one or two objects at a time and re-read the same meshlet and
+// vertex blocks from L2 instead of streaming every object's through it. The
+// order within an object is whatever the atomics give: every tuple writes only
+// its own outputs, so results do not depend on it.
+constexpr int kOrderThreads = 1024;
+
+__global__ __launch_bounds__(kOrderThreads) void k_order_by_slot(const int32_t* __restrict__ slots,
+                                                                  int64_t n, int ns,
+                                                                  int32_t* __restrict__ order) {
+  extern __shared__ int s_cnt[];  // ns + 1 buckets
+  __shared__ int s_wsum[kOrderThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nb = ns + 1;
+  for (int i = tid; i < nb; i += kOrderThreads) s_cnt[i] = 0;
+  __syncthreads();
+  for (int64_t i = tid; i < n; i += kOrderThreads) {
+    const int sl = slots[i];
+    atomicAdd(&s_cnt[(unsigned)sl < (unsigned)ns ? sl : ns], 1);
+  }
+  __syncthreads();
+  // exclusive scan: thread t owns buckets [t * per, (t + 1) * per)
+  const int per = (nb + kOrderThreads - 1) / kOrderThreads;
+  const int lo = min(tid * per, nb), hi = min(lo + per, nb);
+  int sum = 0;
+  for (int i = lo; i < hi; ++i) sum += s_cnt[i];
+  int inc = sum;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += v;
+  }
+  if (lane == 63) s_wsum[wave] = inc;
+  __syncthreads();
+  int run = inc - sum;
+  for (int w = 0; w < wave; ++w) run += s_wsum[w];
+  for (int i = lo; i < hi; ++i) {
+    const int v = s_cnt[i];
+    s_cnt[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  for (int64_t i = tid; i < n; i += kOrderThreads) {
+    const int sl = slots[i];
+    order[atomicAdd(&s_cnt[(unsigned)sl < (unsigned)ns ? sl : ns], 1)] = (int32_t)i;
+  }
+}
+
+hipError_t launch_order_by_slot(const int32_t* slots, int64_t n, int ns, int32_t* order,
+                                hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (ns < 0 || ns > kOrderMaxSlots) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_order_by_slot, dim3(1), dim3(kOrderThreads), (ns + 1) * sizeof(int), s,
+                     slots, n, ns, order);
   return hipGetLastError();
 }
 

@@ -190,7 +190,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   uint32_t(*s_cnt)[2 + kMaxTaus] = reinterpret_cast<uint32_t(*)[2 + kMaxTaus]>(&s_dep[0][0]);
   double(*s_lin)[kMaxTaus] = reinterpret_cast<double(*)[kMaxTaus]>(&s_dep[1][0]);
 
-  const int64_t b = blockIdx.x;
+  const int64_t b = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned long long ph[16] = {}, t_prev = 0;
   if (VSD_DIAG(8)) t_prev = __builtin_amdgcn_s_memtime();

@@ -122,6 +122,35 @@ static size_t carve_size(std::initializer_list<size_t> bytes) {
   return s + 256;
 }
 
+// Object-grouped launch order of a batch (bopx::launch_order_by_slot) in
+// stream-ordered memory, freed behind the launches that read it. Batches below
+// kOrderMinTuples and BOPX_LAUNCH_ORDER=0 keep the identity order (nullptr).
+struct LaunchOrder {
+  int32_t* p = nullptr;
+  hipStream_t s = nullptr;
+  LaunchOrder() = default;
+  LaunchOrder(const LaunchOrder&) = delete;
+  LaunchOrder& operator=(const LaunchOrder&) = delete;
+  ~LaunchOrder() {
+    if (p) (void)hipFreeAsync(p, s);
+  }
+};
+constexpr int64_t kOrderMinTuples = 1024;
+
+int make_order(bopx_ctx* c, int64_t n, const int32_t* slots, hipStream_t s, LaunchOrder& o) {
+  static const bool on = [] {
+    const char* e = getenv("BOPX_LAUNCH_ORDER");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || n < kOrderMinTuples || n > INT32_MAX ||
+      (int64_t)c->objs.size() > bopx::kOrderMaxSlots)
+    return BOPX_OK;
+  HIPCHK(c, hipMallocAsync((void**)&o.p, (size_t)n * sizeof(int32_t), s));
+  o.s = s;
+  HIPCHK(c, bopx::launch_order_by_slot(slots, n, (int)c->objs.size(), o.p, s));
+  return BOPX_OK;
+}
+
 int sync_desc(bopx_ctx* c) {
   std::vector<ObjDesc> h(c->objs.size());
   int max_nf = 0, max_ns = 0, max_nm = 0;
@@ -542,13 +571,17 @@ static int point_batch(bopx_ctx* c, int kind, int64_t n, const int32_t* obj_ids,
   HIPCHK(c, hipMemcpyAsync(d_pe, pe, 96 * n, hipMemcpyHostToDevice, s));
   HIPCHK(c, hipMemcpyAsync(d_pg, pg, 96 * n, hipMemcpyHostToDevice, s));
   if (needK) HIPCHK(c, hipMemcpyAsync(d_K, K, 72 * n, hipMemcpyHostToDevice, s));
+  LaunchOrder ord;
+  if (int r = make_order(c, n, d_s, s, ord)) return r;
   hipError_t e;
   if (kind <= 1)
-    e = bopx::launch_sym_error(kind, c->d_desc, c->max_ns, n, d_s, d_pe, d_pg, d_K, d_out, s);
+    e = bopx::launch_sym_error(kind, c->d_desc, c->max_ns, n, d_s, d_pe, d_pg, d_K, d_out, ord.p,
+                               s);
   else if (kind == 3)
-    e = bopx::launch_adi(c->d_desc, n, d_s, d_pe, d_pg, d_out, s);
+    e = bopx::launch_adi(c->d_desc, n, d_s, d_pe, d_pg, d_out, ord.p, s);
   else
-    e = bopx::launch_mean_error(kind == 2 ? 0 : 1, c->d_desc, n, d_s, d_pe, d_pg, d_K, d_out, s);
+    e = bopx::launch_mean_error(kind == 2 ? 0 : 1, c->d_desc, n, d_s, d_pe, d_pg, d_K, d_out,
+                                ord.p, s);
   HIPCHK(c, e);
   HIPCHK(c, hipMemcpyAsync(out, d_out, 8 * n, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
@@ -580,30 +613,41 @@ int bopx_mssd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doub
                         const double* pg, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
   if (int r = set_dev(c)) return r;
-  HIPCHK(c, bopx::launch_sym_error(0, c->d_desc, c->max_ns, n, slots, pe, pg, nullptr, out,
-                                   pick_stream(c, stream)));
+  hipStream_t s = pick_stream(c, stream);
+  LaunchOrder ord;
+  if (int r = make_order(c, n, slots, s, ord)) return r;
+  HIPCHK(c, bopx::launch_sym_error(0, c->d_desc, c->max_ns, n, slots, pe, pg, nullptr, out, ord.p,
+                                   s));
   return BOPX_OK;
 }
 int bopx_mspd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
                         const double* pg, const double* K, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
   if (int r = set_dev(c)) return r;
-  HIPCHK(c, bopx::launch_sym_error(1, c->d_desc, c->max_ns, n, slots, pe, pg, K, out, pick_stream(c, stream)));
+  hipStream_t s = pick_stream(c, stream);
+  LaunchOrder ord;
+  if (int r = make_order(c, n, slots, s, ord)) return r;
+  HIPCHK(c, bopx::launch_sym_error(1, c->d_desc, c->max_ns, n, slots, pe, pg, K, out, ord.p, s));
   return BOPX_OK;
 }
 int bopx_add_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
                        const double* pg, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
   if (int r = set_dev(c)) return r;
-  HIPCHK(c, bopx::launch_mean_error(0, c->d_desc, n, slots, pe, pg, nullptr, out,
-                                    pick_stream(c, stream)));
+  hipStream_t s = pick_stream(c, stream);
+  LaunchOrder ord;
+  if (int r = make_order(c, n, slots, s, ord)) return r;
+  HIPCHK(c, bopx::launch_mean_error(0, c->d_desc, n, slots, pe, pg, nullptr, out, ord.p, s));
   return BOPX_OK;
 }
 int bopx_adi_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
                        const double* pg, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
   if (int r = set_dev(c)) return r;
-  HIPCHK(c, bopx::launch_adi(c->d_desc, n, slots, pe, pg, out, pick_stream(c, stream)));
+  hipStream_t s = pick_stream(c, stream);
+  LaunchOrder ord;
+  if (int r = make_order(c, n, slots, s, ord)) return r;
+  HIPCHK(c, bopx::launch_adi(c->d_desc, n, slots, pe, pg, out, ord.p, s));
   return BOPX_OK;
 }
 
@@ -611,8 +655,10 @@ int bopx_proj_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doub
                         const double* pg, const double* K, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
   if (int r = set_dev(c)) return r;
-  HIPCHK(c, bopx::launch_mean_error(1, c->d_desc, n, slots, pe, pg, K, out,
-                                    pick_stream(c, stream)));
+  hipStream_t s = pick_stream(c, stream);
+  LaunchOrder ord;
+  if (int r = make_order(c, n, slots, s, ord)) return r;
+  HIPCHK(c, bopx::launch_mean_error(1, c->d_desc, n, slots, pe, pg, K, out, ord.p, s));
   return BOPX_OK;
 }
 
@@ -667,7 +713,13 @@ int bopx_vsd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doubl
   a.diameters = diameters;
   a.out = out;
   a.n = n;
-  HIPCHK(c, bopx::launch_vsd(a, cost_type, pick_stream(c, stream)));
+  {
+    const hipStream_t so = pick_stream(c, stream);
+    LaunchOrder ord;
+    if (int r = make_order(c, a.n, a.slots, so, ord)) return r;
+    a.order = ord.p;
+    HIPCHK(c, bopx::launch_vsd(a, cost_type, so));
+  }
   return BOPX_OK;
 }
 
@@ -725,7 +777,13 @@ int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double*
   a.diameters = d_dia;
   a.out = d_out;
   a.n = n;
-  HIPCHK(c, bopx::launch_vsd(a, cost_type, s));
+  {
+    const hipStream_t so = s;
+    LaunchOrder ord;
+    if (int r = make_order(c, a.n, a.slots, so, ord)) return r;
+    a.order = ord.p;
+    HIPCHK(c, bopx::launch_vsd(a, cost_type, so));
+  }
   HIPCHK(c, hipMemcpyAsync(out, d_out, 8 * (size_t)n * n_tau, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
   return BOPX_OK;
@@ -785,7 +843,13 @@ int bopx_gt_info_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const d
   a.out = out;
   a.masks = masks;
   a.n = n;
-  HIPCHK(c, bopx::launch_vsd(a, bopx::kCostGtInfo, s));
+  {
+    const hipStream_t so = s;
+    LaunchOrder ord;
+    if (int r = make_order(c, a.n, a.slots, so, ord)) return r;
+    a.order = ord.p;
+    HIPCHK(c, bopx::launch_vsd(a, bopx::kCostGtInfo, so));
+  }
   return BOPX_OK;
 }
 
@@ -839,7 +903,13 @@ int bopx_gt_info_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const dou
   a.out = d_out;
   a.masks = d_m;
   a.n = n;
-  HIPCHK(c, bopx::launch_vsd(a, bopx::kCostGtInfo, s));
+  {
+    const hipStream_t so = s;
+    LaunchOrder ord;
+    if (int r = make_order(c, a.n, a.slots, so, ord)) return r;
+    a.order = ord.p;
+    HIPCHK(c, bopx::launch_vsd(a, bopx::kCostGtInfo, so));
+  }
   HIPCHK(c, hipMemcpyAsync(out, d_out, 8 * cols * n, hipMemcpyDeviceToHost, s));
   if (d_m) HIPCHK(c, hipMemcpyAsync(masks, d_m, mbytes, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
@@ -862,7 +932,13 @@ int bopx_cover_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const dou
   a.cam = cam;
   a.out = out;
   a.n = n;
-  HIPCHK(c, bopx::launch_vsd(a, bopx::kCostCover, pick_stream(c, stream)));
+  {
+    const hipStream_t so = pick_stream(c, stream);
+    LaunchOrder ord;
+    if (int r = make_order(c, a.n, a.slots, so, ord)) return r;
+    a.order = ord.p;
+    HIPCHK(c, bopx::launch_vsd(a, bopx::kCostCover, so));
+  }
   return BOPX_OK;
 }
 
@@ -910,7 +986,13 @@ int bopx_cover_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const doubl
   a.cam = d_cam;
   a.out = d_out;
   a.n = n;
-  HIPCHK(c, bopx::launch_vsd(a, bopx::kCostCover, s));
+  {
+    const hipStream_t so = s;
+    LaunchOrder ord;
+    if (int r = make_order(c, a.n, a.slots, so, ord)) return r;
+    a.order = ord.p;
+    HIPCHK(c, bopx::launch_vsd(a, bopx::kCostCover, so));
+  }
   HIPCHK(c, hipMemcpyAsync(out, d_out, 8 * cols * n, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
   return BOPX_OK;

@@ -389,3 +389,63 @@ def test_fused_vsd_bit_exact_large_images(oracle_mod):
   K_hope = np.array([[1390.0, 0.0, 960.0], [0.0, 1390.0, 540.0], [0.0, 0.0, 1.0]])
   _fused_vs_oracle(oracle_mod, 17, 4, 1280, 960, K_itodd, 30, 60, delta=5.0)
   _fused_vs_oracle(oracle_mod, 18, 4, 1920, 1080, K_hope, 30, 60)
+
+
+def test_launch_order_large_batch(oracle_mod):
+  """Batches of >= 1024 tuples run in the object-grouped launch order
+  (k_order_by_slot); the same tuples in chunks of 512 keep the identity order.
+  Every error type must give identical bits both ways, and match the oracle."""
+  import torch
+  from bop_toolkit_amd import misc, synth
+  from bop_toolkit_amd.batch import BatchEvaluator
+  rng = np.random.default_rng(31)
+  ev = BatchEvaluator(0)
+  objs = []
+  for o, (nd, cont) in enumerate([(1, False), (4, False), (8, False), (1, True)]):
+    pts, faces = synth.superellipsoid(12, 24, (30.0 + 5 * o, 40.0, 50.0 - 5 * o), 0.6 + 0.1 * o)
+    info = synth.models_info_entry(pts, nd, cont)
+    syms = misc.get_symmetry_transformations(info, 0.01)
+    ev.add_object(o, pts, faces, syms, info["diameter"])
+    objs.append({"pts": pts, "faces": faces, "syms": misc.symmetries_to_array(syms),
+                 "diameter": info["diameter"]})
+  n, per, W, H = 1536, 16, 640, 480
+  n_img = n // per
+  K = synth.LMO_K
+  obj = rng.integers(0, 4, n).astype(np.int32)
+  Rg, tg = synth.gt_poses(rng, n)
+  Re, te_ = synth.perturb(rng, Rg, tg)
+  dev = ev.device
+  t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+  pe = t(np.concatenate([Re.reshape(n, 9), te_], 1), torch.float64)
+  pg = t(np.concatenate([Rg.reshape(n, 9), tg], 1), torch.float64)
+  cam = t(np.tile([K[0, 0], K[1, 1], K[0, 2], K[1, 2]], (n_img, 1)), torch.float64)
+  fi = t(np.repeat(np.arange(n_img), per), torch.int32)
+  slots = ev.slots(obj)
+  frames = ev.render(slots, pg, fi, cam, n_img, W, H)
+  frames = torch.round(torch.where(frames > 0, frames, torch.full_like(frames, 1500.0)))
+  Kt = t(np.tile(K.reshape(9), (n, 1)), torch.float64)
+  dia = t([objs[o]["diameter"] for o in obj], torch.float64)
+  taus = np.arange(0.05, 0.51, 0.05)
+
+  def run(lo, hi):
+    s = slice(lo, hi)
+    r = ev.bop19(slots[s], pe[s], pg[s], Kt[s], fi[s], frames, cam, 15.0, taus, dia[s])
+    r["add"] = ev.add(slots[s], pe[s], pg[s])
+    r["adi"] = ev.adi(slots[s], pe[s], pg[s])
+    r["proj"] = ev.proj(slots[s], pe[s], pg[s], Kt[s])
+    r["cover"] = ev.cover(slots[s], pe[s], pg[s], fi[s], cam, W, H)
+    r["gt_info"] = ev.gt_info(slots[s], pg[s], fi[s], frames, cam, 15.0)[0]
+    return {k: v.cpu().numpy() for k, v in r.items()}
+
+  full = run(0, n)
+  parts = [run(lo, lo + 512) for lo in range(0, n, 512)]
+  for k in full:
+    assert np.array_equal(full[k], np.concatenate([p[k] for p in parts])), k
+  sub = np.arange(0, n, 24)
+  fr = frames.cpu().numpy()
+  ref_vsd, ref_mssd, ref_mspd = oracle_mod.bop19_batch(
+      objs, obj[sub], pe.cpu().numpy()[sub], pg.cpu().numpy()[sub], fi.cpu().numpy()[sub], fr,
+      cam.cpu().numpy(), 15.0, taus, dia.cpu().numpy()[sub])
+  assert np.array_equal(full["vsd"][sub], ref_vsd)
+  np.testing.assert_allclose(full["mssd"][sub], ref_mssd, rtol=0, atol=TOL)
+  np.testing.assert_allclose(full["mspd"][sub], ref_mspd, rtol=0, atol=TOL)
