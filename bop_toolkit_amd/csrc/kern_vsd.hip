@@ -114,7 +114,7 @@ __device__ __forceinline__ short4 meshlet_rect(gptr<const float> mb, const float
     if (!(Z > 0.0f)) {
       full = true;
     } else {
-      const float iz = 1.0f / Z;
+      const float iz = rcp_rn(Z);
       const float u = (c.fx * X) * iz + c.cx, v = (c.fy * Y) * iz + c.cy;
       umin = fminf(umin, u);
       umax = fmaxf(umax, u);
@@ -159,11 +159,22 @@ constexpr int kVsdWaves = kVsdThreads / 64;
 #define BOPX_VSD_GROUP 2
 #endif
 constexpr int kRowWin = 256;  // row items numbered per window (LDS owner map)
-constexpr int kPixPerWave = kTileW * kTileH / kVsdThreads * 64;  // covered-pixel list
-static_assert(sizeof(RRow) * 64 * kVsdWaves >= 2 * kPixPerWave * kVsdWaves,
-              "pixel lists overlay the raster records");
+// covered-pixel list of a wave: its rows w, w + kVsdWaves, ... of the tile
+constexpr int kPixPerWave = (kTileH + kVsdWaves - 1) / kVsdWaves * kTileW;
+static_assert(sizeof(RRow) * 64 >= 2 * kPixPerWave, "pixel lists overlay the raster records");
+static_assert(kVsdThreads % kTileW == 0, "pixel-pass rows are wave-uniform");
 constexpr int kGroup = BOPX_VSD_GROUP;  // (pose, meshlet) entries staged together per wave step
-constexpr int kRectsPerThread = 2 * kMaxMeshlets / kVsdThreads;  // worst case (RPT)
+// worst case (RPT) of meshlet rectangles per thread
+constexpr int kRectsPerThread = (2 * kMaxMeshlets + kVsdThreads - 1) / kVsdThreads;
+// Wave-private scratch: the staged vertex blocks and compacted triangle refs of
+// an entry group during the raster, the tile's float64 column / row
+// coefficients during the pixel pass.
+constexpr int kStageBytes = kGroup * kMeshletVerts * (int)sizeof(RVtx) + kGroup * kMeshletTris * 4;
+constexpr int kCoefBytes = 8 * (kTileW + kTileH);
+constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
+#ifndef BOPX_VSD_TOUCH
+#define BOPX_VSD_TOUCH 1
+#endif
 
 // COST: 0 = step, 1 = tlinear, kCostCover = silhouette overlap, kCostGtInfo = GT stats.
 // RPT: meshlet rectangles held per thread (1, 2 or 4): the launch picks the
@@ -175,14 +186,11 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   // q = 1/Z bits, 0 = empty; rows padded by one dword so lanes that walk the
   // same column on consecutive rows (row-split) hit different LDS banks.
   __shared__ uint32_t s_dep[2][kTileStride * kTileH];
-  // per wave: staged vertex blocks of one entry group, compacted triangle refs
-  __shared__ RVtx s_stage[kVsdWaves][kGroup * kMeshletVerts];
-  __shared__ uint32_t s_tri[kVsdWaves][kGroup * kMeshletTris];
+  __shared__ __attribute__((aligned(16))) uint8_t s_wscr[kVsdWaves][kWaveScr];
   __shared__ RRow s_rec[kVsdWaves][64];          // set-up triangles of the current chunk
   __shared__ uint8_t s_own[kVsdWaves][kRowWin];  // row item -> record (lane) of a window
   __shared__ uint16_t s_list[2 * kMaxMeshlets];
   __shared__ int s_next;
-  __shared__ double s_pX[kTileW], s_pY[kTileH];
   __shared__ float s_pose[2][12];
   __shared__ int s_roi[4];
   __shared__ int s_nlist;
@@ -192,6 +200,11 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
 
   const int64_t b = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  RVtx* const w_stage = reinterpret_cast<RVtx*>(&s_wscr[wave][0]);
+  uint32_t* const w_tri =
+      reinterpret_cast<uint32_t*>(&s_wscr[wave][kGroup * kMeshletVerts * sizeof(RVtx)]);
+  double* const w_pX = reinterpret_cast<double*>(&s_wscr[wave][0]);
+  double* const w_pY = w_pX + kTileW;
   unsigned long long ph[16] = {}, t_prev = 0;
   if (VSD_DIAG(8)) t_prev = __builtin_amdgcn_s_memtime();
   const ObjDesc o = a.objs[a.slots[b]];
@@ -273,11 +286,6 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         s_nlist = 0;
         s_next = 0;
       }
-      // float64 distance coefficients of the tile's columns / rows (misc.py:137-138)
-      if (tid < kTileW) s_pX[tid] = ((double)(tx0 + tid - ox) - cx) / fx;
-      if (tid >= kVsdThreads - kTileH)
-        s_pY[tid - (kVsdThreads - kTileH)] =
-            ((double)(ty0 + tid - (kVsdThreads - kTileH) - oy) - cy) / fy;
       __syncthreads();
       VSD_STAMP(0);
 #pragma unroll
@@ -313,7 +321,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         }
 #pragma unroll
         for (int g = 0; g < kGroup; ++g)
-          s_stage[wave][g * kMeshletVerts + lane] = r_vertex(s_pose[pose[g]], c32, v[g].x, v[g].y,
+          w_stage[g * kMeshletVerts + lane] = r_vertex(s_pose[pose[g]], c32, v[g].x, v[g].y,
                                                              v[g].z);
         wave_lds_sync();
         VSD_STAMP(8);
@@ -322,13 +330,13 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         for (int g = 0; g < kGroup; ++g) {
           bool hit = false;
           if (pk[g] != 0xFFFFFFFFu) {
-            const RVtx* sg = &s_stage[wave][g * kMeshletVerts];
+            const RVtx* sg = &w_stage[g * kMeshletVerts];
             hit = r_touches(sg[pk[g] & 255u], sg[(pk[g] >> 8) & 255u], sg[(pk[g] >> 16) & 255u],
                             tx0, tx1, ty0, ty1);
           }
           const unsigned long long bal = __ballot(hit);
           if (hit)
-            s_tri[wave][cnt + __popcll(bal & ((1ull << lane) - 1ull))] =
+            w_tri[cnt + __popcll(bal & ((1ull << lane) - 1ull))] =
                 (pk[g] & 0xFFFFFFu) | ((uint32_t)g << 24) | ((uint32_t)pose[g] << 26);
           cnt += __popcll(bal);
         }
@@ -341,8 +349,8 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
           bool ok = false;
           int r = 0, cc0 = 0, cc1 = -1, rr0 = 0, rr1 = -1;
           if (c0 + lane < cnt) {
-            const uint32_t ref = s_tri[wave][c0 + lane];
-            const RVtx* sg = &s_stage[wave][((ref >> 24) & 3u) * kMeshletVerts];
+            const uint32_t ref = w_tri[c0 + lane];
+            const RVtx* sg = &w_stage[((ref >> 24) & 3u) * kMeshletVerts];
             r = (int)(ref >> 26);
             ok = r_setup(sg[ref & 255u], sg[(ref >> 8) & 255u], sg[(ref >> 16) & 255u], T, tx0,
                          tx1, ty0, ty1);
@@ -411,8 +419,28 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         }
         wave_lds_sync();  // the staging area is rewritten by the next group
       }
+      // Touch the test-depth lines of this wave's pixel rows (w, w + 8, ...)
+      // while it waits for the other waves at the raster-end barrier: the
+      // pixel pass then reads them from L2 instead of HBM. The empty asm below
+      // consumes the value (the only wait for these loads).
+      float touch = 0.0f;
+#if BOPX_VSD_TOUCH
+      if constexpr (COST == 0 || COST == 1) {
+        if (lane < 3 * (kTileH / kVsdWaves)) {
+          const int row = ty0 + wave + kVsdWaves * (lane / 3), k = lane % 3;
+          const int col = k == 0 ? tx0 : (k == 1 ? min(tx0 + 32, tx1) : tx1);
+          if (row <= ty1) touch = frame[(int64_t)row * IW + col];
+        }
+      }
+#endif
       VSD_STAMP(2);
       __syncthreads();
+      asm volatile("" ::"v"(touch));
+      // float64 distance coefficients of the tile's columns / rows (misc.py:137-138),
+      // per wave into its scratch (the staging area is dead until the next tile)
+      for (int i = lane; i < kTileW; i += 64) w_pX[i] = ((double)(tx0 + i - ox) - cx) / fx;
+      for (int i = lane; i < kTileH; i += 64) w_pY[i] = ((double)(ty0 + i - oy) - cy) / fy;
+      wave_lds_sync();
       VSD_STAMP(3);
       // 3. per-pixel distances, visibility masks, counters. Each wave first
       // compacts its covered pixels (rows wave, wave + 8, ...) into its own
@@ -463,8 +491,8 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
           bb[2] = max(bb[2], x);
           bb[3] = max(bb[3], y);
           if (x < 0 || y < 0 || x >= IW || y >= IH) continue;
-          const double pX = s_pX[p % kTileW], pY = s_pY[p / kTileW];
-          const double dist_g = dist_of(pX, pY, 1.0f / __uint_as_float(qg));
+          const double pX = w_pX[p % kTileW], pY = w_pY[p / kTileW];
+          const double dist_g = dist_of(pX, pY, rcp_rn(__uint_as_float(qg)));
           const double dist_t = dist_of(pX, pY, frame[(int64_t)y * IW + x]);
           c_valid += dist_t > 0.0;
           const bool vis = visib19(dist_t, dist_g, a.delta32, a.delta_f64, a.delta64);
@@ -481,11 +509,11 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
           }
           continue;
         }
-        const float de = qe ? 1.0f / __uint_as_float(qe) : 0.0f;
-        const float dg = qg ? 1.0f / __uint_as_float(qg) : 0.0f;
+        const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
+        const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
         const float dtest = frame[(int64_t)row * IW + col];
-        const double pX = s_pX[p % kTileW];
-        const double pY = s_pY[p / kTileW];
+        const double pX = w_pX[p % kTileW];
+        const double pY = w_pY[p / kTileW];
         const double dist_t = dist_of(pX, pY, dtest);
         const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
         const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
@@ -612,6 +640,12 @@ hipError_t read_vsd_stats(unsigned long long* out, int reset) {
 template <int RPT>
 static void launch_vsd_rpt(const VsdArgs& a, int cost_type, hipStream_t s) {
   dim3 grid((unsigned)a.n), block(kVsdThreads);
+#ifdef BOPX_VSD_PAD_LDS  // occupancy experiments: unused dynamic LDS per workgroup
+  if (cost_type == 0) {
+    hipLaunchKernelGGL((k_vsd<0, RPT>), grid, block, BOPX_VSD_PAD_LDS, s, a);
+    return;
+  }
+#endif
   if (cost_type == 0)
     hipLaunchKernelGGL((k_vsd<0, RPT>), grid, block, 0, s, a);
   else if (cost_type == 1)

@@ -24,6 +24,18 @@
 
 namespace bopx {
 
+// Correctly rounded 1/x, bit-identical to the IEEE 1.0f / x the spec names:
+// hardware reciprocal plus one fused Newton step. Checked against
+// (float)(1.0 / (double)x) for every float32 x with |x| and |1/x| normal
+// (tools/rcp_exhaustive.hip: 4,227,858,432 values, no mismatch); other inputs
+// take the IEEE division.
+__device__ __forceinline__ float rcp_rn(float x) {
+  const float ax = fabsf(x);
+  if (__builtin_expect(!(ax >= 0x1p-126f && ax < 0x1p126f), 0)) return 1.0f / x;
+  const float r = __builtin_amdgcn_rcpf(x);
+  return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+}
+
 struct Cam32 {
   float fx, fy, cx, cy;
 };
@@ -48,7 +60,7 @@ __device__ __forceinline__ RVtx r_vertex(const float* __restrict__ Rf, const Cam
   o.V = 0;
   o.iz = 0.0f;
   if (!(Z > 0.0f)) return o;
-  const float iz = 1.0f / Z;  // the one IEEE division per vertex (spec v4)
+  const float iz = rcp_rn(Z);  // the one IEEE division per vertex (spec v4)
   const float u = (c.fx * X) * iz + c.cx;
   const float v = (c.fy * Y) * iz + c.cy;
   if (!(fabsf(u) <= kGuardBand) || !(fabsf(v) <= kGuardBand)) return o;
@@ -109,7 +121,7 @@ __device__ __forceinline__ bool r_setup(RVtx a, RVtx b, RVtx c, RTri& t, int x0,
     b = c;
     c = tmp;
   }
-  const float inv_area = 1.0f / farea;
+  const float inv_area = rcp_rn(farea);
   const float dza = a.iz - c.iz, dzb = b.iz - c.iz;
   t.ga = ((float)(b.V - c.V) * dza + (float)(c.V - a.V) * dzb) * inv_area;
   t.gb = ((float)(c.U - b.U) * dza + (float)(a.U - c.U) * dzb) * inv_area;
