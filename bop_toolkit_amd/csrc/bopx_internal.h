@@ -72,6 +72,8 @@ struct VsdArgs {
   float delta32;
   int delta_f64;
   double delta64;
+  // float32 threshold equivalent to the visibility compare (visib_thr32 in runtime.cpp)
+  float dthr;
   int n_tau;
   int normalized;
   int max_nm;        // most meshlets of a registered object (sizes the rect registers)

@@ -32,6 +32,7 @@
 // (calc_gt_info / calc_gt_masks) that reuse steps 1-2 and replace step 3.
 // Results are bit-identical to the reference given identical depth maps.
 #include <algorithm>
+#include <cfloat>
 
 #include "raster.h"
 
@@ -96,6 +97,47 @@ __device__ __forceinline__ bool visib19(double dt, double dm, float delta32, int
   const float diff = (float)dm - (float)dt;
   const bool le = delta_f64 ? ((double)diff <= delta64) : (diff <= delta32);
   return (le || dt == 0.0) && dm > 0.0;
+}
+
+// visib19 with the float32 threshold VsdArgs::dthr (runtime.cpp visib_thr32):
+// (float)diff <= dthr is the same test for every float32 diff as the float32
+// or float64 comparison against delta that visib19 selects.
+__device__ __forceinline__ bool visib19t(double dt, double dm, float dthr) {
+  const float diff = (float)dm - (float)dt;
+  return ((diff <= dthr) || dt == 0.0) && dm > 0.0;
+}
+
+// Step cost of normalised distances (pose_error.py:66-68,80-81):
+// RN(dd / diameter) >= tau is monotone in dd >= 0 for a finite diameter > 0,
+// so it is dd >= T for the least double T that passes it. T is found once per
+// (tuple, tau) with the reference's own IEEE division: from the guess
+// tau * diameter (a few ulps off at most) by ulp steps, else by bisection over
+// the ordered bit patterns of the finite non-negative doubles.
+__device__ __forceinline__ double dbl_of(uint64_t b) { return __longlong_as_double((long long)b); }
+
+__device__ double step_threshold(double tau, double diam) {
+  constexpr uint64_t kMaxBits = 0x7FEFFFFFFFFFFFFFull;  // DBL_MAX
+  auto pass = [&](uint64_t b) { return dbl_of(b) / diam >= tau; };
+  const double x = tau * diam;
+  if (x >= 0.0 && x <= DBL_MAX) {
+    uint64_t b = (uint64_t)__double_as_longlong(x);
+    if (pass(b)) {
+      for (int i = 0; i < 4; ++i, --b)
+        if (b == 0 || !pass(b - 1)) return dbl_of(b);
+    } else {
+      for (int i = 0; i < 4 && b < kMaxBits; ++i)
+        if (pass(++b)) return dbl_of(b);
+    }
+  }
+  if (!pass(kMaxBits)) return INFINITY;  // no finite distance passes
+  if (pass(0)) return 0.0;
+  uint64_t lo = 0, hi = kMaxBits;  // pass(lo) false, pass(hi) true
+  while (hi - lo > 1) {
+    const uint64_t mid = lo + ((hi - lo) >> 1);
+    if (pass(mid)) hi = mid;
+    else lo = mid;
+  }
+  return dbl_of(hi);
 }
 
 // Conservative pixel rectangle of one meshlet bounding box (8 object-space
@@ -177,10 +219,11 @@ constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 #endif
 
 // COST: 0 = step, 1 = tlinear, kCostCover = silhouette overlap, kCostGtInfo = GT stats.
+// NT (step cost): thresholds compared per pixel (>= n_tau; 10 for the BOP taus).
 // RPT: meshlet rectangles held per thread (1, 2 or 4): the launch picks the
 // smallest that covers 2 x the most meshlets of any registered object, so
 // objects of up to 16k triangles keep 6 fewer VGPRs live through the tile loop.
-template <int COST, int RPT>
+template <int COST, int RPT, int NT>
 // Two workgroups per CU: 2 * kVsdThreads / 256 waves per SIMD (caps VGPRs at 128).
 __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdArgs a) {
   // q = 1/Z bits, 0 = empty; rows padded by one dword so lanes that walk the
@@ -194,6 +237,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   __shared__ float s_pose[2][12];
   __shared__ int s_roi[4];
   __shared__ int s_nlist;
+  __shared__ double s_thr[kMaxTaus];  // step-cost thresholds (T_k, +inf past n_tau)
   // Final per-wave partial counters reuse the depth tiles (after the tile loop).
   uint32_t(*s_cnt)[2 + kMaxTaus] = reinterpret_cast<uint32_t(*)[2 + kMaxTaus]>(&s_dep[0][0]);
   double(*s_lin)[kMaxTaus] = reinterpret_cast<double(*)[kMaxTaus]>(&s_dep[1][0]);
@@ -230,6 +274,21 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
     s_pose[0][tid] = (float)a.pose_est[12 * b + tid];
     s_pose[1][tid] = (float)a.pose_gt[12 * b + tid];
   }
+  const double diam = COST == 0 && a.normalized ? a.diameters[b] : 1.0;
+  // Step cost: per-pixel dd >= T_k. Normalised by a finite diameter > 0 with
+  // no NaN tau, T_k = step_threshold; otherwise T_k = tau_k and the pixel
+  // pass divides dd by the diameter itself (`divide`, pathological inputs).
+  bool divide = false;
+  if constexpr (COST == 0) {
+    bool fast = a.normalized && diam > 0.0 && diam <= DBL_MAX;
+    for (int k = 0; k < a.n_tau; ++k) fast = fast && a.taus[k] == a.taus[k];
+    divide = a.normalized && !fast;
+    if (tid < NT) {
+      double T = INFINITY;
+      if (tid < a.n_tau) T = fast ? step_threshold(a.taus[tid], diam) : a.taus[tid];
+      s_thr[tid] = T;
+    }
+  }
   if (tid == 0) {
     s_roi[0] = s_roi[1] = 0x7FFFFFFF;
     s_roi[2] = s_roi[3] = -1;
@@ -259,17 +318,24 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   for (int i = tid; i < 2 * kTileStride * kTileH; i += kVsdThreads) (&s_dep[0][0])[i] = 0u;
   __syncthreads();
   const int rx0 = s_roi[0], ry0 = s_roi[1], rx1 = s_roi[2], ry1 = s_roi[3];
+  double thr[NT];  // wave-uniform (SGPRs)
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    const double v = COST == 0 ? s_thr[k] : 0.0;
+    thr[k] = __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                              __builtin_amdgcn_readfirstlane(__double2loint(v)));
+  }
 
   uint32_t c_union = 0, c_inter = 0, c_valid = 0;
   // cover mode: est / gt silhouette bboxes (x0, y0, x1, y1), empty = (INT_MAX, INT_MAX, -1, -1)
   int bb[8] = {INT32_MAX, INT32_MAX, -1, -1, INT32_MAX, INT32_MAX, -1, -1};
   // step cost: two 16-bit per-tau counters per register (a lane evaluates at
   // most kTileW * kTileH / kVsdThreads pixels per tile, <= kVsdMaxTiles tiles)
-  uint32_t c_tau[kMaxTaus / 2];
+  uint32_t c_tau[(NT + 1) / 2];
   double lin[kMaxTaus];
 #pragma unroll
   for (int k = 0; k < kMaxTaus; ++k) {
-    if (k < kMaxTaus / 2) c_tau[k] = 0;
+    if (k < (NT + 1) / 2) c_tau[k] = 0;
     lin[k] = 0.0;
   }
 
@@ -495,7 +561,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
           const double dist_g = dist_of(pX, pY, rcp_rn(__uint_as_float(qg)));
           const double dist_t = dist_of(pX, pY, frame[(int64_t)y * IW + x]);
           c_valid += dist_t > 0.0;
-          const bool vis = visib19(dist_t, dist_g, a.delta32, a.delta_f64, a.delta64);
+          const bool vis = visib19t(dist_t, dist_g, a.dthr);
           uint8_t* mk = a.masks ? a.masks + (2 * b) * (int64_t)IW * IH + (int64_t)y * IW + x
                                 : nullptr;
           if (mk) mk[0] = 255u;
@@ -517,20 +583,26 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         const double dist_t = dist_of(pX, pY, dtest);
         const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
         const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
-        const bool vg = visib19(dist_t, dist_g, a.delta32, a.delta_f64, a.delta64);
-        bool ve = visib19(dist_t, dist_e, a.delta32, a.delta_f64, a.delta64);
+        const bool vg = visib19t(dist_t, dist_g, a.dthr);
+        bool ve = visib19t(dist_t, dist_e, a.dthr);
         ve = ve || (vg && dist_e > 0.0);  // visibility.py:74
         c_union += (vg || ve);
         if (vg && ve) {
           ++c_inter;
           double dd = fabs(dist_g - dist_e);
-          if (a.normalized) dd /= a.diameters[b];
+          if constexpr (COST == 0) {
+            if (divide) {  // rare: a real branch, not a speculated division
+              dd /= diam;
+              asm volatile("" : "+v"(dd));
+            }
 #pragma unroll
-          for (int k = 0; k < kMaxTaus; ++k) {
-            if (k < a.n_tau) {
-              if (COST == 0) {
-                c_tau[k >> 1] += (uint32_t)(dd >= a.taus[k]) << (16 * (k & 1));
-              } else {
+            for (int k = 0; k < NT; ++k)
+              c_tau[k >> 1] += (uint32_t)(dd >= thr[k]) << (16 * (k & 1));
+          } else {
+            if (a.normalized) dd /= a.diameters[b];
+#pragma unroll
+            for (int k = 0; k < kMaxTaus; ++k) {
+              if (k < a.n_tau) {
                 const double cst = dd / a.taus[k];
                 lin[k] += cst > 1.0 ? 1.0 : cst;
               }
@@ -552,10 +624,11 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
 #pragma unroll
   for (int k = 0; k < kMaxTaus; ++k) {
     tau_sum[k] = 0;
-    if (COST == 0)
-      tau_sum[k] = wave_sum_u32((c_tau[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
-    else
+    if (COST == 0) {
+      if (k < NT) tau_sum[k] = wave_sum_u32((c_tau[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+    } else {
       lin[k] = wave_sum_f64(lin[k]);
+    }
   }
   if (lane == 0) {
     s_cnt[wave][0] = c_union;
@@ -637,23 +710,21 @@ hipError_t read_vsd_stats(unsigned long long* out, int reset) {
   return e == hipSuccess ? hipMemcpyToSymbol(HIP_SYMBOL(g_vsd_time), z, sizeof(z)) : e;
 }
 
+constexpr int kBopTaus = 10;  // eval_calc_errors.py:47, np.arange(0.05, 0.51, 0.05)
+
 template <int RPT>
 static void launch_vsd_rpt(const VsdArgs& a, int cost_type, hipStream_t s) {
   dim3 grid((unsigned)a.n), block(kVsdThreads);
-#ifdef BOPX_VSD_PAD_LDS  // occupancy experiments: unused dynamic LDS per workgroup
-  if (cost_type == 0) {
-    hipLaunchKernelGGL((k_vsd<0, RPT>), grid, block, BOPX_VSD_PAD_LDS, s, a);
-    return;
-  }
-#endif
-  if (cost_type == 0)
-    hipLaunchKernelGGL((k_vsd<0, RPT>), grid, block, 0, s, a);
+  if (cost_type == 0 && a.n_tau <= kBopTaus)
+    hipLaunchKernelGGL((k_vsd<0, RPT, kBopTaus>), grid, block, 0, s, a);
+  else if (cost_type == 0)
+    hipLaunchKernelGGL((k_vsd<0, RPT, kMaxTaus>), grid, block, 0, s, a);
   else if (cost_type == 1)
-    hipLaunchKernelGGL((k_vsd<1, RPT>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_vsd<1, RPT, kMaxTaus>), grid, block, 0, s, a);
   else if (cost_type == kCostCover)
-    hipLaunchKernelGGL((k_vsd<kCostCover, RPT>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_vsd<kCostCover, RPT, kMaxTaus>), grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL((k_vsd<kCostGtInfo, RPT>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_vsd<kCostGtInfo, RPT, kMaxTaus>), grid, block, 0, s, a);
 }
 
 hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s) {

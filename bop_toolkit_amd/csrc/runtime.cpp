@@ -663,6 +663,16 @@ int bopx_proj_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doub
 }
 
 // ------------------------------------------------------------------------ VSD
+// The float32 threshold t with (diff <= t) == the visibility test of
+// visibility.py:35-37 for every float32 diff: delta itself (cast to float32,
+// NumPy's weak Python-float scalar) or, for a float64 delta (BOPX_DELTA_F64,
+// the comparison promoted to float64), the largest float32 <= delta.
+static float visib_thr32(double delta, int flags) {
+  float f = (float)delta;
+  if ((flags & BOPX_DELTA_F64) && (double)f > delta) f = std::nextafter(f, -INFINITY);
+  return f;
+}
+
 static int fill_vsd_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height, double delta,
                          int flags, const double* taus, int n_tau, int normalized,
                          int cost_type) {
@@ -680,6 +690,7 @@ static int fill_vsd_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height, d
   a.delta32 = (float)delta;
   a.delta64 = delta;
   a.delta_f64 = (flags & BOPX_DELTA_F64) ? 1 : 0;
+  a.dthr = visib_thr32(delta, flags);
   a.n_tau = n_tau;
   a.normalized = normalized ? 1 : 0;
   static const int ablate = [] {
@@ -817,6 +828,7 @@ static int gt_info_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height, do
   a.delta32 = (float)delta;
   a.delta64 = delta;
   a.delta_f64 = (flags & BOPX_DELTA_F64) ? 1 : 0;
+  a.dthr = visib_thr32(delta, flags);
   a.n_tau = 0;
   return BOPX_OK;
 }

@@ -149,7 +149,7 @@ def test_raster_bit_exact_vs_oracle(ctx, oracle_mod):
 
 
 def _fused_vs_oracle(oracle_mod, seed, n, W, H, K, n_lat, n_lon, delta=15.0, cost="step",
-                     normalized=True):
+                     normalized=True, taus=None, dia=None, delta_f64=False):
   """Fused k_vsd (raster + VSD) vs oracle raster + oracle VSD, bit for bit."""
   from bop_toolkit_amd import _lib
   from bop_toolkit_amd._lib import _d, _f, _i32, ptr
@@ -165,23 +165,23 @@ def _fused_vs_oracle(oracle_mod, seed, n, W, H, K, n_lat, n_lon, delta=15.0, cos
     dt[rng.random(dt.shape) < 0.1] = 0.0
     frames.append(np.round(dt).astype(np.float32))
   frames = np.stack(frames)
-  taus = np.arange(0.05, 0.51, 0.05)
+  taus = np.arange(0.05, 0.51, 0.05) if taus is None else np.asarray(taus, np.float64)
   ids = np.full(n, 9, np.int32)
   pe = np.concatenate([Re.reshape(n, 9), te_], 1)
   pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
   fi = np.arange(n, dtype=np.int32)
   cam = np.tile([fx, fy, cx, cy], (n, 1)).astype(np.float64)
-  dia = np.full(n, 160.0)
+  dia = np.full(n, 160.0) if dia is None else np.asarray(dia, np.float64)
   out = np.empty((n, len(taus)))
   code = {"step": 0, "tlinear": 1}[cost]
   ctx.call("bopx_vsd_batch", n, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(fi, _i32),
-           ptr(frames, _f), n, W, H, ptr(cam, _d), delta, 0, ptr(taus, _d), len(taus),
+           ptr(frames, _f), n, W, H, ptr(cam, _d), delta, int(delta_f64), ptr(taus, _d), len(taus),
            int(normalized), ptr(dia, _d), code, ptr(out, _d))
   for i in range(n):
     de = oracle_mod.render_depth(pts, faces, Re[i], te_[i], fx, fy, cx, cy, W, H)
     dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, W, H)
     ref = oracle_mod.vsd_depths(frames[i], de, dg, fx, fy, cx, cy, delta, taus, normalized,
-                                160.0, cost)
+                                dia[i], cost, delta_f64)
     if cost == "step":
       assert list(out[i]) == ref, (i, out[i], ref)
     else:
@@ -206,6 +206,29 @@ def test_fused_vsd_tlinear_and_raw(oracle_mod):
   _fused_vs_oracle(oracle_mod, 13, 12, 640, 480, synth.LMO_K, 20, 40, cost="tlinear")
   _fused_vs_oracle(oracle_mod, 14, 12, 720, 540, synth.TLESS_K, 20, 40, delta=5.0,
                    normalized=False)
+
+
+def test_fused_vsd_step_thresholds_edge_cases(oracle_mod):
+  """Per-tuple step thresholds (kern_vsd.hip step_threshold) and the float32
+  visibility threshold (runtime.cpp visib_thr32) vs the oracle's per-pixel
+  division and comparison, on diameters and taus at and beyond the edges:
+  tiny, huge, zero, signed zero, negative, infinite and NaN diameters; zero,
+  negative, subnormal, huge, infinite and NaN taus; float64 delta."""
+  from bop_toolkit_amd import synth
+  inf, nan = float("inf"), float("nan")
+  dia = [160.0, 1e-300, 1e300, 0.0, -0.0, -160.0, inf, -inf, nan, 3.3e-5, 7.0,
+         np.nextafter(160.0, inf), 95.123456789, 1.0]
+  n = len(dia)
+  bop = list(np.arange(0.05, 0.51, 0.05))
+  # 10 taus: the NT = 10 kernel; 13 taus: the NT = 16 kernel
+  taus10 = [0.0, -0.1, 5e-324, 1e308, inf, -inf, 0.1, 0.35, 2.0, 0.15000000000000002]
+  taus13 = bop + [nan, 1e-3, 0.0]
+  for seed, taus in ((21, bop), (22, taus10), (23, taus13)):
+    _fused_vs_oracle(oracle_mod, seed, n, 640, 480, synth.LMO_K, 20, 40, taus=taus, dia=dia)
+  # float64 delta not representable in float32, both comparison modes
+  for f64 in (False, True):
+    _fused_vs_oracle(oracle_mod, 24, 8, 640, 480, synth.LMO_K, 20, 40, delta=15.3,
+                     delta_f64=f64)
 
 
 def test_drop_in_vsd_with_hip_renderer(oracle_mod):
