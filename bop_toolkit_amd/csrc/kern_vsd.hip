@@ -214,6 +214,9 @@ constexpr int kRectsPerThread = (2 * kMaxMeshlets + kVsdThreads - 1) / kVsdThrea
 constexpr int kStageBytes = kGroup * kMeshletVerts * (int)sizeof(RVtx) + kGroup * kMeshletTris * 4;
 constexpr int kCoefBytes = 8 * (kTileW + kTileH);
 constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
+#ifndef BOPX_VSD_POSE4
+#define BOPX_VSD_POSE4 1
+#endif
 #ifndef BOPX_VSD_TOUCH
 #define BOPX_VSD_TOUCH 1
 #endif
@@ -232,9 +235,9 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   __shared__ __attribute__((aligned(16))) uint8_t s_wscr[kVsdWaves][kWaveScr];
   __shared__ RRow s_rec[kVsdWaves][64];          // set-up triangles of the current chunk
   __shared__ uint8_t s_own[kVsdWaves][kRowWin];  // row item -> record (lane) of a window
-  __shared__ uint16_t s_list[2 * kMaxMeshlets];
+  __shared__ __attribute__((aligned(4))) uint16_t s_list[2 * kMaxMeshlets];
   __shared__ int s_next;
-  __shared__ float s_pose[2][12];
+  __shared__ __attribute__((aligned(16))) float s_pose[2][12];
   __shared__ int s_roi[4];
   __shared__ int s_nlist;
   __shared__ double s_thr[kMaxTaus];  // step-cost thresholds (T_k, +inf past n_tau)
@@ -297,6 +300,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
 
   // 1. per-pose meshlet rectangles (kept in registers: entry tid + 256 j) + ROI.
   short4 rect[RPT];
+  int roi[4] = {INT32_MAX, INT32_MAX, -1, -1};
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
     const int i = tid + j * kVsdThreads;
@@ -305,12 +309,26 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       const int r = i >= nm, m = i - r * nm;
       rect[j] = meshlet_rect(g_mlet + 24 * (int64_t)m, s_pose[r], c32, W, H);
       if (rect[j].x <= rect[j].z && rect[j].y <= rect[j].w) {
-        atomicMin(&s_roi[0], (int)rect[j].x);
-        atomicMin(&s_roi[1], (int)rect[j].y);
-        atomicMax(&s_roi[2], (int)rect[j].z);
-        atomicMax(&s_roi[3], (int)rect[j].w);
+        roi[0] = min(roi[0], (int)rect[j].x);
+        roi[1] = min(roi[1], (int)rect[j].y);
+        roi[2] = max(roi[2], (int)rect[j].z);
+        roi[3] = max(roi[3], (int)rect[j].w);
       }
     }
+  }
+  // wave reduction, then one LDS atomic per wave and bound
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    roi[0] = min(roi[0], __shfl_xor(roi[0], off, 64));
+    roi[1] = min(roi[1], __shfl_xor(roi[1], off, 64));
+    roi[2] = max(roi[2], __shfl_xor(roi[2], off, 64));
+    roi[3] = max(roi[3], __shfl_xor(roi[3], off, 64));
+  }
+  if (lane == 0 && roi[2] >= 0) {
+    atomicMin(&s_roi[0], roi[0]);
+    atomicMin(&s_roi[1], roi[1]);
+    atomicMax(&s_roi[2], roi[2]);
+    atomicMax(&s_roi[3], roi[3]);
   }
   // Both q tiles start at 0 once per tuple; afterwards the pixel pass zeroes
   // every pixel it reads (the only ones the raster can have written), so the
@@ -377,18 +395,36 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         f32x4 v[kGroup];
         uint32_t pk[kGroup];
         int pose[kGroup];
+        int ent[kGroup];
+        if constexpr (kGroup == 2) {  // base is even: one 4-byte read of both entries
+          const uint32_t pr = *reinterpret_cast<const uint32_t*>(&s_list[base]);
+          ent[0] = (int)(pr & 0xFFFFu);
+          ent[1] = base + 1 < nl ? (int)(pr >> 16) : ent[0];
+        } else {
+#pragma unroll
+          for (int g = 0; g < kGroup; ++g) ent[g] = s_list[min(base + g, nl - 1)];
+        }
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
-          const int e = __builtin_amdgcn_readfirstlane(s_list[min(base + g, nl - 1)]);
+          const int e = __builtin_amdgcn_readfirstlane(ent[g]);
           pose[g] = e >= nm;
           const int m = e - pose[g] * nm;
           v[g] = g_mvtx[m * kMeshletVerts + lane];
           pk[g] = (base + g < nl) ? g_mtri[m * kMeshletTris + lane] : 0xFFFFFFFFu;
         }
 #pragma unroll
-        for (int g = 0; g < kGroup; ++g)
-          w_stage[g * kMeshletVerts + lane] = r_vertex(s_pose[pose[g]], c32, v[g].x, v[g].y,
-                                                             v[g].z);
+        for (int g = 0; g < kGroup; ++g) {
+#if BOPX_VSD_POSE4
+          const float4* P = reinterpret_cast<const float4*>(&s_pose[pose[g]][0]);
+          const float4 p0 = P[0], p1 = P[1], p2 = P[2];  // 3 x ds_read_b128
+          const float Rf[12] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y,
+                                p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
+          w_stage[g * kMeshletVerts + lane] = r_vertex(Rf, c32, v[g].x, v[g].y, v[g].z);
+#else
+          w_stage[g * kMeshletVerts + lane] =
+              r_vertex(s_pose[pose[g]], c32, v[g].x, v[g].y, v[g].z);
+#endif
+        }
         wave_lds_sync();
         VSD_STAMP(8);
         int cnt = 0;
@@ -499,14 +535,14 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         }
       }
 #endif
+      // float64 distance coefficients of the tile's columns / rows (misc.py:137-138),
+      // per wave into its scratch (its staging area is dead until the next
+      // tile), computed before the raster-end barrier while other waves finish
+      for (int i = lane; i < kTileW; i += 64) w_pX[i] = ((double)(tx0 + i - ox) - cx) / fx;
+      for (int i = lane; i < kTileH; i += 64) w_pY[i] = ((double)(ty0 + i - oy) - cy) / fy;
       VSD_STAMP(2);
       __syncthreads();
       asm volatile("" ::"v"(touch));
-      // float64 distance coefficients of the tile's columns / rows (misc.py:137-138),
-      // per wave into its scratch (the staging area is dead until the next tile)
-      for (int i = lane; i < kTileW; i += 64) w_pX[i] = ((double)(tx0 + i - ox) - cx) / fx;
-      for (int i = lane; i < kTileH; i += 64) w_pY[i] = ((double)(ty0 + i - oy) - cy) / fy;
-      wave_lds_sync();
       VSD_STAMP(3);
       // 3. per-pixel distances, visibility masks, counters. Each wave first
       // compacts its covered pixels (rows wave, wave + 8, ...) into its own

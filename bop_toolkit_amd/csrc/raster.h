@@ -24,16 +24,28 @@
 
 namespace bopx {
 
+#ifndef BOPX_RCP_BALLOT
+#define BOPX_RCP_BALLOT 1
+#endif
+
 // Correctly rounded 1/x, bit-identical to the IEEE 1.0f / x the spec names:
 // hardware reciprocal plus one fused Newton step. Checked against
 // (float)(1.0 / (double)x) for every float32 x with |x| and |1/x| normal
 // (tools/rcp_exhaustive.hip: 4,227,858,432 values, no mismatch); other inputs
 // take the IEEE division.
+// The range test is one unsigned compare on the bits (|x| in [2^-126, 2^126));
+// the IEEE path is a wave-uniform branch taken only if some lane needs it.
 __device__ __forceinline__ float rcp_rn(float x) {
-  const float ax = fabsf(x);
-  if (__builtin_expect(!(ax >= 0x1p-126f && ax < 0x1p126f), 0)) return 1.0f / x;
-  const float r = __builtin_amdgcn_rcpf(x);
-  return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+  const float r0 = __builtin_amdgcn_rcpf(x);
+  const float r = __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+  const bool ok = (__float_as_uint(x) & 0x7FFFFFFFu) - 0x00800000u < 0x7E000000u;
+#if BOPX_RCP_BALLOT
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) != 0, 0)) return ok ? r : 1.0f / x;
+  return r;
+#else
+  if (__builtin_expect(!ok, 0)) return 1.0f / x;
+  return r;
+#endif
 }
 
 struct Cam32 {
