@@ -246,7 +246,8 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   double(*s_lin)[kMaxTaus] = reinterpret_cast<double(*)[kMaxTaus]>(&s_dep[1][0]);
 
   const int64_t b = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   RVtx* const w_stage = reinterpret_cast<RVtx*>(&s_wscr[wave][0]);
   uint32_t* const w_tri =
       reinterpret_cast<uint32_t*>(&s_wscr[wave][kGroup * kMeshletVerts * sizeof(RVtx)]);
@@ -551,13 +552,20 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       // pixel -> lane assignment is fixed (deterministic float64 sums).
       uint16_t* pix = reinterpret_cast<uint16_t*>(&s_rec[0][0]) + wave * kPixPerWave;
       int npix = 0;
-      for (int p = tid; p < (VSD_DIAG(2) ? 0 : kTileW * kTileH); p += kVsdThreads) {
-        const int ps = (p / kTileW) * kTileStride + p % kTileW;
-        const bool cov = ty0 + p / kTileW <= ty1 && tx0 + p % kTileW <= tx1 &&
-                         (s_dep[0][ps] | s_dep[1][ps]) != 0u;
-        const unsigned long long bal = __ballot(cov);
-        if (cov) pix[npix + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)p;
-        npix += __popcll(bal);
+      {
+        // lane = column, one wave-uniform tile row per step (rows w, w + 8, ...)
+        static_assert(kTileW == 64, "pixel compaction maps lanes to tile columns");
+        const int nrow = VSD_DIAG(2) ? 0 : ty1 - ty0 + 1;
+        const bool col_in = tx0 + lane <= tx1;
+        for (int r = wave; r < nrow; r += kVsdWaves) {
+          const int ps = r * kTileStride + lane;
+          const bool cov = col_in & ((s_dep[0][ps] | s_dep[1][ps]) != 0u);
+          const unsigned long long bal = __ballot(cov);
+          const int rank = (int)__builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          if (cov) pix[npix + rank] = (uint16_t)(r * kTileW + lane);
+          npix += __popcll(bal);
+        }
       }
       wave_lds_sync();
       for (int i = lane; i < npix; i += 64) {
