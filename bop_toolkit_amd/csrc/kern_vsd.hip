@@ -408,10 +408,11 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
           const int e = __builtin_amdgcn_readfirstlane(ent[g]);
-          pose[g] = e >= nm;
+          pose[g] = __builtin_amdgcn_readfirstlane(e >= nm ? 1 : 0);  // uniform (SGPR)
           const int m = e - pose[g] * nm;
           v[g] = g_mvtx[m * kMeshletVerts + lane];
-          pk[g] = (base + g < nl) ? g_mtri[m * kMeshletTris + lane] : 0xFFFFFFFFu;
+          pk[g] = g_mtri[m * kMeshletTris + lane];  // unconditional: entry is valid
+          if (base + g >= nl) pk[g] = 0xFFFFFFFFu;   // (clamped duplicate, no triangles)
         }
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {

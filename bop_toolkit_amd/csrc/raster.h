@@ -68,17 +68,15 @@ __device__ __forceinline__ RVtx r_vertex(const float* __restrict__ Rf, const Cam
   const float X = ((Rf[0] * x + Rf[1] * y) + Rf[2] * z) + Rf[9];
   const float Y = ((Rf[3] * x + Rf[4] * y) + Rf[5] * z) + Rf[10];
   const float Z = ((Rf[6] * x + Rf[7] * y) + Rf[8] * z) + Rf[11];
-  o.U = INT32_MIN;
-  o.V = 0;
-  o.iz = 0.0f;
-  if (!(Z > 0.0f)) return o;
+  // Branch-free: every lane computes the projection, invalid ones are
+  // replaced by the sentinel afterwards (same values as an early return).
   const float iz = rcp_rn(Z);  // the one IEEE division per vertex (spec v4)
   const float u = (c.fx * X) * iz + c.cx;
   const float v = (c.fy * Y) * iz + c.cy;
-  if (!(fabsf(u) <= kGuardBand) || !(fabsf(v) <= kGuardBand)) return o;
-  o.U = (int32_t)__builtin_rintf(u * 256.0f);
-  o.V = (int32_t)__builtin_rintf(v * 256.0f);
-  o.iz = iz;
+  const bool ok = (int)(Z > 0.0f) & (int)(fabsf(u) <= kGuardBand) & (int)(fabsf(v) <= kGuardBand);
+  o.U = ok ? (int32_t)__builtin_rintf((ok ? u : 0.0f) * 256.0f) : INT32_MIN;
+  o.V = ok ? (int32_t)__builtin_rintf((ok ? v : 0.0f) * 256.0f) : 0;
+  o.iz = ok ? iz : 0.0f;
   return o;
 }
 
