@@ -456,8 +456,8 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
             const uint32_t ref = w_tri[c0 + lane];
             const RVtx* sg = &w_stage[((ref >> 24) & 3u) * kMeshletVerts];
             r = (int)(ref >> 26);
-            ok = r_setup(sg[ref & 255u], sg[(ref >> 8) & 255u], sg[(ref >> 16) & 255u], T, tx0,
-                         tx1, ty0, ty1);
+            ok = r_setup_touching(sg[ref & 255u], sg[(ref >> 8) & 255u], sg[(ref >> 16) & 255u],
+                                  T);  // passed r_touches in the compaction
             if (ok) {
               cc0 = max(T.c0, tx0);
               cc1 = min(T.c1, tx1);

@@ -150,6 +150,52 @@ __device__ __forceinline__ bool r_setup(RVtx a, RVtx b, RVtx c, RTri& t, int x0,
   return true;
 }
 
+// r_setup for a triangle that already passed r_touches (valid vertices, bbox
+// meets the rectangle): the same RTri, false only for a zero area. Built for
+// full waves (k_vsd): no early returns, the winding swap is a select, and the
+// int64 area of large triangles runs behind a wave-uniform branch.
+__device__ __forceinline__ bool r_setup_touching(const RVtx a, const RVtx b0, const RVtx c0,
+                                                 RTri& t) {
+  const int32_t minU = min(a.U, min(b0.U, c0.U)), maxU = max(a.U, max(b0.U, c0.U));
+  const int32_t minV = min(a.V, min(b0.V, c0.V)), maxV = max(a.V, max(b0.V, c0.V));
+  t.c0 = (minU + 127) >> 8;
+  t.c1 = (maxU - 128) >> 8;
+  t.r0 = (minV + 127) >> 8;
+  t.r1 = (maxV - 128) >> 8;
+  t.small = (maxU - minU) < 32768 && (maxV - minV) < 32768;
+  // small: factors < 2^15, exact 24-bit multiplies (other lanes: replaced below)
+  const int32_t area32 = __mul24(b0.U - a.U, c0.V - a.V) - __mul24(b0.V - a.V, c0.U - a.U);
+  bool neg = area32 < 0, nz = area32 != 0;
+  float farea = (float)(neg ? -area32 : area32);
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(!t.small) != 0, 0)) {
+    if (!t.small) {
+      const int64_t area =
+          (int64_t)(b0.U - a.U) * (c0.V - a.V) - (int64_t)(b0.V - a.V) * (c0.U - a.U);
+      neg = area < 0;
+      nz = area != 0;
+      farea = (float)(double)(neg ? -area : area);
+    }
+  }
+  const RVtx b = neg ? c0 : b0, c = neg ? b0 : c0;
+  const float inv_area = rcp_rn(nz ? farea : 1.0f);
+  const float dza = a.iz - c.iz, dzb = b.iz - c.iz;
+  t.ga = ((float)(b.V - c.V) * dza + (float)(c.V - a.V) * dzb) * inv_area;
+  t.gb = ((float)(c.U - b.U) * dza + (float)(a.U - c.U) * dzb) * inv_area;
+  t.U0 = a.U;
+  t.V0 = a.V;
+  t.iz0 = a.iz;
+  const RVtx s[3] = {b, c, a}, e[3] = {c, a, b};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    t.Us[k] = s[k].U;
+    t.Vs[k] = s[k].V;
+    t.dU[k] = e[k].U - s[k].U;
+    t.dV[k] = e[k].V - s[k].V;
+    t.tl[k] = (t.dV[k] < 0 || (t.dV[k] == 0 && t.dU[k] > 0)) ? 1 : 0;
+  }
+  return nz;
+}
+
 // Cheap pre-test: all vertices valid and the pixel bbox meets [x0,x1] x [y0,y1]
 // (the same bbox r_setup computes; r_setup may still reject zero-area triangles).
 __device__ __forceinline__ bool r_touches(RVtx a, RVtx b, RVtx c, int x0, int x1, int y0,
