@@ -308,18 +308,22 @@ __device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int 
 // loop body: the edge tests, the q plane and the LDS op form straight-line code.
 // dep: the pose's q tile (row pitch kTileStride). Returns the fragment count.
 __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* dep) {
-  const int tc0 = r.meta & 63u, tr = (int)((r.meta >> 6) & 63u) + j;
+  // j < 64 and the tile row tr < 64 always; the masks (no-ops) tell the
+  // compiler so, which keeps every multiply below on the full-rate 24-bit path.
+  j &= 63;
+  const int tc0 = r.meta & 63u, tr = ((int)((r.meta >> 6) & 63u) + j) & 63;
   const int w = (int)((r.meta >> 12) & 63u) + 1;
   uint32_t e[3], sx[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const int32_t dU = (int32_t)(r.duv[k] << 16) >> 16, dV = (int32_t)r.duv[k] >> 16;
-    e[k] = r.er[k] + (uint32_t)__mul24(256 * dU, j);  // |256 dU| < 2^23, j < 64
-    sx[k] = (uint32_t)(-256 * dV);
+    const int32_t dU256 = (int32_t)(r.duv[k] << 16) >> 8;  // 256 dU, |256 dU| < 2^23
+    const int32_t dV = (int32_t)r.duv[k] >> 16;
+    e[k] = r.er[k] + (uint32_t)__mul24(dU256, j);
+    sx[k] = (uint32_t)__mul24(-256, dV);
   }
-  const float qy = r.gb * (float)(r.py0v + 256 * j);
+  const float qy = r.gb * (float)(r.py0v + (j << 8));
   float fdx = (float)r.px0u;  // integers below 2^24: += 256 is exact
-  uint32_t* d = dep + tr * kTileStride + tc0;
+  uint32_t* d = dep + __mul24(tr, kTileStride) + tc0;
   int frags = 0;
   // Two columns per iteration (independent chains). The second column of the
   // last pair may be one past the rectangle: it is masked to 0 and lands in
