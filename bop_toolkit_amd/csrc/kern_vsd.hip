@@ -196,6 +196,13 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Load base[byte_off] for a wave-uniform base and a 32-bit per-lane byte
+// offset: global_load with an SGPR base (saddr) and no 64-bit address math.
+template <class T>
+__device__ __forceinline__ T ld_off(gptr<const T> base, uint32_t byte_off) {
+  return *(gptr<const T>)((gptr<const char>)base + byte_off);
+}
+
 constexpr int kVsdWaves = kVsdThreads / 64;
 #ifndef BOPX_VSD_GROUP
 #define BOPX_VSD_GROUP 2
@@ -405,14 +412,21 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
 #pragma unroll
           for (int g = 0; g < kGroup; ++g) ent[g] = s_list[min(base + g, nl - 1)];
         }
+        int mlt[kGroup];
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
           const int e = __builtin_amdgcn_readfirstlane(ent[g]);
           pose[g] = __builtin_amdgcn_readfirstlane(e >= nm ? 1 : 0);  // uniform (SGPR)
-          const int m = e - pose[g] * nm;
-          v[g] = g_mvtx[m * kMeshletVerts + lane];
-          pk[g] = g_mtri[m * kMeshletTris + lane];  // unconditional: entry is valid
-          if (base + g >= nl) pk[g] = 0xFFFFFFFFu;   // (clamped duplicate, no triangles)
+          mlt[g] = e - pose[g] * nm;
+        }
+        // all loads of the group in flight before the first use
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g)
+          v[g] = ld_off(g_mvtx + mlt[g] * kMeshletVerts, (uint32_t)lane * 16u);
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g) {
+          pk[g] = ld_off(g_mtri + mlt[g] * kMeshletTris, (uint32_t)lane * 4u);  // entry is valid
+          if (base + g >= nl) pk[g] = 0xFFFFFFFFu;  // (clamped duplicate, no triangles)
         }
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
@@ -527,13 +541,16 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       // while it waits for the other waves at the raster-end barrier: the
       // pixel pass then reads them from L2 instead of HBM. The empty asm below
       // consumes the value (the only wait for these loads).
+      // test depth of this tile: wave-uniform base, offsets < 64 rows x IW x 4 B
+      const gptr<const float> tframe = frame + ((int64_t)ty0 * IW + tx0);
       float touch = 0.0f;
 #if BOPX_VSD_TOUCH
       if constexpr (COST == 0 || COST == 1) {
         if (lane < 3 * (kTileH / kVsdWaves)) {
           const int row = ty0 + wave + kVsdWaves * (lane / 3), k = lane % 3;
           const int col = k == 0 ? tx0 : (k == 1 ? min(tx0 + 32, tx1) : tx1);
-          if (row <= ty1) touch = frame[(int64_t)row * IW + col];
+          if (row <= ty1)
+            touch = ld_off(tframe, (uint32_t)(__mul24(row - ty0, IW) + (col - tx0)) * 4u);
         }
       }
 #endif
@@ -622,7 +639,8 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         }
         const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
         const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
-        const float dtest = frame[(int64_t)row * IW + col];
+        const float dtest =
+            ld_off(tframe, (uint32_t)(__mul24(p / kTileW, IW) + p % kTileW) * 4u);
         const double pX = w_pX[p % kTileW];
         const double pY = w_pY[p / kTileW];
         const double dist_t = dist_of(pX, pY, dtest);
