@@ -119,11 +119,12 @@ def test_vsd_foreign_renderer_bit_exact(golden_vsd):
            _Stub([g["depth_est"][3], g["depth_gt"][3]]), 1, "bogus")
 
 
-def _scene(seed, n, W=640, H=480, n_lat=20, n_lon=40, K=None):
+def _scene(seed, n, W=640, H=480, n_lat=20, n_lon=40, K=None, xy=(150.0, 100.0),
+           z_range=(450.0, 1200.0)):
   from bop_toolkit_amd import synth
   rng = np.random.default_rng(seed)
   pts, faces = synth.superellipsoid(n_lat, n_lon, (45.0, 35.0, 55.0), 0.7)
-  Rg, tg = synth.gt_poses(rng, n, z_range=(450.0, 1200.0))
+  Rg, tg = synth.gt_poses(rng, n, z_range=z_range, xy=xy)
   Re, te_ = synth.perturb(rng, Rg, tg)
   K = synth.LMO_K if K is None else K
   return rng, pts, faces, Rg, tg, Re, te_, K
@@ -149,11 +150,11 @@ def test_raster_bit_exact_vs_oracle(ctx, oracle_mod):
 
 
 def _fused_vs_oracle(oracle_mod, seed, n, W, H, K, n_lat, n_lon, delta=15.0, cost="step",
-                     normalized=True, taus=None, dia=None, delta_f64=False):
+                     normalized=True, taus=None, dia=None, delta_f64=False, **scene):
   """Fused k_vsd (raster + VSD) vs oracle raster + oracle VSD, bit for bit."""
   from bop_toolkit_amd import _lib
   from bop_toolkit_amd._lib import _d, _f, _i32, ptr
-  rng, pts, faces, Rg, tg, Re, te_, _ = _scene(seed, n, W, H, n_lat, n_lon)
+  rng, pts, faces, Rg, tg, Re, te_, _ = _scene(seed, n, W, H, n_lat, n_lon, **scene)
   ctx = _lib.Context(0)
   ctx.add_object(9, pts, faces)
   fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
@@ -206,6 +207,16 @@ def test_fused_vsd_tlinear_and_raw(oracle_mod):
   _fused_vs_oracle(oracle_mod, 13, 12, 640, 480, synth.LMO_K, 20, 40, cost="tlinear")
   _fused_vs_oracle(oracle_mod, 14, 12, 720, 540, synth.TLESS_K, 20, 40, delta=5.0,
                    normalized=False)
+
+
+def test_fused_vsd_bit_exact_image_borders(oracle_mod):
+  """Objects straddling and leaving the image borders: ROIs clipped at the
+  image edge, tiles cut by the ROI (the row walk's unmasked column past a cut,
+  cleared by the pixel compaction, must not leak into later tiles)."""
+  from bop_toolkit_amd import synth
+  out = _fused_vs_oracle(oracle_mod, 31, 48, 640, 480, synth.LMO_K, 24, 48, xy=(420.0, 320.0),
+                         z_range=(420.0, 800.0))
+  assert np.ptp(out) > 0.1
 
 
 def test_fused_vsd_step_thresholds_edge_cases(oracle_mod):
