@@ -575,7 +575,11 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         static_assert(kTileW == 64, "pixel compaction maps lanes to tile columns");
         const int nrow = VSD_DIAG(2) ? 0 : ty1 - ty0 + 1;
         const bool col_in = tx0 + lane <= tx1;
+        // column right of a tile cut by the ROI: the row walk may have written
+        // it (r_walk_row_max); cleared here (wave-private rows, raster done)
+        const int cut = tx1 - tx0 + 1;
         for (int r = wave; r < nrow; r += kVsdWaves) {
+          if (cut < kTileW && lane < 2) s_dep[lane][r * kTileStride + cut] = 0u;
           const int ps = r * kTileStride + lane;
           const bool cov = col_in & ((s_dep[0][ps] | s_dep[1][ps]) != 0u);
           const unsigned long long bal = __ballot(cov);

@@ -326,8 +326,10 @@ __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* de
   uint32_t* d = dep + __mul24(tr, kTileStride) + tc0;
   int frags = 0;
   // Two columns per iteration (independent chains). The second column of the
-  // last pair may be one past the rectangle: it is masked to 0 and lands in
-  // the tile (or in its padding column, tc0 + w <= 64 < kTileStride).
+  // last pair may be one past the rectangle and is not masked: past the
+  // triangle's own bbox no pixel centre is inside it; past a tile clip it lands
+  // in the padding column (tc0 + w = 64 < kTileStride) or, for a tile cut by
+  // the ROI, in the column right of it, which the pixel compaction clears.
   for (int i = 0; i < w; i += 2, fdx += 512.0f) {
     const uint32_t f0 = e[0] + sx[0], f1 = e[1] + sx[1], f2 = e[2] + sx[2];
     const int32_t m0 = min((int32_t)e[0], min((int32_t)e[1], (int32_t)e[2]));
@@ -335,8 +337,8 @@ __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* de
     const float q0 = (r.iz0 + r.ga * fdx) + qy;
     const float q1 = (r.iz0 + r.ga * (fdx + 256.0f)) + qy;
     const bool in0 = (m0 > 0) & (q0 > 0.0f);
-    const bool in1 = (i + 1 < w) & (m1 > 0) & (q1 > 0.0f);
-    frags += in0 + in1;
+    const bool in1 = (m1 > 0) & (q1 > 0.0f);
+    frags += in0 + ((i + 1 < w) & in1);  // diagnostics
     atomicMax(d + i, in0 ? __float_as_uint(q0) : 0u);
     atomicMax(d + i + 1, in1 ? __float_as_uint(q1) : 0u);
     e[0] = f0 + sx[0];
