@@ -53,3 +53,35 @@ def test_bop19_two_ranks_match_reference(tmp_path):
     with open(os.path.join(E2E, "expected", sign, "errors_000002.json")) as f, \
         open(tmp_path / name / sign / "errors_000002.json") as g:
       assert g.read() == f.read(), sign
+
+
+_RCCL_GATHER = r"""
+import os, torch, torch.distributed as dist
+from bop_toolkit_amd import shard
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+assert dist.get_backend() == "nccl"
+g = torch.Generator().manual_seed(7)
+n, c = 1000, 12
+rows = torch.rand((n, c), generator=g, dtype=torch.float64).cuda()
+ids = torch.randperm(n, generator=g).cuda()
+for counts in (None, [n]):
+  table = shard.gather_rows(rows, ids, n, counts=counts)
+  ref = torch.empty_like(rows)
+  ref[ids] = rows
+  assert table.device.type == "cuda" and torch.equal(table, ref), counts
+torch.cuda.synchronize()
+dist.destroy_process_group()
+print("RCCL_GATHER_OK")
+"""
+
+
+def test_rccl_gather_rows_one_rank():
+  """shard.gather_rows over the real RCCL backend (the collective bench.py and
+  the sharded callers use at N > 1: one all_gather_into_tensor of device rows,
+  scattered by tuple id on rank 0), world size 1 on this one-GPU box."""
+  env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
+             WORLD_SIZE="1", LOCAL_RANK="0", PYTHONPATH=REPO)
+  r = subprocess.run([sys.executable, "-c", _RCCL_GATHER], env=env, cwd=REPO,
+                     capture_output=True, text=True, timeout=180)
+  assert r.returncode == 0 and "RCCL_GATHER_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
