@@ -227,6 +227,12 @@ constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 #ifndef BOPX_VSD_TOUCH
 #define BOPX_VSD_TOUCH 1
 #endif
+// Waves that claim the last entry groups of a tile run at raised issue priority
+// until the raster-end barrier (the tile's critical path; the sibling
+// workgroup's waves yield to them).
+#ifndef BOPX_VSD_PRIO
+#define BOPX_VSD_PRIO 3
+#endif
 
 // COST: 0 = step, 1 = tlinear, kCostCover = silhouette overlap, kCostGtInfo = GT stats.
 // NT (step cost): thresholds compared per pixel (>= n_tau; 10 for the BOP taus).
@@ -400,6 +406,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         if (lane == 0) base = atomicAdd(&s_next, kGroup);
         base = __builtin_amdgcn_readfirstlane(base);
         if (base >= nl) break;
+        if (BOPX_VSD_PRIO && base + kGroup * kVsdWaves >= nl) __builtin_amdgcn_s_setprio(BOPX_VSD_PRIO);
         f32x4 v[kGroup];
         uint32_t pk[kGroup];
         int pose[kGroup];
@@ -561,6 +568,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       for (int i = lane; i < kTileH; i += 64) w_pY[i] = ((double)(ty0 + i - oy) - cy) / fy;
       VSD_STAMP(2);
       __syncthreads();
+      if (BOPX_VSD_PRIO) __builtin_amdgcn_s_setprio(0);
       asm volatile("" ::"v"(touch));
       VSD_STAMP(3);
       // 3. per-pixel distances, visibility masks, counters. Each wave first
