@@ -230,6 +230,12 @@ constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 // Waves that claim the last entry groups of a tile run at raised issue priority
 // until the raster-end barrier (the tile's critical path; the sibling
 // workgroup's waves yield to them).
+// Entry queue order: entries whose rectangle overlaps the tile by at least
+// BOPX_VSD_LPT pixels are dealt first (front of s_list), the rest after them
+// (back of s_list, growing down), so the queue tail holds the cheap entries.
+#ifndef BOPX_VSD_LPT
+#define BOPX_VSD_LPT 1024
+#endif
 #ifndef BOPX_VSD_PRIO
 #define BOPX_VSD_PRIO 3
 #endif
@@ -253,6 +259,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   __shared__ __attribute__((aligned(16))) float s_pose[2][12];
   __shared__ int s_roi[4];
   __shared__ int s_nlist;
+  __shared__ int s_nsmall;
   __shared__ double s_thr[kMaxTaus];  // step-cost thresholds (T_k, +inf past n_tau)
   // Final per-wave partial counters reuse the depth tiles (after the tile loop).
   uint32_t(*s_cnt)[2 + kMaxTaus] = reinterpret_cast<uint32_t(*)[2 + kMaxTaus]>(&s_dep[0][0]);
@@ -382,6 +389,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       // already zero, see the pixel pass).
       if (tid == 0) {
         s_nlist = 0;
+        s_nsmall = 0;
         s_next = 0;
       }
       __syncthreads();
@@ -390,8 +398,19 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       for (int j = 0; j < RPT; ++j) {
         const short4 rc = rect[j];
         if (rc.x <= tx1 && rc.z >= tx0 && rc.y <= ty1 && rc.w >= ty0 && rc.x <= rc.z &&
-            rc.y <= rc.w)
+            rc.y <= rc.w) {
+#if BOPX_VSD_LPT
+          const int ow = min((int)rc.z, tx1) - max((int)rc.x, tx0) + 1;
+          const int oh = min((int)rc.w, ty1) - max((int)rc.y, ty0) + 1;
+          if (ow * oh >= BOPX_VSD_LPT)
+            s_list[atomicAdd(&s_nlist, 1)] = (uint16_t)(tid + j * kVsdThreads);
+          else
+            s_list[2 * kMaxMeshlets - 1 - atomicAdd(&s_nsmall, 1)] =
+                (uint16_t)(tid + j * kVsdThreads);
+#else
           s_list[atomicAdd(&s_nlist, 1)] = (uint16_t)(tid + j * kVsdThreads);
+#endif
+        }
       }
       __syncthreads();
       VSD_STAMP(1);
@@ -400,7 +419,9 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       // three fixed-stride vertex blocks once (lane = vertex) into LDS, tests
       // every triangle's bbox against the tile, compacts the hits (ballot rank)
       // and only then sets up and rasterises them, one triangle per lane.
-      const int nl = __builtin_amdgcn_readfirstlane(VSD_DIAG(1) ? 0 : s_nlist);
+      const int nbig = __builtin_amdgcn_readfirstlane(s_nlist);
+      const int nl =
+          __builtin_amdgcn_readfirstlane(VSD_DIAG(1) ? 0 : s_nlist + (BOPX_VSD_LPT ? s_nsmall : 0));
       for (;;) {
         int base = 0;
         if (lane == 0) base = atomicAdd(&s_next, kGroup);
@@ -411,7 +432,13 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         uint32_t pk[kGroup];
         int pose[kGroup];
         int ent[kGroup];
-        if constexpr (kGroup == 2) {  // base is even: one 4-byte read of both entries
+        if constexpr (BOPX_VSD_LPT != 0) {
+#pragma unroll
+          for (int g = 0; g < kGroup; ++g) {
+            const int q = min(base + g, nl - 1);
+            ent[g] = s_list[q < nbig ? q : 2 * kMaxMeshlets - 1 - (q - nbig)];
+          }
+        } else if constexpr (kGroup == 2) {  // base is even: one 4-byte read of both entries
           const uint32_t pr = *reinterpret_cast<const uint32_t*>(&s_list[base]);
           ent[0] = (int)(pr & 0xFFFFu);
           ent[1] = base + 1 < nl ? (int)(pr >> 16) : ent[0];
