@@ -22,6 +22,7 @@ namespace bopx {
 template <class T>
 using gptr = __attribute__((address_space(1))) T*;
 typedef float f32x4 __attribute__((ext_vector_type(4)));  // native vector: works in any addrspace
+typedef float f32x3 __attribute__((ext_vector_type(3)));
 
 constexpr int kMeshletTris = 64;    // one wave lane per triangle
 constexpr int kMeshletVerts = 64;   // unique vertices per meshlet (one per lane)
@@ -82,6 +83,7 @@ struct VsdArgs {
   uint8_t* masks;    // GT-info mode, optional: n x 2 x img_h x img_w (mask, mask_visib)
   const int32_t* order;  // optional launch order (launch_order_by_slot): block k takes tuple order[k]
   int ablate;  // BOPX_VSD_ABLATE, read only by -DBOPX_VSD_DIAG=1 builds (kern_vsd.hip)
+  int cull;    // k_vsd occlusion test of far meshlet entries (BOPX_VSD_CULL, default 1)
   double taus[kMaxTaus];
 };
 

@@ -33,6 +33,7 @@
 // Results are bit-identical to the reference given identical depth maps.
 #include <algorithm>
 #include <cfloat>
+#include <type_traits>
 
 #include "raster.h"
 
@@ -144,15 +145,29 @@ __device__ double step_threshold(double tau, double diam) {
 // corners, runtime.cpp obb_corners) under a pose. Any corner with Z <= 0 (or a
 // non-finite projection) gives the whole image.
 __device__ __forceinline__ short4 meshlet_rect(gptr<const float> mb, const float* Rf,
-                                               const Cam32& c, int W, int H) {
+                                               const Cam32& c, int W, int H, float& zmin) {
   float umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
   bool full = false;
+  zmin = INFINITY;
+  // the 96 B of corners in six 16-B loads, all in flight before the first use
+  f32x4 cb[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) cb[k] = *(gptr<const f32x4>)(mb + 4 * k);
+  float cf[24];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    cf[4 * k] = cb[k].x;
+    cf[4 * k + 1] = cb[k].y;
+    cf[4 * k + 2] = cb[k].z;
+    cf[4 * k + 3] = cb[k].w;
+  }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const float x = mb[3 * k], y = mb[3 * k + 1], z = mb[3 * k + 2];
+    const float x = cf[3 * k], y = cf[3 * k + 1], z = cf[3 * k + 2];
     const float X = ((Rf[0] * x + Rf[1] * y) + Rf[2] * z) + Rf[9];
     const float Y = ((Rf[3] * x + Rf[4] * y) + Rf[5] * z) + Rf[10];
     const float Z = ((Rf[6] * x + Rf[7] * y) + Rf[8] * z) + Rf[11];
+    zmin = fminf(zmin, Z);
     if (!(Z > 0.0f)) {
       full = true;
     } else {
@@ -177,6 +192,74 @@ __device__ __forceinline__ short4 meshlet_rect(gptr<const float> mb, const float
   const int x0 = (int)fmaxf(fx0, 0.0f), y0 = (int)fmaxf(fy0, 0.0f);
   const int x1 = (int)fminf(fx1, (float)(W - 1)), y1 = (int)fminf(fy1, (float)(H - 1));
   return make_short4((short)x0, (short)y0, (short)x1, (short)y1);
+}
+
+// Max over the 64 lanes of non-negative floats (full exec): DPP butterflies
+// inside each row of 16 lanes, then the four row maxima in SALU. No LDS
+// round trips (a __shfl_xor reduction is six dependent ds_bpermute).
+__device__ __forceinline__ float wave_max_nonneg_f32(float x) {
+  int v = __float_as_int(x);  // non-negative floats order like their bits
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false));  // row_ror 4
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false));  // row_ror 8
+  const int m = max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+                    max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+  return __int_as_float(m);
+}
+
+// True iff every pixel of the tile rectangle [x0, x1] x [y0, y1] (tile-relative,
+// wave-uniform, x1 - x0 < 64) holds q bits >= qb in the q tile `dep`. Lanes
+// cover 64 / w rows per step, eight steps per LDS round trip; early exit on the
+// first failing round.
+// A tile rectangle [x0, x1] x [y0, y1] (tile-relative) swept in 8 x 8 pixel
+// blocks, lane = (row lane >> 3, column lane & 7) inside a block; a lane past
+// the rectangle re-reads its last row / column (harmless for a minimum).
+struct Region {
+  int x0, x1, y0, y1, nbx, nb;
+};
+
+__device__ __forceinline__ Region make_region(uint32_t word, int tw, int th) {
+  Region g;
+  g.x0 = (int)((word >> 12) & 31u) * 2;
+  g.x1 = min((int)((word >> 17) & 31u) * 2 + 1, tw - 1);
+  g.y0 = (int)((word >> 22) & 31u) * 2;
+  g.y1 = min((int)((word >> 27) & 31u) * 2 + 1, th - 1);
+  g.nbx = (g.x1 - g.x0 + 8) >> 3;
+  g.nb = g.nbx * ((g.y1 - g.y0 + 8) >> 3);
+  return g;
+}
+
+// Smallest q bits this lane reads in blocks [b0, b0 + 8) of the region (LDS
+// reads issued back to back, one wait at the use).
+__device__ __forceinline__ uint32_t region_min8(const uint32_t* dep, const Region& g, int b0,
+                                                int lane) {
+  uint32_t v[8];
+  // block (bx, by) stepped incrementally (wave-uniform, SALU); past the last
+  // block the last one is re-read
+  int by = (unsigned)b0 / (unsigned)g.nbx, bx = b0 - by * g.nbx;
+  const int lr = lane >> 3, lc = lane & 7;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int r = min(g.y0 + 8 * by + lr, g.y1);
+    const int c = min(g.x0 + 8 * bx + lc, g.x1);
+    v[k] = dep[__mul24(r, kTileStride) + c];
+    if (b0 + k + 1 < g.nb) {
+      if (++bx == g.nbx) {
+        bx = 0;
+        ++by;
+      }
+    }
+  }
+  return min(min(min(v[0], v[1]), min(v[2], v[3])), min(min(v[4], v[5]), min(v[6], v[7])));
+}
+
+// True iff every pixel of the region from block b0 on holds q bits >= qb.
+__device__ __forceinline__ bool region_covered(const uint32_t* dep, const Region& g, int b0,
+                                               uint32_t qb, int lane) {
+  for (int b = b0; b < g.nb; b += 8)
+    if (__builtin_amdgcn_ballot_w64(region_min8(dep, g, b, lane) < qb) != 0) return false;
+  return true;
 }
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
@@ -230,14 +313,28 @@ constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 // Waves that claim the last entry groups of a tile run at raised issue priority
 // until the raster-end barrier (the tile's critical path; the sibling
 // workgroup's waves yield to them).
-// Entry queue order: entries whose rectangle overlaps the tile by at least
-// BOPX_VSD_LPT pixels are dealt first (front of s_list), the rest after them
-// (back of s_list, growing down), so the queue tail holds the cheap entries.
-#ifndef BOPX_VSD_LPT
-#define BOPX_VSD_LPT 1024
-#endif
+// Entry queue order and occlusion culling: per pose, the (pose, meshlet) entries
+// whose nearest OBB corner lies in the near half of that pose's depth range are
+// dealt first (front of s_list), the far ones after them (back of s_list,
+// growing down). A far entry, once its vertex block is staged, is skipped when
+// every pixel of its rectangle inside the tile already holds q >= (1 + 2^-8) x
+// the largest 1/Z of its vertices: spec v5 bounds every fragment of the meshlet
+// by that (raster.h), and q-buffer values only grow, so a value read while other
+// waves still write is a lower bound of the final one. The result is
+// bit-identical with or without the test (VsdArgs::cull, BOPX_VSD_CULL=0).
 #ifndef BOPX_VSD_PRIO
 #define BOPX_VSD_PRIO 3
+#endif
+// Software-pipelined VSD pixel loop: measured 2 % slower than the plain loop
+// (same-box A/B, round 2), kept as an option.
+#ifndef BOPX_VSD_PIXPIPE
+#define BOPX_VSD_PIXPIPE 0
+#endif
+// Queue order: 0 = near entries first (depth), 1 = entries overlapping the tile
+// by >= 1024 px first (round-1 LPT order, 2 % faster without the occlusion
+// test); the occlusion test applies to far entries either way.
+#ifndef BOPX_VSD_LPT_ORDER
+#define BOPX_VSD_LPT_ORDER 1
 #endif
 
 // COST: 0 = step, 1 = tlinear, kCostCover = silhouette overlap, kCostGtInfo = GT stats.
@@ -254,7 +351,15 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   __shared__ __attribute__((aligned(16))) uint8_t s_wscr[kVsdWaves][kWaveScr];
   __shared__ RRow s_rec[kVsdWaves][64];          // set-up triangles of the current chunk
   __shared__ uint8_t s_own[kVsdWaves][kRowWin];  // row item -> record (lane) of a window
-  __shared__ __attribute__((aligned(4))) uint16_t s_list[2 * kMaxMeshlets];
+  // Tile entry queue. RPT <= 2 (objects of <= 512 meshlets): 32-bit words
+  // entry | far << 11 | rectangle in the tile at 2-px granularity (x0/2, x1/2,
+  // y0/2, y1/2: 5 bits each from bit 12) for the occlusion test; RPT 4: 16-bit
+  // entry indices, no occlusion test (the list would not fit the LDS budget).
+  constexpr bool kCull = RPT <= 2;
+  constexpr int kListLen = RPT * kVsdThreads;  // >= 2 * nm (launch_vsd)
+  using ListT = typename std::conditional<kCull, uint32_t, uint16_t>::type;
+  __shared__ __attribute__((aligned(4))) ListT s_list[kListLen];
+  __shared__ float s_zr[2][2];  // per pose: depth range of the meshlet corners (min, max)
   __shared__ int s_next;
   __shared__ __attribute__((aligned(16))) float s_pose[2][12];
   __shared__ int s_roi[4];
@@ -279,7 +384,9 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   const int W = a.width, H = a.height, nm = o.nm;
   // Object arrays live in global memory: address-space-1 views give
   // global_load (vmcnt only) instead of flat_load for pointers read from memory.
-  const gptr<const f32x4> g_mvtx = (gptr<const f32x4>)o.mlet_vtx;
+  // vertex blocks are float32x4 at a 16-B stride; only x, y, z are loaded
+  // (global_load_dwordx3), so no register is held by the padding word
+  const gptr<const f32x3> g_mvtx3 = (gptr<const f32x3>)o.mlet_vtx;
   const gptr<const uint32_t> g_mtri = (gptr<const uint32_t>)o.mlet_tri;
   const gptr<const float> g_mlet = (gptr<const float>)o.mlet;
   const int64_t fidx = a.frame_idx[b];
@@ -316,24 +423,53 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   if (tid == 0) {
     s_roi[0] = s_roi[1] = 0x7FFFFFFF;
     s_roi[2] = s_roi[3] = -1;
+    s_zr[0][0] = s_zr[1][0] = INFINITY;
+    s_zr[0][1] = s_zr[1][1] = 0.0f;
   }
   __syncthreads();
 
-  // 1. per-pose meshlet rectangles (kept in registers: entry tid + 256 j) + ROI.
+  // 1. per-pose meshlet rectangles (kept in registers: entry tid + 512 j) + ROI,
+  // and each entry's nearest corner depth (queue order, see BOPX_VSD_PRIO above).
   short4 rect[RPT];
+  float zmin[RPT];
   int roi[4] = {INT32_MAX, INT32_MAX, -1, -1};
+  float zr[4] = {INFINITY, -INFINITY, INFINITY, -INFINITY};  // pose 0 min, max; pose 1
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
     const int i = tid + j * kVsdThreads;
     rect[j] = make_short4(1, 1, 0, 0);
+    zmin[j] = -INFINITY;
     if (i < 2 * nm && !(COST == kCostGtInfo && i < nm)) {  // GT-info: gt pose only
       const int r = i >= nm, m = i - r * nm;
-      rect[j] = meshlet_rect(g_mlet + 24 * (int64_t)m, s_pose[r], c32, W, H);
+      rect[j] = meshlet_rect(g_mlet + 24 * (int64_t)m, s_pose[r], c32, W, H, zmin[j]);
       if (rect[j].x <= rect[j].z && rect[j].y <= rect[j].w) {
         roi[0] = min(roi[0], (int)rect[j].x);
         roi[1] = min(roi[1], (int)rect[j].y);
         roi[2] = max(roi[2], (int)rect[j].z);
         roi[3] = max(roi[3], (int)rect[j].w);
+        if (zmin[j] > 0.0f) {  // finite (every corner in front of the camera)
+          zr[2 * r] = fminf(zr[2 * r], zmin[j]);
+          zr[2 * r + 1] = fmaxf(zr[2 * r + 1], zmin[j]);
+        }
+      }
+    }
+  }
+  if constexpr (kCull) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float o = __shfl_xor(zr[k], off, 64);
+        zr[k] = (k & 1) ? fmaxf(zr[k], o) : fminf(zr[k], o);
+      }
+    }
+    // positive floats (or +-inf) order like their int bits: LDS int atomics
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        int* z = reinterpret_cast<int*>(&s_zr[0][0]) + k;
+        if (k & 1) atomicMax(z, __float_as_int(fmaxf(zr[k], 0.0f)));
+        else atomicMin(z, __float_as_int(zr[k]));
       }
     }
   }
@@ -357,6 +493,15 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
   for (int i = tid; i < 2 * kTileStride * kTileH; i += kVsdThreads) (&s_dep[0][0])[i] = 0u;
   __syncthreads();
   const int rx0 = s_roi[0], ry0 = s_roi[1], rx1 = s_roi[2], ry1 = s_roi[3];
+  // far half of each pose's depth range (wave-uniform thresholds)
+  uint32_t far_bits = 0;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int i = tid + j * kVsdThreads;
+    const int r = i >= nm;
+    const float zmid = 0.5f * (s_zr[r][0] + s_zr[r][1]);
+    far_bits |= (uint32_t)(zmin[j] > zmid) << j;
+  }
   double thr[NT];  // wave-uniform (SGPRs)
 #pragma unroll
   for (int k = 0; k < NT; ++k) {
@@ -399,17 +544,25 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         const short4 rc = rect[j];
         if (rc.x <= tx1 && rc.z >= tx0 && rc.y <= ty1 && rc.w >= ty0 && rc.x <= rc.z &&
             rc.y <= rc.w) {
-#if BOPX_VSD_LPT
-          const int ow = min((int)rc.z, tx1) - max((int)rc.x, tx0) + 1;
-          const int oh = min((int)rc.w, ty1) - max((int)rc.y, ty0) + 1;
-          if (ow * oh >= BOPX_VSD_LPT)
-            s_list[atomicAdd(&s_nlist, 1)] = (uint16_t)(tid + j * kVsdThreads);
+          const uint32_t far = (far_bits >> j) & 1u;
+          ListT word = (ListT)(tid + j * kVsdThreads);
+          if constexpr (kCull) {
+            const uint32_t x0 = (uint32_t)(max((int)rc.x, tx0) - tx0) >> 1;
+            const uint32_t x1 = (uint32_t)(min((int)rc.z, tx1) - tx0) >> 1;
+            const uint32_t y0 = (uint32_t)(max((int)rc.y, ty0) - ty0) >> 1;
+            const uint32_t y1 = (uint32_t)(min((int)rc.w, ty1) - ty0) >> 1;
+            word |= (far << 11) | (x0 << 12) | (x1 << 17) | (y0 << 22) | (y1 << 27);
+          }
+          bool front = !far;
+          if (BOPX_VSD_LPT_ORDER) {
+            const int ow = min((int)rc.z, tx1) - max((int)rc.x, tx0) + 1;
+            const int oh = min((int)rc.w, ty1) - max((int)rc.y, ty0) + 1;
+            front = ow * oh >= 1024;
+          }
+          if (front)
+            s_list[atomicAdd(&s_nlist, 1)] = word;
           else
-            s_list[2 * kMaxMeshlets - 1 - atomicAdd(&s_nsmall, 1)] =
-                (uint16_t)(tid + j * kVsdThreads);
-#else
-          s_list[atomicAdd(&s_nlist, 1)] = (uint16_t)(tid + j * kVsdThreads);
-#endif
+            s_list[kListLen - 1 - atomicAdd(&s_nsmall, 1)] = word;
         }
       }
       __syncthreads();
@@ -419,49 +572,64 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       // three fixed-stride vertex blocks once (lane = vertex) into LDS, tests
       // every triangle's bbox against the tile, compacts the hits (ballot rank)
       // and only then sets up and rasterises them, one triangle per lane.
-      const int nbig = __builtin_amdgcn_readfirstlane(s_nlist);
-      const int nl =
-          __builtin_amdgcn_readfirstlane(VSD_DIAG(1) ? 0 : s_nlist + (BOPX_VSD_LPT ? s_nsmall : 0));
+      const int nnear = __builtin_amdgcn_readfirstlane(s_nlist);
+      const int nl = __builtin_amdgcn_readfirstlane(VSD_DIAG(1) ? 0 : s_nlist + s_nsmall);
       for (;;) {
         int base = 0;
         if (lane == 0) base = atomicAdd(&s_next, kGroup);
         base = __builtin_amdgcn_readfirstlane(base);
+        VSD_STAMP(12);
         if (base >= nl) break;
         if (BOPX_VSD_PRIO && base + kGroup * kVsdWaves >= nl) __builtin_amdgcn_s_setprio(BOPX_VSD_PRIO);
-        f32x4 v[kGroup];
+        f32x3 v[kGroup];
         uint32_t pk[kGroup];
         int pose[kGroup];
         int ent[kGroup];
-        if constexpr (BOPX_VSD_LPT != 0) {
+        uint32_t word[kGroup];
 #pragma unroll
-          for (int g = 0; g < kGroup; ++g) {
-            const int q = min(base + g, nl - 1);
-            ent[g] = s_list[q < nbig ? q : 2 * kMaxMeshlets - 1 - (q - nbig)];
-          }
-        } else if constexpr (kGroup == 2) {  // base is even: one 4-byte read of both entries
-          const uint32_t pr = *reinterpret_cast<const uint32_t*>(&s_list[base]);
-          ent[0] = (int)(pr & 0xFFFFu);
-          ent[1] = base + 1 < nl ? (int)(pr >> 16) : ent[0];
-        } else {
-#pragma unroll
-          for (int g = 0; g < kGroup; ++g) ent[g] = s_list[min(base + g, nl - 1)];
+        for (int g = 0; g < kGroup; ++g) {
+          const int q = min(base + g, nl - 1);
+          word[g] = __builtin_amdgcn_readfirstlane(
+              (uint32_t)s_list[q < nnear ? q : kListLen - 1 - (q - nnear)]);
         }
         int mlt[kGroup];
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
-          const int e = __builtin_amdgcn_readfirstlane(ent[g]);
+          const int e = (int)(word[g] & 0x7FFu);
           pose[g] = __builtin_amdgcn_readfirstlane(e >= nm ? 1 : 0);  // uniform (SGPR)
           mlt[g] = e - pose[g] * nm;
+          ent[g] = e;
         }
         // all loads of the group in flight before the first use
 #pragma unroll
         for (int g = 0; g < kGroup; ++g)
-          v[g] = ld_off(g_mvtx + mlt[g] * kMeshletVerts, (uint32_t)lane * 16u);
+          v[g] = ld_off(g_mvtx3 + mlt[g] * kMeshletVerts, (uint32_t)lane * 16u);
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
           pk[g] = ld_off(g_mtri + mlt[g] * kMeshletTris, (uint32_t)lane * 4u);  // entry is valid
           if (base + g >= nl) pk[g] = 0xFFFFFFFFu;  // (clamped duplicate, no triangles)
         }
+        // occlusion test of far entries, part 1: the q reads of the region's
+        // first 8 steps go out now, behind the vertex loads, and are compared
+        // once the vertex 1/Z maximum is known (after the staging)
+        uint32_t qmin[kGroup];
+        bool test[kGroup];
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g) {
+          qmin[g] = 0xFFFFFFFFu;
+          test[g] = false;
+          if constexpr (kCull) {
+            test[g] = a.cull && ((word[g] >> 11) & 1u) && base + g < nl;
+            if (test[g])
+              qmin[g] = region_min8(s_dep[pose[g]],
+                                    make_region(word[g], tx1 - tx0 + 1, ty1 - ty0 + 1), 0, lane);
+          }
+        }
+        if (VSD_DIAG(8)) {  // diagnostics: time the vertex-block loads alone
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          VSD_STAMP(13);
+        }
+        float izl[kGroup];  // this lane's vertex 1/Z (0 for an invalid vertex)
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
 #if BOPX_VSD_POSE4
@@ -469,14 +637,34 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
           const float4 p0 = P[0], p1 = P[1], p2 = P[2];  // 3 x ds_read_b128
           const float Rf[12] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y,
                                 p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
-          w_stage[g * kMeshletVerts + lane] = r_vertex(Rf, c32, v[g].x, v[g].y, v[g].z);
+          const RVtx rv = r_vertex(Rf, c32, v[g].x, v[g].y, v[g].z);
 #else
-          w_stage[g * kMeshletVerts + lane] =
-              r_vertex(s_pose[pose[g]], c32, v[g].x, v[g].y, v[g].z);
+          const RVtx rv = r_vertex(s_pose[pose[g]], c32, v[g].x, v[g].y, v[g].z);
 #endif
+          w_stage[g * kMeshletVerts + lane] = rv;
+          izl[g] = rv.iz;
         }
         wave_lds_sync();
         VSD_STAMP(8);
+        if constexpr (kCull) {
+          // occlusion test of the far entries (see BOPX_VSD_PRIO above)
+#pragma unroll
+          for (int g = 0; g < kGroup; ++g) {
+            if (test[g]) {
+              const uint32_t qb =
+                  __float_as_uint(wave_max_nonneg_f32(izl[g]) * 1.00390625f);  // (1 + 2^-8) izmax
+              if (__builtin_amdgcn_ballot_w64(qmin[g] < qb) == 0) {
+                // first 8 blocks covered; a larger region continues from block 8
+                const Region rg = make_region(word[g], tx1 - tx0 + 1, ty1 - ty0 + 1);
+                if (rg.nb <= 8 || region_covered(s_dep[pose[g]], rg, 8, qb, lane)) {
+                  if (a.cull == 1) pk[g] = 0xFFFFFFFFu;  // no triangle of it can change the tile
+                  if (VSD_DIAG(4) && lane == 0) atomicAdd(&g_vsd_stats[9], 1ull);
+                }
+              }
+            }
+          }
+          VSD_STAMP(14);
+        }
         int cnt = 0;
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
@@ -519,9 +707,13 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
               atomicAdd(&g_vsd_stats[2], 1ull);
               atomicAdd(&g_vsd_stats[3], (unsigned long long)(cc1 - cc0 + 1) * (rr1 - rr0 + 1));
             }
-            if (ok && T.small) atomicAdd(&g_vsd_stats[4], (unsigned long long)(rr1 - rr0 + 1));
+            if (ok && T.small && T.regular)
+              atomicAdd(&g_vsd_stats[4], (unsigned long long)(rr1 - rr0 + 1));
           }
-          if (ok && !T.small) {  // extent >= 128 px: int64 edges, walked by its own lane
+          // extent >= 128 px (int64 edges) or an irregular sliver (clamped q):
+          // walked by its own lane with the full spec arithmetic (r_raster)
+          const bool fast = T.small & T.regular;
+          if (ok && !fast) {
             uint32_t* dep = s_dep[r];
             r_raster(T, cc0, cc1, rr0, rr1, [&](int col, int row, float q) {
               if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], 1ull);
@@ -530,7 +722,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
           }
           // Row items: publish one record per small triangle, number its rows
           // (wave prefix sum), then deal the rows out one per lane.
-          const bool rows = ok && T.small;
+          const bool rows = ok && fast;
           const int h = rows ? rr1 - rr0 + 1 : 0;
           int inc = h;
 #pragma unroll
@@ -561,8 +753,11 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
             }
             for (int p = lane; p < wn; p += 64) {
               const RRow rec = s_rec[wave][s_own[wave][p]];
-              const int fr = r_walk_row_max(rec, wb + p - (int)(rec.meta >> 19),
-                                            s_dep[(rec.meta >> 18) & 1u]);
+              const int fr =
+                  VSD_DIAG(16) ? r_walk_row_max<true>(rec, wb + p - (int)(rec.meta >> 19),
+                                                      s_dep[(rec.meta >> 18) & 1u])
+                               : r_walk_row_max(rec, wb + p - (int)(rec.meta >> 19),
+                                                s_dep[(rec.meta >> 18) & 1u]);
               if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
             }
           }
@@ -625,6 +820,46 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
         }
       }
       wave_lds_sync();
+      auto ps_of = [](int p) { return (p >> 6) * kTileStride + (p & 63); };
+      auto dt_of = [&](int p) {
+        return ld_off(tframe, (uint32_t)(__mul24(p >> 6, IW) + (p & 63)) * 4u);
+      };
+      auto vsd_px = [&](int p, uint32_t qe, uint32_t qg, float dtest) {
+        const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
+        const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
+        const double pX = w_pX[p % kTileW];
+        const double pY = w_pY[p / kTileW];
+        const double dist_t = dist_of(pX, pY, dtest);
+        const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
+        const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
+        const bool vg = visib19t(dist_t, dist_g, a.dthr);
+        bool ve = visib19t(dist_t, dist_e, a.dthr);
+        ve = ve || (vg && dist_e > 0.0);  // visibility.py:74
+        c_union += (vg || ve);
+        if (vg && ve) {
+          ++c_inter;
+          double dd = fabs(dist_g - dist_e);
+          if constexpr (COST == 0) {
+            if (divide) {  // rare: a real branch, not a speculated division
+              dd /= diam;
+              asm volatile("" : "+v"(dd));
+            }
+#pragma unroll
+            for (int k = 0; k < NT; ++k)
+              c_tau[k >> 1] += (uint32_t)(dd >= thr[k]) << (16 * (k & 1));
+          } else {
+            if (a.normalized) dd /= a.diameters[b];
+#pragma unroll
+            for (int k = 0; k < kMaxTaus; ++k) {
+              if (k < a.n_tau) {
+                const double cst = dd / a.taus[k];
+                lin[k] += cst > 1.0 ? 1.0 : cst;
+              }
+            }
+          }
+        }
+      };
+      if constexpr (COST == kCostCover || COST == kCostGtInfo || !BOPX_VSD_PIXPIPE) {
       for (int i = lane; i < npix; i += 64) {
         const int p = pix[i];
         const int row = ty0 + p / kTileW, col = tx0 + p % kTileW;
@@ -676,39 +911,36 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
           }
           continue;
         }
-        const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
-        const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
-        const float dtest =
-            ld_off(tframe, (uint32_t)(__mul24(p / kTileW, IW) + p % kTileW) * 4u);
-        const double pX = w_pX[p % kTileW];
-        const double pY = w_pY[p / kTileW];
-        const double dist_t = dist_of(pX, pY, dtest);
-        const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
-        const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
-        const bool vg = visib19t(dist_t, dist_g, a.dthr);
-        bool ve = visib19t(dist_t, dist_e, a.dthr);
-        ve = ve || (vg && dist_e > 0.0);  // visibility.py:74
-        c_union += (vg || ve);
-        if (vg && ve) {
-          ++c_inter;
-          double dd = fabs(dist_g - dist_e);
-          if constexpr (COST == 0) {
-            if (divide) {  // rare: a real branch, not a speculated division
-              dd /= diam;
-              asm volatile("" : "+v"(dd));
+        if constexpr (COST == 0 || COST == 1) vsd_px(p, qe, qg, dt_of(p));
+      }
+      } else {
+        // VSD: software-pipelined over the wave's pixel list. Pixel i + 64's q
+        // pair and test depth are in flight (and pixel i + 128's index) while
+        // pixel i is evaluated: the chain index -> (q, depth) -> float64 math
+        // would otherwise pay an LDS and a global round trip per 64 pixels.
+        // Lane -> pixel assignment unchanged (i = lane + 64 k: deterministic sums).
+        if (npix > 0) {
+          const int last = npix - 1;
+          int p0 = pix[min(lane, last)];
+          int p1 = pix[min(lane + 64, last)];
+          uint32_t qe0 = s_dep[0][ps_of(p0)], qg0 = s_dep[1][ps_of(p0)];
+          float dt0 = dt_of(p0);
+          for (int i = lane; i - lane < npix; i += 64) {
+            // next pixel's loads (clamped indices: unpredicated, no serialising waits)
+            const uint32_t qe1 = s_dep[0][ps_of(p1)], qg1 = s_dep[1][ps_of(p1)];
+            const float dt1 = dt_of(p1);
+            const int p2 = pix[min(i + 128, last)];
+            if (i < npix) {
+              s_dep[0][ps_of(p0)] = 0u;  // clean for the next tile (rows are wave-private)
+              s_dep[1][ps_of(p0)] = 0u;
+              if VSD_DIAG(4) atomicAdd(&g_vsd_stats[6], 1ull);
+              vsd_px(p0, qe0, qg0, dt0);
             }
-#pragma unroll
-            for (int k = 0; k < NT; ++k)
-              c_tau[k >> 1] += (uint32_t)(dd >= thr[k]) << (16 * (k & 1));
-          } else {
-            if (a.normalized) dd /= a.diameters[b];
-#pragma unroll
-            for (int k = 0; k < kMaxTaus; ++k) {
-              if (k < a.n_tau) {
-                const double cst = dd / a.taus[k];
-                lin[k] += cst > 1.0 ? 1.0 : cst;
-              }
-            }
+            p0 = p1;
+            qe0 = qe1;
+            qg0 = qg1;
+            dt0 = dt1;
+            p1 = p2;
           }
         }
       }
@@ -817,8 +1049,17 @@ constexpr int kBopTaus = 10;  // eval_calc_errors.py:47, np.arange(0.05, 0.51, 0
 template <int RPT>
 static void launch_vsd_rpt(const VsdArgs& a, int cost_type, hipStream_t s) {
   dim3 grid((unsigned)a.n), block(kVsdThreads);
+#if BOPX_VSD_DIAG
+  // occupancy experiment (diag builds): unused dynamic LDS per workgroup
+  static const unsigned dyn = [] {
+    const char* e = getenv("BOPX_VSD_DYNLDS");
+    return e ? (unsigned)atoi(e) : 0u;
+  }();
+#else
+  constexpr unsigned dyn = 0;
+#endif
   if (cost_type == 0 && a.n_tau <= kBopTaus)
-    hipLaunchKernelGGL((k_vsd<0, RPT, kBopTaus>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_vsd<0, RPT, kBopTaus>), grid, block, dyn, s, a);
   else if (cost_type == 0)
     hipLaunchKernelGGL((k_vsd<0, RPT, kMaxTaus>), grid, block, 0, s, a);
   else if (cost_type == 1)

@@ -2,7 +2,7 @@
 //
 // Replaces the OpenGL depth pass of renderer_vispy.py:433-538 /
 // renderer_py.py:422-555 (eye-Z depth, pixel-centre sampling, no culling,
-// GL_LESS z-test, background 0). The arithmetic follows raster spec v4 of
+// GL_LESS z-test, background 0). The arithmetic follows raster spec v5 of
 // DESIGN.md §4 exactly, so results are bit-identical to the CPU twin
 // (oracle/bopx_oracle.c: oracle_render_depth) whatever the tiling, culling or
 // triangle order:
@@ -14,16 +14,24 @@
 //     Triangles whose fixed-point extent is < 2^15 (128 px) step their edge
 //     functions incrementally in int32 (|E| < 2^31 is guaranteed there); larger
 //     ones evaluate them directly in int64 — the same integers either way;
-//   * 1/Z is affine in screen space: q = (iz0 + ga*dx) + gb*dy in float32 per
-//     fragment (gradients set up once per triangle in float32, spec v3);
-//   * the z-buffer keeps max q with an order-independent unsigned atomicMax on
-//     the positive-float bits; depth = 1.0f / q_max (= min of the per-fragment
+//   * 1/Z is affine in screen space: q = fma(ga, dx, fma(gb, dy, iz0)) in
+//     float32 per fragment (gradients set up once per triangle in float32);
+//   * a "regular" triangle (|ga|, |gb| <= 2^64 and 2^10 * 2area >= bw^2 + bh^2 of
+//     its snapped bbox) has |q - exact plane| <= 2^-9 dz + 2^-23 izmax (DESIGN.md
+//     §4), so q <= (1 + 2^-8) izmax; an irregular one (a sliver) has its q clamped
+//     to izmax (fminf). Every fragment is therefore bounded by its triangle's
+//     largest vertex 1/Z times (1 + 2^-8): the occlusion test of k_vsd relies on it;
+//   * the z-buffer keeps max q with an order-independent atomicMax on the
+//     positive-float bits; depth = 1.0f / q_max (= min of the per-fragment
 //     depths, RN(1/x) being monotone). 0 bits = no fragment = background.
 #pragma once
 #include "bopx_internal.h"
 
 namespace bopx {
 
+#ifndef BOPX_WALK_MASKED
+#define BOPX_WALK_MASKED 1
+#endif
 #ifndef BOPX_RCP_BALLOT
 #define BOPX_RCP_BALLOT 1
 #endif
@@ -93,8 +101,24 @@ struct RTri {
   int32_t dU[3], dV[3];     // edge vectors
   int32_t tl[3];            // top-left bias (1 = edge owns its centres)
   int32_t c0, c1, r0, r1;   // pixel bbox (unclipped)
+  float izmax;              // largest vertex 1/Z (the clamp of irregular triangles)
   bool small;               // int32 incremental path is exact
+  bool regular;             // q needs no clamp (spec v5)
 };
+
+// Spec v5 regularity (exact integers, the oracle's formula): finite moderate
+// gradients and 2^10 * area2 >= bw^2 + bh^2 (area2 = twice the fixed-point area,
+// bw / bh = fixed-point bbox extents).
+__device__ __forceinline__ bool r_regular(float ga, float gb, int64_t area2, int64_t bw,
+                                          int64_t bh) {
+  return fabsf(ga) <= 0x1p64f && fabsf(gb) <= 0x1p64f && (area2 << 10) >= bw * bw + bh * bh;
+}
+// The same for a small triangle (bw, bh < 2^15, area2 < 2^31) in uint32:
+// 2^10 a >= s  <=>  a >= ceil(s / 2^10), s = bw^2 + bh^2 < 2^31.
+__device__ __forceinline__ bool r_regular_small(float ga, float gb, uint32_t area2, uint32_t bw,
+                                                uint32_t bh) {
+  return fmaxf(fabsf(ga), fabsf(gb)) <= 0x1p64f && area2 >= (bw * bw + bh * bh + 1023u) >> 10;
+}
 
 // Returns false for triangles with no fragment inside the pixel rectangle
 // [x0,x1] x [y0,y1] (invalid vertex, zero area, or bbox outside the rectangle);
@@ -114,17 +138,20 @@ __device__ __forceinline__ bool r_setup(RVtx a, RVtx b, RVtx c, RTri& t, int x0,
     t.small = (maxU - minU) < 32768 && (maxV - minV) < 32768;
   }
   float farea;
+  int64_t farea_exact;
   bool neg;
   if (t.small) {  // |area| <= 2 * 32767^2 < 2^31; factors < 2^15: exact 24-bit multiplies
     const int32_t area = __mul24(b.U - a.U, c.V - a.V) - __mul24(b.V - a.V, c.U - a.U);
     if (area == 0) return false;
     neg = area < 0;
-    farea = (float)(neg ? -area : area);
+    farea_exact = neg ? -area : area;
+    farea = (float)farea_exact;
   } else {
     const int64_t area = (int64_t)(b.U - a.U) * (c.V - a.V) - (int64_t)(b.V - a.V) * (c.U - a.U);
     if (area == 0) return false;
     neg = area < 0;
-    farea = (float)(double)(neg ? -area : area);
+    farea_exact = neg ? -area : area;
+    farea = (float)(double)farea_exact;
   }
   if (neg) {
     const RVtx tmp = b;
@@ -138,6 +165,13 @@ __device__ __forceinline__ bool r_setup(RVtx a, RVtx b, RVtx c, RTri& t, int x0,
   t.U0 = a.U;
   t.V0 = a.V;
   t.iz0 = a.iz;
+  t.izmax = fmaxf(a.iz, fmaxf(b.iz, c.iz));
+  {
+    const int32_t minU = min(a.U, min(b.U, c.U)), maxU = max(a.U, max(b.U, c.U));
+    const int32_t minV = min(a.V, min(b.V, c.V)), maxV = max(a.V, max(b.V, c.V));
+    t.regular = r_regular(t.ga, t.gb, (int64_t)farea_exact, (int64_t)maxU - minU,
+                          (int64_t)maxV - minV);
+  }
   const RVtx s[3] = {b, c, a}, e[3] = {c, a, b};
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -166,14 +200,17 @@ __device__ __forceinline__ bool r_setup_touching(const RVtx a, const RVtx b0, co
   // small: factors < 2^15, exact 24-bit multiplies (other lanes: replaced below)
   const int32_t area32 = __mul24(b0.U - a.U, c0.V - a.V) - __mul24(b0.V - a.V, c0.U - a.U);
   bool neg = area32 < 0, nz = area32 != 0;
-  float farea = (float)(neg ? -area32 : area32);
+  const uint32_t aabs = (uint32_t)(neg ? -area32 : area32);
+  float farea = (float)aabs;
+  int64_t area64 = 0;
   if (__builtin_expect(__builtin_amdgcn_ballot_w64(!t.small) != 0, 0)) {
     if (!t.small) {
       const int64_t area =
           (int64_t)(b0.U - a.U) * (c0.V - a.V) - (int64_t)(b0.V - a.V) * (c0.U - a.U);
       neg = area < 0;
       nz = area != 0;
-      farea = (float)(double)(neg ? -area : area);
+      area64 = neg ? -area : area;
+      farea = (float)(double)area64;
     }
   }
   const RVtx b = neg ? c0 : b0, c = neg ? b0 : c0;
@@ -184,6 +221,12 @@ __device__ __forceinline__ bool r_setup_touching(const RVtx a, const RVtx b0, co
   t.U0 = a.U;
   t.V0 = a.V;
   t.iz0 = a.iz;
+  t.izmax = fmaxf(a.iz, fmaxf(b.iz, c.iz));
+  t.regular = r_regular_small(t.ga, t.gb, aabs, (uint32_t)(maxU - minU), (uint32_t)(maxV - minV));
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(!t.small) != 0, 0)) {
+    if (!t.small)
+      t.regular = r_regular(t.ga, t.gb, area64, (int64_t)maxU - minU, (int64_t)maxV - minV);
+  }
   const RVtx s[3] = {b, c, a}, e[3] = {c, a, b};
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -206,8 +249,12 @@ __device__ __forceinline__ bool r_touches(RVtx a, RVtx b, RVtx c, int x0, int x1
          max((minV + 127) >> 8, y0) <= min((maxV - 128) >> 8, y1);
 }
 
+// Spec v5 fragment value: fused plane evaluation, clamped to izmax for an
+// irregular triangle (fminf: a NaN becomes izmax).
 __device__ __forceinline__ float r_q(const RTri& t, int32_t px, int32_t py) {
-  return (t.iz0 + t.ga * (float)(px - t.U0)) + t.gb * (float)(py - t.V0);
+  const float q = __builtin_fmaf(t.ga, (float)(px - t.U0),
+                                 __builtin_fmaf(t.gb, (float)(py - t.V0), t.iz0));
+  return t.regular ? q : fminf(q, t.izmax);
 }
 
 // Visit every fragment of t inside the pixel rectangle [cc0,cc1] x [rr0,rr1]
@@ -303,10 +350,14 @@ __device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int 
 }
 
 // Walk row j of a record into the LDS z-buffer, branch-free: every column issues one
-// atomicMax, with 0 (a no-op on the 0-initialised buffer) where the pixel
-// centre is outside the triangle or q <= 0 / NaN. No exec-mask branches in the
-// loop body: the edge tests, the q plane and the LDS op form straight-line code.
-// dep: the pose's q tile (row pitch kTileStride). Returns the fragment count.
+// signed atomicMax, with 0 (a no-op on the 0-initialised buffer) where the pixel
+// centre is outside the triangle. Records are regular small triangles only, so q
+// is finite (never NaN): a q <= 0 (including -0.0) has a sign bit or is +0 and
+// loses the signed max against 0, which is exactly the spec's "fragments with
+// q <= 0 are dropped" without a compare. No exec-mask branches in the loop body.
+// dep: the pose's q tile (row pitch kTileStride). Returns the fragment count
+// (diagnostics).
+template <bool kNoAtomics = false>  // kNoAtomics: timing ablation only (diag builds)
 __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* dep) {
   // j < 64 and the tile row tr < 64 always; the masks (no-ops) tell the
   // compiler so, which keeps every multiply below on the full-rate 24-bit path.
@@ -321,26 +372,39 @@ __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* de
     e[k] = r.er[k] + (uint32_t)__mul24(dU256, j);
     sx[k] = (uint32_t)__mul24(-256, dV);
   }
-  const float qy = r.gb * (float)(r.py0v + (j << 8));
-  float fdx = (float)r.px0u;  // integers below 2^24: += 256 is exact
-  uint32_t* d = dep + __mul24(tr, kTileStride) + tc0;
+  // spec v5: q = fma(ga, dx, fma(gb, dy, iz0)); the row term once per row
+  const float qrow = __builtin_fmaf(r.gb, (float)(r.py0v + (j << 8)), r.iz0);
+  // the column pair's dx (integers below 2^24: += 512 is exact), packed so the
+  // two fmas and the step are one v_pk_fma_f32 / v_pk_add_f32 each
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  f32x2 fdx = {(float)r.px0u, (float)r.px0u + 256.0f};
+  const f32x2 ga2 = {r.ga, r.ga}, qrow2 = {qrow, qrow}, step2 = {512.0f, 512.0f};
+  int* d = reinterpret_cast<int*>(dep) + __mul24(tr, kTileStride) + tc0;
   int frags = 0;
   // Two columns per iteration (independent chains). The second column of the
   // last pair may be one past the rectangle and is not masked: past the
   // triangle's own bbox no pixel centre is inside it; past a tile clip it lands
   // in the padding column (tc0 + w = 64 < kTileStride) or, for a tile cut by
   // the ROI, in the column right of it, which the pixel compaction clears.
-  for (int i = 0; i < w; i += 2, fdx += 512.0f) {
+  for (int i = 0; i < w; i += 2, fdx += step2) {
     const uint32_t f0 = e[0] + sx[0], f1 = e[1] + sx[1], f2 = e[2] + sx[2];
     const int32_t m0 = min((int32_t)e[0], min((int32_t)e[1], (int32_t)e[2]));
     const int32_t m1 = min((int32_t)f0, min((int32_t)f1, (int32_t)f2));
-    const float q0 = (r.iz0 + r.ga * fdx) + qy;
-    const float q1 = (r.iz0 + r.ga * (fdx + 256.0f)) + qy;
-    const bool in0 = (m0 > 0) & (q0 > 0.0f);
-    const bool in1 = (m1 > 0) & (q1 > 0.0f);
-    frags += in0 + ((i + 1 < w) & in1);  // diagnostics
-    atomicMax(d + i, in0 ? __float_as_uint(q0) : 0u);
-    atomicMax(d + i + 1, in1 ? __float_as_uint(q1) : 0u);
+    const f32x2 q = __builtin_elementwise_fma(ga2, fdx, qrow2);
+    const float q0 = q.x, q1 = q.y;
+    frags += (m0 > 0) + ((i + 1 < w) & (m1 > 0));  // diagnostics (dead in the product build)
+#if BOPX_WALK_MASKED
+    if constexpr (kNoAtomics) {
+      asm volatile("" ::"v"(m0 > 0 ? q0 : 0.0f), "v"(m1 > 0 ? q1 : 0.0f), "v"(d + i));
+    } else {
+      // only covered centres touch LDS (fewer bank conflicts on the scattered rows)
+      if (m0 > 0) atomicMax(d + i, __float_as_int(q0));
+      if (m1 > 0) atomicMax(d + i + 1, __float_as_int(q1));
+    }
+#else
+    atomicMax(d + i, m0 > 0 ? __float_as_int(q0) : 0);
+    atomicMax(d + i + 1, m1 > 0 ? __float_as_int(q1) : 0);
+#endif
     e[0] = f0 + sx[0];
     e[1] = f1 + sx[1];
     e[2] = f2 + sx[2];

@@ -737,6 +737,15 @@ static float visib_thr32(double delta, int flags) {
   return f;
 }
 
+// k_vsd's occlusion test of far meshlet entries (bit-identical results either
+// way; off by default: on the bench workload its test cost equals the raster
+// work it saves). Read per call, so a test can compare the two:
+// BOPX_VSD_CULL=1 on, 0 off, 2 test only (timing).
+static int vsd_cull_enabled() {
+  const char* e = getenv("BOPX_VSD_CULL");
+  return e ? atoi(e) : 0;
+}
+
 static int fill_vsd_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height, double delta,
                          int flags, const double* taus, int n_tau, int normalized,
                          int cost_type) {
@@ -774,6 +783,7 @@ int bopx_vsd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doubl
   if (!c) return BOPX_E_INVALID;
   if (int r = set_dev(c)) return r;
   bopx::VsdArgs a{};
+  a.cull = vsd_cull_enabled();
   if (int r = fill_vsd_args(c, a, width, height, delta, flags, taus, n_tau, normalized,
                             cost_type))
     return r;
@@ -814,6 +824,7 @@ int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double*
                   frame_idx[i]);
   if (int r = set_dev(c)) return r;
   bopx::VsdArgs a{};
+  a.cull = vsd_cull_enabled();
   if (int r = fill_vsd_args(c, a, width, height, delta, flags, taus, n_tau, normalized,
                             cost_type))
     return r;
@@ -904,6 +915,7 @@ int bopx_gt_info_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const d
   if (!c) return BOPX_E_INVALID;
   if (int r = set_dev(c)) return r;
   bopx::VsdArgs a{};
+  a.cull = vsd_cull_enabled();
   if (int r = gt_info_args(c, a, width, height, delta, flags, canvas_scale)) return r;
   hipStream_t s = pick_stream(c, stream);
   if (masks && n > 0)
@@ -944,6 +956,7 @@ int bopx_gt_info_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const dou
                   frame_idx[i]);
   if (int r = set_dev(c)) return r;
   bopx::VsdArgs a{};
+  a.cull = vsd_cull_enabled();
   if (int r = gt_info_args(c, a, width, height, delta, flags, canvas_scale)) return r;
   std::vector<int32_t> slots;
   if (int r = map_slots(c, n, obj_ids, slots, false, true)) return r;
@@ -998,6 +1011,7 @@ int bopx_cover_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const dou
   if (!c) return BOPX_E_INVALID;
   if (int r = set_dev(c)) return r;
   bopx::VsdArgs a{};
+  a.cull = vsd_cull_enabled();
   if (int r = cover_args(c, a, width, height)) return r;
   a.objs = c->d_desc;
   a.max_nm = c->max_nm;
@@ -1032,6 +1046,7 @@ int bopx_cover_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const doubl
                   frame_idx[i]);
   if (int r = set_dev(c)) return r;
   bopx::VsdArgs a{};
+  a.cull = vsd_cull_enabled();
   if (int r = cover_args(c, a, width, height)) return r;
   std::vector<int32_t> slots;
   if (int r = map_slots(c, n, obj_ids, slots, false, true)) return r;

@@ -365,7 +365,7 @@ def run(p, device=0):
       ests_counter += n_ests
       errs = evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
                       models_info, sym_ids) if recs else []
-      if errs is None:  # another rank writes
+      if errs is None or _dist()[0] != 0:  # rank 0 writes (also for a scene with no records)
         continue
       scene_errs = [{"im_id": r["im_id"], "obj_id": r["obj_id"], "est_id": r["est_id"],
                      "score": r["score"], "errors": e} for r, e in zip(recs, errs)]

@@ -126,9 +126,11 @@ def get_error_signature(error_type, n_top, **kwargs):
 def calc_pts_diameter(pts):
   """Max pairwise distance of a point set (misc.py:279-306)."""
   pts = np.asarray(pts, np.float64)
-  best = 0.0
-  for i in range(0, len(pts), 2048):
-    d = ((pts[i:i + 2048, None, :] - pts[None, :, :]) ** 2).sum(-1)
+  best = -1.0  # the reference's value for an empty set
+  # rows per chunk: ~4M pairwise entries (~100 MB of float64 temporaries)
+  chunk = max(1, 2 ** 22 // max(len(pts), 1))
+  for i in range(0, len(pts), chunk):
+    d = ((pts[i:i + chunk, None, :] - pts[None, :, :]) ** 2).sum(-1)
     best = max(best, float(np.sqrt(d.max())))
   return best
 
@@ -150,7 +152,10 @@ def get_score_signature(correct_th, visib_gt_min):
 
 
 def calc_pts_diameter2(pts):
-  """Same value as calc_pts_diameter (misc.py:296-306 is the all-pairs variant)."""
+  """Same value as calc_pts_diameter (misc.py:296-306 is the all-pairs variant;
+  like its np.max over an empty cdist, an empty set raises ValueError)."""
+  if len(pts) == 0:
+    raise ValueError("zero-size array to reduction operation maximum which has no identity")
   return calc_pts_diameter(pts)
 
 

@@ -3,7 +3,8 @@ bop_toolkit_lib/visibility.py), evaluated by the gfx950 kernel k_visib.
 
 Bit-exact with the reference: the model and test distances are rounded to
 float32 before the difference (visibility.py:31/35) and compared with `delta`
-under NumPy >= 2 promotion rules (runtime.delta_flags).
+in float32, the legacy NumPy < 1.24 casting of the reference's pinned runtime
+(runtime.delta_flags).
 """
 from . import runtime
 

@@ -258,7 +258,7 @@ int oracle_vsd_depths(int W, int H, const float* depth_test, const float* depth_
 }
 
 /* ------------------------------------------------------------ depth raster */
-/* Spec v4:
+/* Spec v5:
  *  - R, t, fx, fy, cx, cy rounded to float32 (GL uniforms, renderer_vispy.py:441-442);
  *    vertices float32 (renderer_vispy.py:373).
  *  - X = ((r0*x + r1*y) + r2*z) + t, float32, no FMA; valid iff Z > 0.
@@ -271,8 +271,14 @@ int oracle_vsd_depths(int W, int H, const float* depth_test, const float* depth_
  *    all float32: inv = 1.0f / (float)(double)area, dza = iz_a - iz_c, dzb = iz_b - iz_c,
  *      ga = ((float)(Vb - Vc)*dza + (float)(Vc - Va)*dzb) * inv
  *      gb = ((float)(Uc - Ub)*dza + (float)(Ua - Uc)*dzb) * inv
- *    and per fragment  q = (iz_a + ga*(float)(px - Ua)) + gb*(float)(py - Va);
- *    fragments with q <= 0 are dropped.
+ *    and per fragment  q = fmaf(ga, (float)(px - Ua), fmaf(gb, (float)(py - Va), iz_a))
+ *    (spec v5: fused, one rounding per step).
+ *  - A triangle is regular iff |ga|, |gb| <= 2^64 and 2^10 * area >= bw^2 + bh^2
+ *    (area = twice the fixed-point area, bw / bh = fixed-point bbox extents, exact
+ *    integers); an irregular triangle's q is clamped: q = fminf(q, izmax), izmax the
+ *    largest vertex iz (a NaN q becomes izmax). Every fragment is then <= izmax * (1 + 2^-8)
+ *    (DESIGN.md §4), the bound k_vsd's occlusion test relies on.
+ *    Fragments with q <= 0 are dropped.
  *  - z-test: keep the largest q per pixel; depth = 1.0f / q_max (float32), 0 = background.
  *    Since RN(1/x) is monotone, this equals min over fragments of RN(1/q).
  * The HIP rasteriser (bop_toolkit_amd/csrc/raster.h) must match this bit for bit. */
@@ -340,6 +346,10 @@ static void raster_tri(ovtx a, ovtx b, ovtx c, int W, int H, float* qbuf) {
   if (r0 < 0) r0 = 0;
   if (c1 > W - 1) c1 = W - 1;
   if (r1 > H - 1) r1 = H - 1;
+  float izmax = a.iz > b.iz ? a.iz : b.iz;
+  if (c.iz > izmax) izmax = c.iz;
+  int64_t bw = (int64_t)maxU - minU, bh = (int64_t)maxV - minV;
+  int regular = fabsf(ga) <= 0x1p64f && fabsf(gb) <= 0x1p64f && (area << 10) >= bw * bw + bh * bh;
   int tl0 = top_left(&b, &c), tl1 = top_left(&c, &a), tl2 = top_left(&a, &b);
   for (int64_t r = r0; r <= r1; ++r) {
     int64_t py = 256 * r + 128;
@@ -349,7 +359,8 @@ static void raster_tri(ovtx a, ovtx b, ovtx c, int W, int H, float* qbuf) {
       if (!(w0 > 0 || (w0 == 0 && tl0))) continue;
       if (!(w1 > 0 || (w1 == 0 && tl1))) continue;
       if (!(w2 > 0 || (w2 == 0 && tl2))) continue;
-      float q = (a.iz + ga * (float)(px - a.U)) + gb * (float)(py - a.V);
+      float q = fmaf(ga, (float)(px - a.U), fmaf(gb, (float)(py - a.V), a.iz));
+      if (!regular) q = fminf(q, izmax);
       float* o = qbuf + (size_t)r * W + col;
       if (q > *o) *o = q;
     }

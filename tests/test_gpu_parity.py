@@ -68,6 +68,46 @@ def test_drop_in_point_errors(golden_errors):
     assert abs(pe.proj(Re, te_, Rg, tg, K, pts) - g["out_proj"][i]) < TOL
 
 
+def test_drop_in_cache_bounded(golden_errors, monkeypatch):
+  """Fresh arrays per call (model['pts'] * 1.0) share one content-keyed HBM slot,
+  and distinct point sets beyond the LRU bound evict (and free) old slots."""
+  from bop_toolkit_amd import pose_error as pe
+  from bop_toolkit_amd import runtime
+  g = golden_errors
+  pts = g["pts_0"]
+  Re, te_ = g["pose_est"][0][:9].reshape(3, 3), g["pose_est"][0][9:].reshape(3, 1)
+  Rg, tg = g["pose_gt"][0][:9].reshape(3, 3), g["pose_gt"][0][9:].reshape(3, 1)
+  want = pe.add(Re, te_, Rg, tg, pts)
+  n0 = runtime.resident_count()
+  for _ in range(50):
+    assert pe.add(Re, te_, Rg, tg, pts * 1.0) == want
+  assert runtime.resident_count() <= n0 + 1
+  monkeypatch.setattr(runtime, "MAX_RESIDENT", 8)
+  monkeypatch.setattr(runtime, "MAX_IDENTITY", 32)
+  for k in range(40):
+    shifted = pts + float(k + 1)
+    got = pe.add(Re, te_, Rg, tg, shifted)
+    assert abs(got - pe.add(Re, te_, Rg, tg, shifted.copy())) == 0.0
+    assert runtime.resident_count() <= 8
+  assert pe.add(Re, te_, Rg, tg, pts) == want
+
+
+def test_visibility_numpy_scalar_delta_float32(oracle_mod):
+  """delta = np.float64(15.3): compared in float32 (legacy NumPy casting of the
+  reference's runtime, runtime.delta_flags), so d_diff = float32(15.3) is visible."""
+  from bop_toolkit_amd import visibility
+  rng = np.random.default_rng(7)
+  dt = np.round(rng.uniform(400, 900, (48, 64)) * 64) / 64
+  d15 = float(np.float32(15.3))
+  dm = dt + np.where(rng.random(dt.shape) < 0.5, d15, 16.0)
+  dm[::5] = 0.0
+  dt[1::7] = 0.0
+  got = visibility.estimate_visib_mask_gt(dt, dm, np.float64(15.3))
+  want = oracle_mod.visib_mask(dt, dm, 15.3, delta_f64=False).astype(bool)
+  assert np.array_equal(got, want)
+  assert got[(dm - dt == d15) & (dm > 0)].all()
+
+
 def test_dist_and_visibility_bit_exact(golden_vsd):
   from bop_toolkit_amd import misc, visibility
   g = golden_vsd
@@ -120,10 +160,11 @@ def test_vsd_foreign_renderer_bit_exact(golden_vsd):
 
 
 def _scene(seed, n, W=640, H=480, n_lat=20, n_lon=40, K=None, xy=(150.0, 100.0),
-           z_range=(450.0, 1200.0)):
+           z_range=(450.0, 1200.0), mesh=None):
   from bop_toolkit_amd import synth
   rng = np.random.default_rng(seed)
-  pts, faces = synth.superellipsoid(n_lat, n_lon, (45.0, 35.0, 55.0), 0.7)
+  pts, faces = (synth.superellipsoid(n_lat, n_lon, (45.0, 35.0, 55.0), 0.7) if mesh is None
+                else mesh)
   Rg, tg = synth.gt_poses(rng, n, z_range=z_range, xy=xy)
   Re, te_ = synth.perturb(rng, Rg, tg)
   K = synth.LMO_K if K is None else K
@@ -240,6 +281,30 @@ def test_fused_vsd_step_thresholds_edge_cases(oracle_mod):
   for f64 in (False, True):
     _fused_vs_oracle(oracle_mod, 24, 8, 640, 480, synth.LMO_K, 20, 40, delta=15.3,
                      delta_f64=f64)
+
+
+def _bumpy_mesh(seed, n_lat=40, n_lon=80, amp=0.35):
+  """Non-convex closed mesh (radial noise on a superellipsoid): self-occlusion,
+  folds and near-edge-on slivers for the occlusion test and the spec v5 clamp."""
+  from bop_toolkit_amd import synth
+  rng = np.random.default_rng(seed)
+  pts, faces = synth.superellipsoid(n_lat, n_lon, (50.0, 40.0, 60.0), 0.8)
+  pts = pts * (1.0 + amp * rng.uniform(-1.0, 1.0, (len(pts), 1)))
+  return pts.astype(np.float32).astype(np.float64), faces
+
+
+@pytest.mark.parametrize("cull", ["1", "0"])
+def test_fused_vsd_occlusion_cull_exact(oracle_mod, monkeypatch, cull):
+  """k_vsd's occlusion test of far meshlet entries (BOPX_VSD_CULL) on a
+  non-convex mesh and on an almost flat one (edge-on views: irregular, clamped
+  triangles of raster spec v5): bit-exact vs the oracle either way."""
+  from bop_toolkit_amd import synth
+  monkeypatch.setenv("BOPX_VSD_CULL", cull)
+  out = _fused_vs_oracle(oracle_mod, 41, 24, 640, 480, synth.YCBV_K, 0, 0,
+                         mesh=_bumpy_mesh(3), z_range=(500.0, 900.0))
+  assert np.ptp(out) > 0.1
+  flat = synth.superellipsoid(30, 60, (70.0, 50.0, 0.02), 0.9)
+  _fused_vs_oracle(oracle_mod, 42, 24, 640, 480, synth.LMO_K, 0, 0, mesh=flat)
 
 
 def test_drop_in_vsd_with_hip_renderer(oracle_mod):

@@ -1,6 +1,7 @@
 """Host helpers of bop_toolkit_amd.misc that the callers use around the GPU
 path (misc.py:191-263, 279-306, 353-361): values checked by hand."""
 import numpy as np
+import pytest
 
 from bop_toolkit_amd import misc
 
@@ -23,9 +24,33 @@ def test_iou():
 def test_diameter_and_signatures(tmp_path):
   pts = np.array([[0.0, 0, 0], [3, 4, 0], [1, 1, 1]])
   assert misc.calc_pts_diameter(pts) == 5.0 == misc.calc_pts_diameter2(pts)
+  # reference misc.py:286 starts from -1.0; calc_pts_diameter2's np.max raises
+  assert misc.calc_pts_diameter(np.zeros((0, 3))) == -1.0
+  with pytest.raises(ValueError):
+    misc.calc_pts_diameter2(np.zeros((0, 3)))
+  # chunked evaluation (rows per chunk shrink with N) = brute force
+  rng = np.random.default_rng(3)
+  big = rng.normal(size=(3000, 3)) * [100.0, 50.0, 20.0]
+  d2 = ((big[:, None, :] - big[None, :, :]) ** 2).sum(-1)
+  assert misc.calc_pts_diameter(big) == float(np.sqrt(d2.max()))
   assert misc.get_score_signature([0.3], -1) == "th=0.300_min-visib=-1.000"
   assert misc.get_score_signature([5.0, 5.0], 0.1) == "th=5.000-5.000_min-visib=0.100"
   d = tmp_path / "a" / "b"
   misc.ensure_dir(str(d))
   misc.ensure_dir(str(d))
   assert d.is_dir()
+
+
+def test_delta_flags_follow_legacy_numpy_casting():
+  """float32 d_diff <= scalar delta compares in float32 for every scalar type
+  under NumPy < 1.24 (the reference's runtime): np.float64(15.3) included."""
+  from bop_toolkit_amd import _lib, runtime
+  for delta in (15, 15.0, 15.3, np.float64(15.3), np.float32(15.3), np.int64(15), np.int32(5),
+                float("inf"), np.float64("nan")):
+    assert runtime.delta_flags(delta) == 0, delta
+  assert runtime.delta_flags(1e39) == _lib.DELTA_F64
+  assert runtime.delta_flags(np.float64(-1e39)) == _lib.DELTA_F64
+  # what the float32 comparison means for delta = 15.3 (not representable):
+  # 15.3 rounds to 15.300000190734863 in float32, so d_diff = that value passes
+  d = np.float32(15.3)
+  assert d <= np.float32(np.float64(15.3)) and not float(d) <= 15.3

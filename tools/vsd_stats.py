@@ -41,11 +41,12 @@ def main():
   torch.cuda.synchronize()
   fn(ev.ctx.h, st, 1)
   names = ["tiles", "meshlet_entries", "tri_setups", "bbox_iters", "rows",
-           "fragments", "covered_px", "row_passes", "pass_max_w_sum"]
+           "fragments", "covered_px", "row_passes", "pass_max_w_sum", "culled_entries"]
   for i, k in enumerate(names):
     print("%-20s total %14d  per tuple %12.1f" % (k, st[i], st[i] / n))
   ph = ["clear+coeffs", "list", "raster work", "raster barrier", "pixel work",
-        "pixel barrier", "pre-loop", "epilogue", "r:stage", "r:compact", "r:setup", "r:walk"]
+        "pixel barrier", "pre-loop", "epilogue", "r:stage", "r:compact", "r:setup", "r:walk",
+        "r:claim", "r:vload", "r:occl"]
   tot = sum(st[16 + i] for i in range(16))
   for i, k in enumerate(ph):
     print("phase %-16s %6.1f %%  (%.3g cycles/wave-tuple)" % (k, 100.0 * st[16 + i] / max(1, tot),
