@@ -149,6 +149,23 @@ def build_workload(ev, objs, args, rank, torch):
   frames[torch.rand(frames.shape, device=dev, generator=g) < 0.1] = 0.0
   d["frames"] = frames.contiguous()
   d["host"] = {"obj": obj, "pe": pe, "pg": pg, "frame_idx": frame_idx, "cam": cam}
+  perm = os.environ.get("BOPX_BENCH_PERM")  # launch-order experiments
+  if perm:
+    cost = (np.array([objs[o]["diameter"] for o in obj]) / pg[:, 11]) ** 2
+    if perm == "lpt":
+      idx = np.argsort(-cost, kind="stable")
+    elif perm.startswith("lptobj"):
+      nb = int(perm[6:] or 4)
+      q = np.quantile(cost, np.linspace(0, 1, nb + 1)[1:-1])
+      bucket = nb - 1 - np.searchsorted(q, cost)
+      idx = np.lexsort((obj, bucket))
+    else:
+      idx = np.arange(n)
+    it = torch.as_tensor(idx, device=dev)
+    for k in ("slots", "pose_est", "pose_gt", "frame_idx", "K", "diameters"):
+      d[k] = d[k][it].contiguous()
+    d["host"] = {"obj": obj[idx], "pe": pe[idx], "pg": pg[idx], "frame_idx": frame_idx[idx],
+                 "cam": cam}
   torch.cuda.synchronize()
   return n, d
 

@@ -100,8 +100,16 @@ hipError_t launch_adi(const ObjDesc* objs, int64_t n, const int32_t* slots, cons
                       const double* pg, double* out, const int32_t* order, hipStream_t s);
 // order: nullptr (block k takes tuple k) or a launch order from launch_order_by_slot
 constexpr int kOrderMaxSlots = 16383;  // LDS buckets of k_order_by_slot
+constexpr int kOrderCostClasses = 48;  // half-octave classes of the projected area (VSD order)
+struct OrderCost {  // VSD inputs of the cost classes (pe == nullptr: order by slot only)
+  const double* pe;
+  const double* pg;
+  const int32_t* frame_idx;
+  const double* cam;
+  const double* dia;
+};
 hipError_t launch_order_by_slot(const int32_t* slots, int64_t n, int ns, int32_t* order,
-                                hipStream_t s);
+                                hipStream_t s, const OrderCost* cost = nullptr);
 hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s);  // or kCostCover
 hipError_t launch_cover_depths(int W, int H, const float* de, const float* dg,
                                long long* acc /* kCoverCols, device */, hipStream_t s);

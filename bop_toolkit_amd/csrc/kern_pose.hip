@@ -425,19 +425,41 @@ hipError_t launch_adi(const ObjDesc* objs, int64_t n, const int32_t* slots, cons
 // its own outputs, so results do not depend on it.
 constexpr int kOrderThreads = 1024;
 
+// Sort key of tuple i: its object slot, or, with VSD cost inputs, (cost class
+// descending, slot): the class is 2 log2 (half octaves) of the projected bounding-sphere
+// area (diameter * f / z)^2 in px^2 at the nearer of the two poses, so the
+// expensive tuples start first (LPT over the workgroup slots; a big tuple
+// starting last would set the launch's tail) while tuples of one object stay
+// adjacent within a class (meshlet data hot in L2).
+__device__ __forceinline__ int order_key(const int32_t* __restrict__ slots, int64_t i, int ns,
+                                         const OrderCost& oc) {
+  const int sl = (unsigned)slots[i] < (unsigned)ns ? slots[i] : ns;
+  if (!oc.pe) return sl;
+  const double z = fmin(oc.pe[12 * i + 11], oc.pg[12 * i + 11]);
+  const int64_t fi = oc.frame_idx[i];
+  const double f = fmax(oc.cam[4 * fi], oc.cam[4 * fi + 1]);
+  const double r = oc.dia[i] * f / z;
+  const double area = r * r;
+  int cls = kOrderCostClasses - 1;  // behind the camera / non-finite: most expensive
+  if (z > 0.0 && area == area && area < 1e18) {
+    // half-octave classes: 2 floor(log2 a) + (a >= sqrt(2) 2^floor(log2 a))
+    const unsigned ai = (unsigned)fmin(fmax(area, 1.0), 2147483647.0);
+    const int e = 31 - __clz(ai);
+    cls = min(kOrderCostClasses - 1, 2 * e + (area >= 1.4142135623730951 * (double)(1u << e)));
+  }
+  return (kOrderCostClasses - 1 - cls) * (ns + 1) + sl;
+}
+
 __global__ __launch_bounds__(kOrderThreads) void k_order_by_slot(const int32_t* __restrict__ slots,
-                                                                  int64_t n, int ns,
+                                                                  int64_t n, int ns, OrderCost oc,
                                                                   int32_t* __restrict__ order) {
-  extern __shared__ int s_cnt[];  // ns + 1 buckets
+  extern __shared__ int s_cnt[];  // one bucket per key
   __shared__ int s_wsum[kOrderThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nb = ns + 1;
+  const int nb = oc.pe ? kOrderCostClasses * (ns + 1) : ns + 1;
   for (int i = tid; i < nb; i += kOrderThreads) s_cnt[i] = 0;
   __syncthreads();
-  for (int64_t i = tid; i < n; i += kOrderThreads) {
-    const int sl = slots[i];
-    atomicAdd(&s_cnt[(unsigned)sl < (unsigned)ns ? sl : ns], 1);
-  }
+  for (int64_t i = tid; i < n; i += kOrderThreads) atomicAdd(&s_cnt[order_key(slots, i, ns, oc)], 1);
   __syncthreads();
   // exclusive scan: thread t owns buckets [t * per, (t + 1) * per)
   const int per = (nb + kOrderThreads - 1) / kOrderThreads;
@@ -459,18 +481,19 @@ __global__ __launch_bounds__(kOrderThreads) void k_order_by_slot(const int32_t* 
     run += v;
   }
   __syncthreads();
-  for (int64_t i = tid; i < n; i += kOrderThreads) {
-    const int sl = slots[i];
-    order[atomicAdd(&s_cnt[(unsigned)sl < (unsigned)ns ? sl : ns], 1)] = (int32_t)i;
-  }
+  for (int64_t i = tid; i < n; i += kOrderThreads)
+    order[atomicAdd(&s_cnt[order_key(slots, i, ns, oc)], 1)] = (int32_t)i;
 }
 
 hipError_t launch_order_by_slot(const int32_t* slots, int64_t n, int ns, int32_t* order,
-                                hipStream_t s) {
+                                hipStream_t s, const OrderCost* cost) {
   if (n <= 0) return hipSuccess;
   if (ns < 0 || ns > kOrderMaxSlots) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_order_by_slot, dim3(1), dim3(kOrderThreads), (ns + 1) * sizeof(int), s,
-                     slots, n, ns, order);
+  OrderCost oc{};
+  if (cost && (int64_t)kOrderCostClasses * (ns + 1) <= kOrderMaxSlots + 1) oc = *cost;
+  const int nb = oc.pe ? kOrderCostClasses * (ns + 1) : ns + 1;
+  hipLaunchKernelGGL(k_order_by_slot, dim3(1), dim3(kOrderThreads), nb * sizeof(int), s, slots, n,
+                     ns, oc, order);
   return hipGetLastError();
 }
 

@@ -293,7 +293,16 @@ constexpr int kVsdWaves = kVsdThreads / 64;
 constexpr int kRowWin = 256;  // row items numbered per window (LDS owner map)
 // covered-pixel list of a wave: its rows w, w + kVsdWaves, ... of the tile
 constexpr int kPixPerWave = (kTileH + kVsdWaves - 1) / kVsdWaves * kTileW;
-static_assert(sizeof(RRow) * 64 >= 2 * kPixPerWave, "pixel lists overlay the raster records");
+// Row records of the walk: in LDS (s_rec, 24 KiB per workgroup) or, with
+// BOPX_VSD_REGREC, kept in the set-up lane's registers and fetched by the
+// walking lane with ds_bpermute: the workgroup then fits 3 per CU (LDS <= 54 KiB).
+// Measured (round 2, same box): 1 % slower than LDS records at 2 workgroups
+// per CU; at 3 per CU the 80-VGPR budget spills (+32 %). Off by default.
+#ifndef BOPX_VSD_REGREC
+#define BOPX_VSD_REGREC 0
+#endif
+static_assert(BOPX_VSD_REGREC || sizeof(RRow) * 64 >= 2 * kPixPerWave,
+              "pixel lists overlay the raster records");
 static_assert(kVsdThreads % kTileW == 0, "pixel-pass rows are wave-uniform");
 constexpr int kGroup = BOPX_VSD_GROUP;  // (pose, meshlet) entries staged together per wave step
 // worst case (RPT) of meshlet rectangles per thread
@@ -302,7 +311,9 @@ constexpr int kRectsPerThread = (2 * kMaxMeshlets + kVsdThreads - 1) / kVsdThrea
 // an entry group during the raster, the tile's float64 column / row
 // coefficients during the pixel pass.
 constexpr int kStageBytes = kGroup * kMeshletVerts * (int)sizeof(RVtx) + kGroup * kMeshletTris * 4;
-constexpr int kCoefBytes = 8 * (kTileW + kTileH);
+// pixel pass: float64 column / row coefficients (+ the covered-pixel list
+// when the records are not in LDS)
+constexpr int kCoefBytes = 8 * (kTileW + kTileH) + (BOPX_VSD_REGREC ? 2 * kPixPerWave : 0);
 constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 #ifndef BOPX_VSD_POSE4
 #define BOPX_VSD_POSE4 1
@@ -343,13 +354,22 @@ constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 // smallest that covers 2 x the most meshlets of any registered object, so
 // objects of up to 16k triangles keep 6 fewer VGPRs live through the tile loop.
 template <int COST, int RPT, int NT>
-// Two workgroups per CU: 2 * kVsdThreads / 256 waves per SIMD (caps VGPRs at 128).
-__global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdArgs a) {
+// Workgroups per CU: 3 with register records and <= 512 meshlet entries
+// (6 waves per SIMD: VGPRs <= 80), else 2 (4 waves per SIMD: VGPRs <= 128).
+#ifndef BOPX_VSD_WG3
+#define BOPX_VSD_WG3 1
+#endif
+__global__ __launch_bounds__(kVsdThreads,
+                             (BOPX_VSD_REGREC && BOPX_VSD_WG3 && RPT == 1 ? 3 : 2) * kVsdThreads /
+                                 256)
+void k_vsd(VsdArgs a) {
   // q = 1/Z bits, 0 = empty; rows padded by one dword so lanes that walk the
   // same column on consecutive rows (row-split) hit different LDS banks.
   __shared__ uint32_t s_dep[2][kTileStride * kTileH];
   __shared__ __attribute__((aligned(16))) uint8_t s_wscr[kVsdWaves][kWaveScr];
+#if !BOPX_VSD_REGREC
   __shared__ RRow s_rec[kVsdWaves][64];          // set-up triangles of the current chunk
+#endif
   __shared__ uint8_t s_own[kVsdWaves][kRowWin];  // row item -> record (lane) of a window
   // Tile entry queue. RPT <= 2 (objects of <= 512 meshlets): 32-bit words
   // entry | far << 11 | rectangle in the tile at 2-px granularity (x0/2, x1/2,
@@ -732,13 +752,43 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
           }
           const int first = inc - h;
           const int nrow = __builtin_amdgcn_readlane(inc, 63);
+#if BOPX_VSD_REGREC
+          RRow own;  // this lane's record (defined in every lane: fetched with full exec)
+          r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first, own);
+#else
           if (rows) r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first, s_rec[wave][lane]);
+#endif
           for (int wb = 0; wb < nrow; wb += kRowWin) {
             wave_lds_sync();  // records written / previous window's owners consumed
             for (int k = max(first, wb); k < min(first + h, wb + kRowWin); ++k)
               s_own[wave][k - wb] = (uint8_t)lane;
             wave_lds_sync();
             const int wn = min(nrow - wb, kRowWin);
+#if BOPX_VSD_REGREC
+            // uniform loop: every lane takes part in the record fetch (ds_bpermute
+            // reads the owner's register, so owners must be active)
+            for (int p0 = 0; p0 < wn; p0 += 64) {
+              const int p = p0 + lane;
+              const bool valid = p < wn;
+              const RRow rec = r_fetch_row(own, s_own[wave][valid ? p : 0]);
+              if VSD_DIAG(4) {  // passes, sum over passes of the widest row
+                int wmax = valid ? (int)((rec.meta >> 12) & 63u) + 1 : 0;
+                for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, __shfl_xor(wmax, off, 64));
+                if (lane == 0) {
+                  atomicAdd(&g_vsd_stats[7], 1ull);
+                  atomicAdd(&g_vsd_stats[8], (unsigned long long)wmax);
+                }
+              }
+              if (valid) {
+                const int fr =
+                    VSD_DIAG(16) ? r_walk_row_max<true>(rec, wb + p - (int)(rec.meta >> 19),
+                                                        s_dep[(rec.meta >> 18) & 1u])
+                                 : r_walk_row_max(rec, wb + p - (int)(rec.meta >> 19),
+                                                  s_dep[(rec.meta >> 18) & 1u]);
+                if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
+              }
+            }
+#else
             if VSD_DIAG(4) {  // passes, sum over passes of the widest row
               for (int p0 = 0; p0 < wn; p0 += 64) {
                 int wmax = p0 + lane < wn
@@ -760,6 +810,7 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
                                                 s_dep[(rec.meta >> 18) & 1u]);
               if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
             }
+#endif
           }
           VSD_STAMP(11);
           wave_lds_sync();  // records are rewritten by the next chunk
@@ -798,7 +849,11 @@ __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256) void k_vsd(VsdA
       // list (ballot rank; the raster records are dead here), then evaluates
       // the list with full lanes. Wave-private: no block barrier, and the
       // pixel -> lane assignment is fixed (deterministic float64 sums).
+#if BOPX_VSD_REGREC
+      uint16_t* pix = reinterpret_cast<uint16_t*>(&s_wscr[wave][8 * (kTileW + kTileH)]);
+#else
       uint16_t* pix = reinterpret_cast<uint16_t*>(&s_rec[0][0]) + wave * kPixPerWave;
+#endif
       int npix = 0;
       {
         // lane = column, one wave-uniform tile row per step (rows w, w + 8, ...)

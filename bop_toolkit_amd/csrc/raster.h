@@ -349,6 +349,26 @@ __device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int 
            ((uint32_t)pose << 18) | ((uint32_t)first << 19);
 }
 
+// The record of lane `owner` of this wave, read from its registers
+// (ds_bpermute; every lane of the wave must be active).
+__device__ __forceinline__ RRow r_fetch_row(const RRow& own, int owner) {
+  const int addr = owner << 2;
+  auto f = [addr](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v); };
+  RRow r;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    r.er[k] = f(own.er[k]);
+    r.duv[k] = f(own.duv[k]);
+  }
+  r.px0u = (int32_t)f((uint32_t)own.px0u);
+  r.py0v = (int32_t)f((uint32_t)own.py0v);
+  r.iz0 = __uint_as_float(f(__float_as_uint(own.iz0)));
+  r.ga = __uint_as_float(f(__float_as_uint(own.ga)));
+  r.gb = __uint_as_float(f(__float_as_uint(own.gb)));
+  r.meta = f(own.meta);
+  return r;
+}
+
 // Walk row j of a record into the LDS z-buffer, branch-free: every column issues one
 // signed atomicMax, with 0 (a no-op on the 0-initialised buffer) where the pixel
 // centre is outside the triangle. Records are regular small triangles only, so q
