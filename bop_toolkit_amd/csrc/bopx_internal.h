@@ -107,6 +107,7 @@ struct OrderCost {  // VSD inputs of the cost classes (pe == nullptr: order by s
   const int32_t* frame_idx;
   const double* cam;
   const double* dia;
+  const int32_t* slot_rank;  // pe == nullptr: key = slot_rank[slot] (slots by descending cost)
 };
 hipError_t launch_order_by_slot(const int32_t* slots, int64_t n, int ns, int32_t* order,
                                 hipStream_t s, const OrderCost* cost = nullptr);

@@ -434,7 +434,7 @@ constexpr int kOrderThreads = 1024;
 __device__ __forceinline__ int order_key(const int32_t* __restrict__ slots, int64_t i, int ns,
                                          const OrderCost& oc) {
   const int sl = (unsigned)slots[i] < (unsigned)ns ? slots[i] : ns;
-  if (!oc.pe) return sl;
+  if (!oc.pe) return oc.slot_rank && sl < ns ? oc.slot_rank[sl] : sl;
   const double z = fmin(oc.pe[12 * i + 11], oc.pg[12 * i + 11]);
   const int64_t fi = oc.frame_idx[i];
   const double f = fmax(oc.cam[4 * fi], oc.cam[4 * fi + 1]);
@@ -490,7 +490,8 @@ hipError_t launch_order_by_slot(const int32_t* slots, int64_t n, int ns, int32_t
   if (n <= 0) return hipSuccess;
   if (ns < 0 || ns > kOrderMaxSlots) return hipErrorInvalidValue;
   OrderCost oc{};
-  if (cost && (int64_t)kOrderCostClasses * (ns + 1) <= kOrderMaxSlots + 1) oc = *cost;
+  if (cost && (!cost->pe || (int64_t)kOrderCostClasses * (ns + 1) <= kOrderMaxSlots + 1))
+    oc = *cost;
   const int nb = oc.pe ? kOrderCostClasses * (ns + 1) : ns + 1;
   hipLaunchKernelGGL(k_order_by_slot, dim3(1), dim3(kOrderThreads), nb * sizeof(int), s, slots, n,
                      ns, oc, order);

@@ -51,6 +51,7 @@ struct bopx_ctx {
   std::unordered_map<int, int> slot_of;
   std::vector<Object> objs;
   ObjDesc* d_desc = nullptr;
+  int32_t* d_rank = nullptr;  // slot -> rank by descending symmetry-error cost (nv * ns)
   size_t desc_cap = 0;
   int max_nf = 0;
   int max_ns = 0;  // most symmetries of a live object (MSSD/MSPD grid)
@@ -152,6 +153,12 @@ int make_order(bopx_ctx* c, int64_t n, const int32_t* slots, hipStream_t s, Laun
   return BOPX_OK;
 }
 
+bopx::OrderCost sym_order_cost(const bopx_ctx* c) {
+  bopx::OrderCost oc{};
+  oc.slot_rank = c->d_rank;
+  return oc;
+}
+
 int sync_desc(bopx_ctx* c) {
   std::vector<ObjDesc> h(c->objs.size());
   int max_nf = 0, max_ns = 0, max_nm = 0;
@@ -182,13 +189,28 @@ int sync_desc(bopx_ctx* c) {
   c->max_nm = max_nm;
   if (h.size() > c->desc_cap) {
     if (c->d_desc) HIPCHK(c, hipFree(c->d_desc));
+    if (c->d_rank) HIPCHK(c, hipFree(c->d_rank));
+    c->d_rank = nullptr;
     size_t cap = std::max<size_t>(64, h.size() * 2);
     HIPCHK(c, hipMalloc(&c->d_desc, cap * sizeof(ObjDesc)));
+    HIPCHK(c, hipMalloc(&c->d_rank, cap * sizeof(int32_t)));
     c->desc_cap = cap;
   }
-  if (!h.empty())
+  // MSSD / MSPD launch order: the slots by descending work (nv * ns; free slots
+  // last), so the heavy objects' tuples start first (LPT; a heavy tail of
+  // continuous-symmetry tuples otherwise sets the end of the launch)
+  std::vector<int32_t> by_cost(h.size()), rank(h.size());
+  for (size_t i = 0; i < h.size(); ++i) by_cost[i] = (int32_t)i;
+  std::stable_sort(by_cost.begin(), by_cost.end(), [&](int32_t x, int32_t y) {
+    return (int64_t)h[x].nv * std::max(h[x].ns, 1) > (int64_t)h[y].nv * std::max(h[y].ns, 1);
+  });
+  for (size_t i = 0; i < h.size(); ++i) rank[by_cost[i]] = (int32_t)i;
+  if (!h.empty()) {
     HIPCHK(c, hipMemcpyAsync(c->d_desc, h.data(), h.size() * sizeof(ObjDesc),
                              hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_rank, rank.data(), rank.size() * sizeof(int32_t),
+                             hipMemcpyHostToDevice, c->stream));
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return BOPX_OK;
 }
@@ -330,6 +352,7 @@ void bopx_destroy(bopx_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   for (Object& o : c->objs) free_object(o);
   if (c->d_desc) (void)hipFree(c->d_desc);
+  if (c->d_rank) (void)hipFree(c->d_rank);
   if (c->ws.p) (void)hipFree(c->ws.p);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -637,7 +660,8 @@ static int point_batch(bopx_ctx* c, int kind, int64_t n, const int32_t* obj_ids,
   HIPCHK(c, hipMemcpyAsync(d_pg, pg, 96 * n, hipMemcpyHostToDevice, s));
   if (needK) HIPCHK(c, hipMemcpyAsync(d_K, K, 72 * n, hipMemcpyHostToDevice, s));
   LaunchOrder ord;
-  if (int r = make_order(c, n, d_s, s, ord)) return r;
+  const bopx::OrderCost sc = sym_order_cost(c);
+  if (int r = make_order(c, n, d_s, s, ord, kind <= 1 ? &sc : nullptr)) return r;
   hipError_t e;
   if (kind <= 1)
     e = bopx::launch_sym_error(kind, c->d_desc, c->max_ns, n, d_s, d_pe, d_pg, d_K, d_out, ord.p,
@@ -680,7 +704,8 @@ int bopx_mssd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doub
   if (int r = set_dev(c)) return r;
   hipStream_t s = pick_stream(c, stream);
   LaunchOrder ord;
-  if (int r = make_order(c, n, slots, s, ord)) return r;
+  const bopx::OrderCost sc = sym_order_cost(c);
+  if (int r = make_order(c, n, slots, s, ord, &sc)) return r;
   HIPCHK(c, bopx::launch_sym_error(0, c->d_desc, c->max_ns, n, slots, pe, pg, nullptr, out, ord.p,
                                    s));
   return BOPX_OK;
@@ -691,7 +716,8 @@ int bopx_mspd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doub
   if (int r = set_dev(c)) return r;
   hipStream_t s = pick_stream(c, stream);
   LaunchOrder ord;
-  if (int r = make_order(c, n, slots, s, ord)) return r;
+  const bopx::OrderCost sc = sym_order_cost(c);
+  if (int r = make_order(c, n, slots, s, ord, &sc)) return r;
   HIPCHK(c, bopx::launch_sym_error(1, c->d_desc, c->max_ns, n, slots, pe, pg, K, out, ord.p, s));
   return BOPX_OK;
 }
