@@ -39,6 +39,9 @@
 
 namespace bopx {
 
+#ifndef BOPX_SCAN_DPP
+#define BOPX_SCAN_DPP 1
+#endif
 #ifndef BOPX_VSD_THREADS
 #define BOPX_VSD_THREADS 512
 #endif
@@ -262,6 +265,29 @@ __device__ __forceinline__ bool region_covered(const uint32_t* dep, const Region
   return true;
 }
 
+// Inclusive prefix sum over the 64 lanes (full exec), all in DPP: row_shr 1, 2,
+// 4, 8 inside each row of 16 lanes, then row_bcast 15 / 31 carry the row totals
+// into the rows above. No LDS round trips (the __shfl_up scan is six dependent
+// ds_bpermute + lgkmcnt waits per call).
+__device__ __forceinline__ int wave_incl_scan(int x) {
+#if BOPX_SCAN_DPP
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+#else
+  const int lane = __lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(x, d, 64);
+    if (lane >= d) x += v;
+  }
+#endif
+  return x;
+}
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
@@ -341,12 +367,14 @@ constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 #ifndef BOPX_VSD_PIXPIPE
 #define BOPX_VSD_PIXPIPE 0
 #endif
-// Queue order: 0 = near entries first (depth), 1 = entries overlapping the tile
-// by >= 1024 px first (round-1 LPT order, 2 % faster without the occlusion
-// test); the occlusion test applies to far entries either way.
-#ifndef BOPX_VSD_LPT_ORDER
-#define BOPX_VSD_LPT_ORDER 1
-#endif
+// Queue order (VsdArgs::qorder, wave-uniform): 0 = near entries first (depth),
+// 1 = entries overlapping the tile by >= a quarter of its area first (longest
+// first for the raster-end barrier: 1,024 px on the 64x64 tile, round-1 LPT
+// order, 2 % faster without the occlusion test); the occlusion test applies to
+// far entries either way. The z-buffer is order-independent (atomicMax on the
+// q bits), so both orders give bit-identical results
+// (test_fused_vsd_occlusion_cull_exact runs both).
+constexpr int kLptOverlap = kTileW * kTileH / 4;
 
 // COST: 0 = step, 1 = tlinear, kCostCover = silhouette overlap, kCostGtInfo = GT stats.
 // NT (step cost): thresholds compared per pixel (>= n_tau; 10 for the BOP taus).
@@ -574,10 +602,10 @@ void k_vsd(VsdArgs a) {
             word |= (far << 11) | (x0 << 12) | (x1 << 17) | (y0 << 22) | (y1 << 27);
           }
           bool front = !far;
-          if (BOPX_VSD_LPT_ORDER) {
+          if (a.qorder) {
             const int ow = min((int)rc.z, tx1) - max((int)rc.x, tx0) + 1;
             const int oh = min((int)rc.w, ty1) - max((int)rc.y, ty0) + 1;
-            front = ow * oh >= 1024;
+            front = ow * oh >= kLptOverlap;
           }
           if (front)
             s_list[atomicAdd(&s_nlist, 1)] = word;
@@ -744,12 +772,7 @@ void k_vsd(VsdArgs a) {
           // (wave prefix sum), then deal the rows out one per lane.
           const bool rows = ok && fast;
           const int h = rows ? rr1 - rr0 + 1 : 0;
-          int inc = h;
-#pragma unroll
-          for (int d = 1; d < 64; d <<= 1) {
-            const int v = __shfl_up(inc, d, 64);
-            if (lane >= d) inc += v;
-          }
+          const int inc = wave_incl_scan(h);
           const int first = inc - h;
           const int nrow = __builtin_amdgcn_readlane(inc, 63);
 #if BOPX_VSD_REGREC

@@ -773,6 +773,13 @@ static int vsd_cull_enabled() {
   return e ? atoi(e) : 0;
 }
 
+// k_vsd tile entry-queue order (kern_vsd.hip kLptOverlap): 1 = large overlaps
+// first (default), 0 = near entries first. Read per call like BOPX_VSD_CULL.
+static int vsd_queue_order() {
+  const char* e = getenv("BOPX_VSD_QORDER");
+  return e ? (atoi(e) != 0) : 1;
+}
+
 // k_vsd launch order: cost classes (projected bounding-sphere area, expensive
 // tuples first) then object slot. Measured on the bench workload (round 2,
 // same box): 10.76 -> 10.0 ms against the slot-only order; the slot grouping
@@ -827,6 +834,7 @@ int bopx_vsd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doubl
   if (int r = set_dev(c)) return r;
   bopx::VsdArgs a{};
   a.cull = vsd_cull_enabled();
+  a.qorder = vsd_queue_order();
   if (int r = fill_vsd_args(c, a, width, height, delta, flags, taus, n_tau, normalized,
                             cost_type))
     return r;
@@ -869,6 +877,7 @@ int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double*
   if (int r = set_dev(c)) return r;
   bopx::VsdArgs a{};
   a.cull = vsd_cull_enabled();
+  a.qorder = vsd_queue_order();
   if (int r = fill_vsd_args(c, a, width, height, delta, flags, taus, n_tau, normalized,
                             cost_type))
     return r;
@@ -961,6 +970,7 @@ int bopx_gt_info_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const d
   if (int r = set_dev(c)) return r;
   bopx::VsdArgs a{};
   a.cull = vsd_cull_enabled();
+  a.qorder = vsd_queue_order();
   if (int r = gt_info_args(c, a, width, height, delta, flags, canvas_scale)) return r;
   hipStream_t s = pick_stream(c, stream);
   if (masks && n > 0)
@@ -1002,6 +1012,7 @@ int bopx_gt_info_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const dou
   if (int r = set_dev(c)) return r;
   bopx::VsdArgs a{};
   a.cull = vsd_cull_enabled();
+  a.qorder = vsd_queue_order();
   if (int r = gt_info_args(c, a, width, height, delta, flags, canvas_scale)) return r;
   std::vector<int32_t> slots;
   if (int r = map_slots(c, n, obj_ids, slots, false, true)) return r;
@@ -1057,6 +1068,7 @@ int bopx_cover_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const dou
   if (int r = set_dev(c)) return r;
   bopx::VsdArgs a{};
   a.cull = vsd_cull_enabled();
+  a.qorder = vsd_queue_order();
   if (int r = cover_args(c, a, width, height)) return r;
   a.objs = c->d_desc;
   a.max_nm = c->max_nm;
@@ -1092,6 +1104,7 @@ int bopx_cover_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const doubl
   if (int r = set_dev(c)) return r;
   bopx::VsdArgs a{};
   a.cull = vsd_cull_enabled();
+  a.qorder = vsd_queue_order();
   if (int r = cover_args(c, a, width, height)) return r;
   std::vector<int32_t> slots;
   if (int r = map_slots(c, n, obj_ids, slots, false, true)) return r;

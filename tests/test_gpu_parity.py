@@ -293,13 +293,15 @@ def _bumpy_mesh(seed, n_lat=40, n_lon=80, amp=0.35):
   return pts.astype(np.float32).astype(np.float64), faces
 
 
-@pytest.mark.parametrize("cull", ["1", "0"])
-def test_fused_vsd_occlusion_cull_exact(oracle_mod, monkeypatch, cull):
-  """k_vsd's occlusion test of far meshlet entries (BOPX_VSD_CULL) on a
-  non-convex mesh and on an almost flat one (edge-on views: irregular, clamped
-  triangles of raster spec v5): bit-exact vs the oracle either way."""
+@pytest.mark.parametrize("cull,qorder", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")])
+def test_fused_vsd_occlusion_cull_exact(oracle_mod, monkeypatch, cull, qorder):
+  """k_vsd's occlusion test of far meshlet entries (BOPX_VSD_CULL) and both
+  tile entry-queue orders (BOPX_VSD_QORDER: large overlaps first / near first)
+  on a non-convex mesh and on an almost flat one (edge-on views: irregular,
+  clamped triangles of raster spec v5): bit-exact vs the oracle every way."""
   from bop_toolkit_amd import synth
   monkeypatch.setenv("BOPX_VSD_CULL", cull)
+  monkeypatch.setenv("BOPX_VSD_QORDER", qorder)
   out = _fused_vs_oracle(oracle_mod, 41, 24, 640, 480, synth.YCBV_K, 0, 0,
                          mesh=_bumpy_mesh(3), z_range=(500.0, 900.0))
   assert np.ptp(out) > 0.1
