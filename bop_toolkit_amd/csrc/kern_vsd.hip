@@ -376,6 +376,19 @@ constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 // (test_fused_vsd_occlusion_cull_exact runs both).
 constexpr int kLptOverlap = kTileW * kTileH / 4;
 
+// Tile loop barriers and the entry queue. Each wave's first entry group is
+// pre-assigned (no claim round trip for it): -0.9 % (same-box A/B, round 2).
+// BOPX_VSD_EARLY_RESET resets the queue counters behind the raster-end barrier
+// and drops the tile-start barrier: measured +0.5 % against keeping the
+// barrier, so off.
+#ifndef BOPX_VSD_EARLY_RESET
+#define BOPX_VSD_EARLY_RESET 0
+#endif
+#ifndef BOPX_VSD_PRECLAIM
+#define BOPX_VSD_PRECLAIM 1
+#endif
+constexpr int kVsdFirstClaim = BOPX_VSD_PRECLAIM ? kVsdWaves * kGroup : 0;
+
 // COST: 0 = step, 1 = tlinear, kCostCover = silhouette overlap, kCostGtInfo = GT stats.
 // NT (step cost): thresholds compared per pixel (>= n_tau; 10 for the BOP taus).
 // RPT: meshlet rectangles held per thread (1, 2 or 4): the launch picks the
@@ -469,6 +482,9 @@ void k_vsd(VsdArgs a) {
     }
   }
   if (tid == 0) {
+    s_nlist = 0;  // tile queue counters (reset again behind each raster-end barrier)
+    s_nsmall = 0;
+    s_next = kVsdFirstClaim;
     s_roi[0] = s_roi[1] = 0x7FFFFFFF;
     s_roi[2] = s_roi[3] = -1;
     s_zr[0][0] = s_zr[1][0] = INFINITY;
@@ -579,13 +595,17 @@ void k_vsd(VsdArgs a) {
       const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
       const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
       // 2a. list the (pose, meshlet) entries touching the tile (the q tiles are
-      // already zero, see the pixel pass).
-      if (tid == 0) {
-        s_nlist = 0;
-        s_nsmall = 0;
-        s_next = 0;
+      // already zero, see the pixel pass). The queue counters were reset behind
+      // the previous tile's raster-end barrier (or before the loop), so no
+      // barrier is needed here: the previous tile's pixel-end barrier orders it.
+      if (!BOPX_VSD_EARLY_RESET) {
+        if (tid == 0) {
+          s_nlist = 0;
+          s_nsmall = 0;
+          s_next = kVsdFirstClaim;
+        }
+        __syncthreads();
       }
-      __syncthreads();
       VSD_STAMP(0);
 #pragma unroll
       for (int j = 0; j < RPT; ++j) {
@@ -622,10 +642,14 @@ void k_vsd(VsdArgs a) {
       // and only then sets up and rasterises them, one triangle per lane.
       const int nnear = __builtin_amdgcn_readfirstlane(s_nlist);
       const int nl = __builtin_amdgcn_readfirstlane(VSD_DIAG(1) ? 0 : s_nlist + s_nsmall);
-      for (;;) {
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&s_next, kGroup);
-        base = __builtin_amdgcn_readfirstlane(base);
+      // each wave's first group is pre-assigned (wave-th group of the queue),
+      // the rest are claimed from s_next, which starts past them
+      for (int claimed = 0;; claimed = 1) {
+        int base = BOPX_VSD_PRECLAIM ? wave * kGroup : 0;
+        if (!BOPX_VSD_PRECLAIM || claimed) {
+          if (lane == 0) base = atomicAdd(&s_next, kGroup);
+          base = __builtin_amdgcn_readfirstlane(base);
+        }
         VSD_STAMP(12);
         if (base >= nl) break;
         if (BOPX_VSD_PRIO && base + kGroup * kVsdWaves >= nl) __builtin_amdgcn_s_setprio(BOPX_VSD_PRIO);
@@ -865,6 +889,14 @@ void k_vsd(VsdArgs a) {
       VSD_STAMP(2);
       __syncthreads();
       if (BOPX_VSD_PRIO) __builtin_amdgcn_s_setprio(0);
+      // every wave has read the queue counters (after the list barrier) and is
+      // done with s_next: reset them for the next tile (ordered by the
+      // pixel-end barrier)
+      if (BOPX_VSD_EARLY_RESET && tid == 0) {
+        s_nlist = 0;
+        s_nsmall = 0;
+        s_next = kVsdFirstClaim;
+      }
       asm volatile("" ::"v"(touch));
       VSD_STAMP(3);
       // 3. per-pixel distances, visibility masks, counters. Each wave first
