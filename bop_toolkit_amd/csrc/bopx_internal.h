@@ -55,8 +55,10 @@ struct ObjDesc {
                              // (vertices shared by neighbouring meshlets are duplicated)
   const uint32_t* mlet_tri;  // nm x 64: local indices a | b << 8 | c << 16, 0xFFFFFFFF = none
   const double* syms;        // 12*ns
-  int nv, nf, nm, ns;
+  const double* seed;        // 3*nseed SoA: farthest-point-sampled vertices (MSSD/MSPD pruning)
+  int nv, nf, nm, ns, nseed;
 };
+constexpr int kSymSeeds = 128;  // seed vertices per object (k_sym_error's symmetry bounds)
 
 struct VsdArgs {
   const ObjDesc* objs;

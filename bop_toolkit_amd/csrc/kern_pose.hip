@@ -15,6 +15,8 @@
 // squared distances (sqrt is monotone, so one sqrt per tuple), reduced through
 // LDS; min over symmetries likewise. Reductions run in a fixed order:
 // results are deterministic.
+#include <cstdlib>
+
 #include "bopx_internal.h"
 
 namespace bopx {
@@ -98,6 +100,86 @@ __device__ __forceinline__ double rcp64(double x) {
   return fma(r, fma(-x, r, 1.0), r);
 }
 
+// Compose R_gs = R_g S_R, t_gs = R_g S_t + t_g (pose_error.py:114-115).
+__device__ __forceinline__ void sym_compose(const double* G, const double* S, double* Rgs,
+                                            double* tgs) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      Rgs[3 * i + j] = fma(G[3 * i + 2], S[6 + j], fma(G[3 * i + 1], S[3 + j], G[3 * i] * S[j]));
+    tgs[i] = fma(G[3 * i + 2], S[11], fma(G[3 * i + 1], S[10], fma(G[3 * i], S[9], G[9 + i])));
+  }
+}
+
+// Per-symmetry 3x4 matrix of the error: MSSD the difference-affine form
+// T_e p - T_gs p = (R_e - R_gs) p + (t_e - t_gs); MSPD the projection K [R_gs | t_gs].
+template <int MODE>
+__device__ __forceinline__ void sym_matrix(const double* E, const double* K, const double* G,
+                                           const double* S, double* A) {
+  double Rgs[9], tgs[3];
+  sym_compose(G, S, Rgs, tgs);
+  if constexpr (MODE == 0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) A[4 * i + j] = E[3 * i + j] - Rgs[3 * i + j];
+      A[4 * i + 3] = E[9 + i] - tgs[i];
+    }
+  } else {
+    proj_mat(K, Rgs, tgs, A);
+  }
+}
+
+// Squared error of one vertex under one symmetry (the same expressions in the
+// exhaustive and the pruned sweep, so both give the same bits). MSPD: (ue, ve)
+// is the vertex's projection under the estimate (est_proj).
+__device__ __forceinline__ double d2_mssd(const double* A, double x, double y, double z) {
+  const double dx = aff(A, 0, x, y, z), dy = aff(A, 1, x, y, z), dz = aff(A, 2, x, y, z);
+  return fma(dz, dz, fma(dy, dy, dx * dx));
+}
+__device__ __forceinline__ double d2_mspd(const double* A, double x, double y, double z, double ue,
+                                          double ve) {
+  const double izg = rcp64(aff(A, 2, x, y, z));
+  const double du = fma(-aff(A, 0, x, y, z), izg, ue);
+  const double dv = fma(-aff(A, 1, x, y, z), izg, ve);
+  return fma(dv, dv, du * du);
+}
+__device__ __forceinline__ void est_proj(const double* Pe, double x, double y, double z,
+                                         double& ue, double& ve) {
+  const double ize = rcp64(aff(Pe, 2, x, y, z));
+  ue = aff(Pe, 0, x, y, z) * ize;
+  ve = aff(Pe, 1, x, y, z) * ize;
+}
+
+// Symmetry pruning (units with >= prune_min symmetries). min_s max_v d2(s, v)
+// does not need every max: a symmetry whose max over ANY subset of the vertices
+// already exceeds the max of a fully swept symmetry cannot be the minimum. The
+// unit (1) bounds every symmetry from below by its max over the object's seed
+// vertices (farthest-point samples, runtime.cpp seed_vertices), (2) sweeps the
+// lowest-bound symmetry over all vertices with the whole workgroup, then
+// (3) lets each wave take the next symmetries in ascending bound order and drop
+// one as soon as a partial max exceeds the best completed max (or stop once a
+// bound does). The best so far is shared by the unit (LDS) and across the
+// chunks of a tuple (the output word, read at the start). Every symmetry that
+// can be the minimum is swept in full with the same d2 expressions as the
+// exhaustive path and max is exact, so the result is bit-identical to it
+// (tests/test_gpu_parity.py compares both).
+#ifndef BOPX_SYM_PRUNE_MIN
+#define BOPX_SYM_PRUNE_MIN 2
+#endif
+#ifndef BOPX_SYM_SEEDS
+#define BOPX_SYM_SEEDS 128  // seed vertices used of the object's kSymSeeds
+#endif
+constexpr int kPruneSpan = 320;  // symmetry sets up to this size are pruned by one unit
+
+// Make LDS written by other lanes of this wave visible (LDS is in order per wave).
+__device__ __forceinline__ void wave_lds_sync_pose() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int MODE>  // 0 = MSSD, 1 = MSPD
 __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __restrict__ objs,
                                                             const int32_t* __restrict__ slots,
@@ -105,7 +187,8 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
                                                             const double* __restrict__ pg,
                                                             const double* __restrict__ Km,
                                                             double* __restrict__ out, int nch,
-                                                            const int32_t* __restrict__ order) {
+                                                            const int32_t* __restrict__ order,
+                                                            int prune_min) {
   __shared__ double s_red[kPoseThreads];
   // A block of kSymStage vertices staged for every symmetry of the unit: x, y, z
   // and, for MSPD, the estimate's projection u_e, v_e.
@@ -122,36 +205,218 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
   double G[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) G[i] = pg[12 * b + i];
-  // Compose R_gs = R_g S_R, t_gs = R_g S_t + t_g (pose_error.py:114-115).
-  const double* S = o.syms + 12 * (int64_t)(s0 + k);
-  double Rgs[9], tgs[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      Rgs[3 * i + j] = fma(G[3 * i + 2], S[6 + j], fma(G[3 * i + 1], S[3 + j], G[3 * i] * S[j]));
-    tgs[i] = fma(G[3 * i + 2], S[11], fma(G[3 * i + 1], S[10], fma(G[3 * i], S[9], G[9 + i])));
-  }
   const gptr<const double> px = (gptr<const double>)o.pts;
   const gptr<const double> py = px + nv;
   const gptr<const double> pz = py + nv;
+  // A tuple's whole symmetry set (<= kPruneSpan) is pruned by one unit (chunk
+  // 0; the tuple's other chunks exit), larger sets chunk by chunk.
+  const bool whole = ns <= kPruneSpan;
+  const int span = whole ? ns : sp;
+  if (span >= prune_min) {
+    if (whole && c != 0) return;
+    static_assert(kSymSeeds <= kPoseThreads && kSymSeeds <= kSymStage<MODE>, "seed staging");
+    __shared__ double s_L[kPruneSpan];    // per-symmetry lower bound (max over the seeds)
+    __shared__ int s_cand[kPruneSpan];    // symmetries left to sweep
+    __shared__ unsigned long long s_best;  // best completed max (bits of a non-negative double)
+    __shared__ int s_next, s_ncand, s_k0;
+    const int sb = whole ? 0 : s0;  // the unit's first symmetry
+    const double* syms = o.syms + 12 * (int64_t)sb;
+    const int lane = tid & 63, wave = tid >> 6;
+    double E[12], K[9], Pe[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) E[i] = pe[12 * b + i];
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) K[i] = Km[9 * b + i];
+      proj_mat(K, E, E + 9, Pe);
+    }
+    auto d2v = [&](const double* A, int v) {  // vertex v from global memory
+      const double x = px[v], y = py[v], z = pz[v];
+      if constexpr (MODE == 0) {
+        return d2_mssd(A, x, y, z);
+      } else {
+        double ue, ve;
+        est_proj(Pe, x, y, z, ue, ve);
+        return d2_mspd(A, x, y, z, ue, ve);
+      }
+    };
+    auto best_now = [&]() {
+      return __longlong_as_double((long long)__hip_atomic_load(&s_best, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_WORKGROUP));
+    };
+    auto publish = [&](double M) {
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(M);
+      atomicMin(&s_best, bits);
+      atomicMin((unsigned long long*)&out[b], bits);
+    };
+    // (1) bounds over the seed vertices, 64 symmetries at a time, lane (k, g) =
+    // (symmetry, seed group)
+    const int np = min(o.nseed, BOPX_SYM_SEEDS);
+    if (tid < np) {
+      const gptr<const double> sd = (gptr<const double>)o.seed;
+      const int ns_all = o.nseed;  // SoA stride
+      const double x = sd[tid], y = sd[ns_all + tid], z = sd[2 * ns_all + tid];
+      s_v[0][tid] = x;
+      s_v[1][tid] = y;
+      s_v[2][tid] = z;
+      if constexpr (MODE == 1) est_proj(Pe, x, y, z, s_v[3][tid], s_v[4][tid]);
+    }
+    if (tid == 0) {
+      // another chunk's result (chunked sets), else +inf
+      s_best = __hip_atomic_load((unsigned long long*)&out[b], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      s_next = 0;
+      s_ncand = 0;
+    }
+    __syncthreads();
+    for (int kb = 0; kb < span; kb += 64) {
+      const int bp = min(span - kb, 64), bng = kPoseThreads / bp;
+      const int bk = tid % bp, bg = tid / bp;
+      double m = -INFINITY;
+      if (bg < bng) {
+        double A[12];
+        sym_matrix<MODE>(E, K, G, syms + 12 * (int64_t)(kb + bk), A);
+        for (int j = bg; j < np; j += bng)
+          m = fmax(m, MODE == 0 ? d2_mssd(A, s_v[0][j], s_v[1][j], s_v[2][j])
+                                : d2_mspd(A, s_v[0][j], s_v[1][j], s_v[2][j], s_v[3][j], s_v[4][j]));
+      }
+      s_red[tid] = m;
+      __syncthreads();
+      if (tid < bp) {
+        double L = -INFINITY;
+        for (int gg = 0; gg < bng; ++gg) L = fmax(L, s_red[gg * bp + tid]);
+        s_L[kb + tid] = L;
+      }
+      __syncthreads();
+    }
+    // argmin of (bound, index): per thread, then per wave, then over the waves
+    {
+      double L = INFINITY;
+      int kk = 0x7FFFFFFF;
+      for (int i = tid; i < span; i += kPoseThreads)
+        if (s_L[i] < L) {
+          L = s_L[i];
+          kk = i;
+        }
+      for (int off = 32; off > 0; off >>= 1) {
+        const double oL = __shfl_xor(L, off, 64);
+        const int ok = __shfl_xor(kk, off, 64);
+        if (oL < L || (oL == L && ok < kk)) {
+          L = oL;
+          kk = ok;
+        }
+      }
+      if (lane == 0) {
+        s_red[wave] = L;
+        s_cand[wave] = kk;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        double bL = s_red[0];
+        int bk = s_cand[0];
+        for (int w = 1; w < kPoseThreads / 64; ++w)
+          if (s_red[w] < bL || (s_red[w] == bL && s_cand[w] < bk)) {
+            bL = s_red[w];
+            bk = s_cand[w];
+          }
+        s_k0 = bk;
+      }
+      __syncthreads();
+    }
+    const int k0 = s_k0;
+    if (!(s_L[k0] <= best_now())) return;  // no symmetry of the unit can win
+    // (2) the lowest bound, swept by the whole workgroup
+    {
+      double A[12];
+      sym_matrix<MODE>(E, K, G, syms + 12 * (int64_t)k0, A);
+      double m = -INFINITY;
+      for (int v0 = 0; v0 < nv; v0 += 4 * kPoseThreads) {
+        double d[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) d[u] = d2v(A, min(v0 + u * kPoseThreads + tid, nv - 1));
+        m = fmax(m, fmax(fmax(d[0], d[1]), fmax(d[2], d[3])));
+      }
+      m = wave_max(m);
+      if (lane == 0) s_red[wave] = m;
+      __syncthreads();
+      if (tid == 0) publish(fmax(fmax(s_red[0], s_red[1]), fmax(s_red[2], s_red[3])));
+      __syncthreads();
+    }
+    // candidates: the other symmetries whose bound does not exceed the best max
+    {
+      const double best = best_now();
+      for (int i0 = 0; i0 < span; i0 += kPoseThreads) {
+        const int i = i0 + tid;
+        const bool cand = i < span && i != k0 && s_L[i] <= best;
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
+        int base = 0;
+        if (lane == 0 && bal) base = atomicAdd(&s_ncand, __popcll(bal));
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (cand)
+          s_cand[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = i;
+      }
+      __syncthreads();
+      // short lists in ascending bound order (wave 0), so that the best
+      // candidates tighten the bound first
+      const int nc = s_ncand;
+      if (nc <= 64 && wave == 0) {
+        const int kk = lane < nc ? s_cand[lane] : 0x7FFFFFFF;
+        const double L = lane < nc ? s_L[kk] : INFINITY;
+        int r = 0;
+        for (int j = 0; j < 64; ++j) {
+          const double Lj = __shfl(L, j, 64);
+          const int kj = __shfl(kk, j, 64);
+          r += (Lj < L) || (Lj == L && kj < kk);
+        }
+        wave_lds_sync_pose();
+        if (lane < nc) s_cand[r] = kk;
+      }
+      __syncthreads();
+    }
+    // (3) the candidates, one wave each. Single-exit loops with wave-uniform
+    // conditions (SGPR claims and ballots).
+    const int nc = s_ncand;
+    auto claim = [&]() {
+      int i = 0;
+      if (lane == 0) i = atomicAdd(&s_next, 1);
+      return __builtin_amdgcn_readfirstlane(i);
+    };
+    int idx = claim();
+    while (idx < nc) {
+      const int kk = __builtin_amdgcn_readfirstlane(s_cand[idx]);
+      double best = best_now();
+      if (s_L[kk] <= best) {  // (else: the bound has passed the best by now)
+        double A[12];
+        sym_matrix<MODE>(E, K, G, syms + 12 * (int64_t)kk, A);
+        double m = -INFINITY;
+        uint64_t dead = 0;  // a lane's partial max exceeds a completed symmetry's max
+        for (int v0 = 0; v0 < nv && dead == 0; v0 += 256) {
+          double d[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) d[u] = d2v(A, min(v0 + 64 * u + lane, nv - 1));
+          m = fmax(m, fmax(fmax(d[0], d[1]), fmax(d[2], d[3])));
+          dead = __builtin_amdgcn_ballot_w64(m > best);
+          best = best_now();
+        }
+        if (dead == 0) {
+          m = wave_max(m);
+          if (lane == 0) publish(m);
+        }
+      }
+      idx = claim();
+    }
+    return;
+  }
+  // Exhaustive path: lane (k, g) = (symmetry, vertex group).
+  const double* S = o.syms + 12 * (int64_t)(s0 + k);
   double m0 = -INFINITY, m1 = -INFINITY, m2 = -INFINITY, m3 = -INFINITY;
   if constexpr (MODE == 0) {
     double E[12], A[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) E[i] = pe[12 * b + i];
-    // Difference-affine form: T_e p - T_gs p = (R_e - R_gs) p + (t_e - t_gs).
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) A[4 * i + j] = E[3 * i + j] - Rgs[3 * i + j];
-      A[4 * i + 3] = E[9 + i] - tgs[i];
-    }
-    auto d2 = [&](int j) {
-      const double x = s_v[0][j], y = s_v[1][j], z = s_v[2][j];
-      const double dx = aff(A, 0, x, y, z), dy = aff(A, 1, x, y, z), dz = aff(A, 2, x, y, z);
-      return fma(dz, dz, fma(dy, dy, dx * dx));
-    };
+    sym_matrix<0>(E, nullptr, G, S, A);
+    auto d2 = [&](int j) { return d2_mssd(A, s_v[0][j], s_v[1][j], s_v[2][j]); };
     for (int v0 = 0; v0 < nv; v0 += kSymStage<MODE>) {
       const int nb = min(kSymStage<MODE>, nv - v0);
       __syncthreads();
@@ -179,13 +444,9 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
 #pragma unroll
     for (int i = 0; i < 12; ++i) E[i] = pe[12 * b + i];
     proj_mat(K, E, E + 9, Pe);
-    proj_mat(K, Rgs, tgs, A);
+    sym_matrix<1>(E, K, G, S, A);
     auto d2 = [&](int j) {
-      const double x = s_v[0][j], y = s_v[1][j], z = s_v[2][j];
-      const double izg = rcp64(aff(A, 2, x, y, z));
-      const double du = fma(-aff(A, 0, x, y, z), izg, s_v[3][j]);
-      const double dv = fma(-aff(A, 1, x, y, z), izg, s_v[4][j]);
-      return fma(dv, dv, du * du);
+      return d2_mspd(A, s_v[0][j], s_v[1][j], s_v[2][j], s_v[3][j], s_v[4][j]);
     };
     for (int v0 = 0; v0 < nv; v0 += kSymStage<MODE>) {
       const int nb = min(kSymStage<MODE>, nv - v0);
@@ -194,12 +455,10 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
       for (int i = tid; i < kSymStage<MODE>; i += kPoseThreads)
         if (i < nb) {
           const double x = px[v0 + i], y = py[v0 + i], z = pz[v0 + i];
-          const double ize = rcp64(aff(Pe, 2, x, y, z));
           s_v[0][i] = x;
           s_v[1][i] = y;
           s_v[2][i] = z;
-          s_v[3][i] = aff(Pe, 0, x, y, z) * ize;
-          s_v[4][i] = aff(Pe, 1, x, y, z) * ize;
+          est_proj(Pe, x, y, z, s_v[3][i], s_v[4][i]);
         }
       __syncthreads();
       if (g < ng) {
@@ -385,12 +644,17 @@ hipError_t launch_sym_error(int mode, const ObjDesc* objs, int max_ns, int64_t n
   const dim3 gfix((unsigned)((n + 255) / 256)), bfix(256);
   hipLaunchKernelGGL(k_sym_init, gfix, bfix, 0, s, out, n);
   dim3 grid((unsigned)(n * nch)), block(kPoseThreads);
+  // BOPX_SYM_PRUNE: units with at least this many symmetries take the pruned
+  // path (0 = never; identical results either way)
+  const char* pe_env = getenv("BOPX_SYM_PRUNE");  // read per call (tests compare both paths)
+  const int prune_env = pe_env ? atoi(pe_env) : BOPX_SYM_PRUNE_MIN;
+  const int prune_min = prune_env > 0 ? prune_env : kSymChunk + 1;
   if (mode == 0)
     hipLaunchKernelGGL(k_sym_error<0>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch,
-                       order);
+                       order, prune_min);
   else
     hipLaunchKernelGGL(k_sym_error<1>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch,
-                       order);
+                       order, prune_min);
   hipLaunchKernelGGL(k_sym_finish, gfix, bfix, 0, s, out, n);
   return hipGetLastError();
 }

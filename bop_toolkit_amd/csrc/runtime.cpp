@@ -40,6 +40,8 @@ struct Object {
   float4* d_mvtx = nullptr;
   uint32_t* d_mtri = nullptr;
   double* d_syms = nullptr;
+  double* d_seed = nullptr;
+  int64_t nseed = 0;
 };
 
 }  // namespace
@@ -174,6 +176,8 @@ int sync_desc(bopx_ctx* c) {
       d.mlet_vtx = o.d_mvtx;
       d.mlet_tri = o.d_mtri;
       d.syms = o.d_syms;
+      d.seed = o.d_seed;
+      d.nseed = (int)o.nseed;
       d.nv = (int)o.nv;
       d.nf = (int)o.nf;
       d.nm = (int)o.nm;
@@ -224,6 +228,7 @@ void free_object(Object& o) {
   if (o.d_mvtx) (void)hipFree(o.d_mvtx);
   if (o.d_mtri) (void)hipFree(o.d_mtri);
   if (o.d_syms) (void)hipFree(o.d_syms);
+  if (o.d_seed) (void)hipFree(o.d_seed);
   o = Object();
 }
 
@@ -470,6 +475,53 @@ static void greedy_meshlets(const uint32_t* faces, int64_t nv, int64_t nf,
   }
 }
 
+// Seed vertices of the MSSD / MSPD symmetry bounds (kern_pose.hip): up to
+// kSymSeeds vertices by farthest-point sampling from the one farthest from the
+// centroid, SoA x | y | z. The max of a pose error over a spread-out subset is
+// a tight lower bound of its max over all vertices, which lets k_sym_error skip
+// symmetries that cannot be the minimum. Only the speed depends on the choice.
+static std::vector<double> seed_vertices(const double* pts, int64_t nv) {
+  const int64_t np = std::min<int64_t>(nv, bopx::kSymSeeds);
+  std::vector<double> seed(3 * (size_t)np);
+  double cx = 0.0, cy = 0.0, cz = 0.0;
+  for (int64_t v = 0; v < nv; ++v) {
+    cx += pts[3 * v];
+    cy += pts[3 * v + 1];
+    cz += pts[3 * v + 2];
+  }
+  cx /= (double)nv;
+  cy /= (double)nv;
+  cz /= (double)nv;
+  auto d2 = [&](int64_t v, double x, double y, double z) {
+    const double dx = pts[3 * v] - x, dy = pts[3 * v + 1] - y, dz = pts[3 * v + 2] - z;
+    return dx * dx + dy * dy + dz * dz;
+  };
+  std::vector<double> near((size_t)nv);
+  int64_t pick = 0;
+  for (int64_t v = 0; v < nv; ++v) {
+    near[v] = d2(v, cx, cy, cz);
+    if (near[v] > near[pick]) pick = v;
+  }
+  for (int64_t i = 0; i < np; ++i) {
+    const double x = pts[3 * pick], y = pts[3 * pick + 1], z = pts[3 * pick + 2];
+    seed[i] = x;
+    seed[np + i] = y;
+    seed[2 * np + i] = z;
+    int64_t next = pick;
+    double far = -1.0;
+    for (int64_t v = 0; v < nv; ++v) {
+      const double e = d2(v, x, y, z);
+      if (i == 0 || e < near[v]) near[v] = e;
+      if (near[v] > far) {
+        far = near[v];
+        next = v;
+      }
+    }
+    pick = next;
+  }
+  return seed;
+}
+
 int bopx_add_object(bopx_ctx* c, int obj_id, const double* pts, int64_t nv,
                     const uint32_t* faces, int64_t nf) {
   if (!c) return BOPX_E_INVALID;
@@ -571,8 +623,11 @@ int bopx_add_object(bopx_ctx* c, int obj_id, const double* pts, int64_t nv,
     }
     o.nm = (int64_t)minfo.size();
   }
+  const std::vector<double> seed = seed_vertices(pts, nv);
+  o.nseed = (int64_t)seed.size() / 3;
   int r;
   if ((r = upload(c, &o.d_pts, soa.data(), soa.size())) ||
+      (r = upload(c, &o.d_seed, seed.data(), seed.size())) ||
       (r = upload(c, &o.d_vtx, vtx.data(), vtx.size())) ||
       (r = upload(c, &o.d_faces, fsorted.data(), fsorted.size())) ||
       (r = upload(c, &o.d_mlet, mlet.data(), mlet.size())) ||

@@ -382,6 +382,51 @@ def test_batch_evaluator_matches_oracle(oracle_mod):
   assert np.array_equal(np.round(comp), fr[0])
 
 
+def test_sym_pruning_bit_identical(ctx, oracle_mod, monkeypatch):
+  """MSSD / MSPD with symmetry pruning (BOPX_SYM_PRUNE, default: units of >= 2
+  symmetries) give the same bits as the exhaustive sweep, and match the oracle,
+  over discrete sets of 2 .. 64 (one chunk), 65 and 128 (two chunks) and a
+  continuous 314-element set, with gross outliers and a pose behind the camera."""
+  from bop_toolkit_amd import misc, synth
+  rng = np.random.default_rng(77)
+  objs = []
+  for o, (nd, cont) in enumerate([(2, False), (8, False), (16, False), (64, False), (65, False),
+                                  (128, False), (1, True), (2, True)]):
+    pts, faces = synth.superellipsoid(12 + 2 * o, 24, (30.0 + 4 * o, 45.0, 55.0 - 3 * o),
+                                      0.55 + 0.05 * o)
+    pts = pts * (1.0 + 0.2 * rng.uniform(-1.0, 1.0, (len(pts), 1)))  # non-convex
+    info = synth.models_info_entry(pts, nd, cont)
+    syms = misc.symmetries_to_array(misc.get_symmetry_transformations(info, 0.01))
+    ctx.add_object(700 + o, pts, faces)
+    ctx.set_symmetries(700 + o, syms)
+    objs.append({"pts": pts, "faces": faces, "syms": syms})
+  n = 96
+  obj = (np.arange(n) % len(objs)).astype(np.int32)
+  Rg, tg = synth.gt_poses(rng, n)
+  Re, te_ = synth.perturb(rng, Rg, tg, outlier_frac=0.3)
+  te_[5, 2] = -50.0  # estimate behind the camera (MSPD: negative / tiny depths)
+  pe = np.concatenate([Re.reshape(n, 9), te_], 1)
+  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
+  K = np.tile(synth.LMO_K.reshape(9), (n, 1))
+  res = {}
+  for mode in ("0", "8", "2"):
+    monkeypatch.setenv("BOPX_SYM_PRUNE", mode)
+    res[mode] = (_batch(ctx, "bopx_mssd_batch", obj + 700, pe, pg),
+                 _batch(ctx, "bopx_mspd_batch", obj + 700, pe, pg, K))
+  for mode in ("8", "2"):
+    assert np.array_equal(res[mode][0], res["0"][0]), "MSSD pruned != exhaustive"
+    assert np.array_equal(res[mode][1], res["0"][1]), "MSPD pruned != exhaustive"
+  for i in range(0, n, 5):
+    o = objs[obj[i]]
+    want = oracle_mod.mssd(o["pts"], o["syms"], pe[i], pg[i])
+    assert abs(res["8"][0][i] - want) <= TOL * max(1.0, abs(want))
+    if i != 5:
+      want = oracle_mod.mspd(o["pts"], o["syms"], pe[i], pg[i], K[i])
+      assert abs(res["8"][1][i] - want) <= TOL * max(1.0, abs(want))
+  for o in range(len(objs)):
+    ctx.remove_object(700 + o)
+
+
 def test_errors_on_bad_input(ctx):
   from bop_toolkit_amd._lib import _d, _i32, ptr
   ids = np.array([12345], np.int32)
