@@ -362,6 +362,12 @@ constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 #ifndef BOPX_VSD_PRIO
 #define BOPX_VSD_PRIO 3
 #endif
+// Pixel pass without per-pose branches (all three distances on every lane):
+// measured +0.9 % (round 2, same box; waves whose pixels all miss one pose
+// skip that pose's distance), so off.
+#ifndef BOPX_VSD_PIX_BRANCHFREE
+#define BOPX_VSD_PIX_BRANCHFREE 0
+#endif
 // Software-pipelined VSD pixel loop: measured 2 % slower than the plain loop
 // (same-box A/B, round 2), kept as an option.
 #ifndef BOPX_VSD_PIXPIPE
@@ -935,6 +941,18 @@ void k_vsd(VsdArgs a) {
         return ld_off(tframe, (uint32_t)(__mul24(p >> 6, IW) + (p & 63)) * 4u);
       };
       auto vsd_px = [&](int p, uint32_t qe, uint32_t qg, float dtest) {
+#if BOPX_VSD_PIX_BRANCHFREE
+        // branch-free: a background pose (q = 0) takes 1/1 (no IEEE fallback
+        // in rcp_rn) and depth 0, whose distance is exactly +0 (sqrt_depth(0))
+        const float re = rcp_rn(__uint_as_float(qe ? qe : 0x3F800000u));
+        const float rg = rcp_rn(__uint_as_float(qg ? qg : 0x3F800000u));
+        const float de = qe ? re : 0.0f, dg = qg ? rg : 0.0f;
+        const double pX = w_pX[p % kTileW];
+        const double pY = w_pY[p / kTileW];
+        const double dist_t = dist_of(pX, pY, dtest);
+        const double dist_g = dist_of(pX, pY, dg);
+        const double dist_e = dist_of(pX, pY, de);
+#else
         const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
         const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
         const double pX = w_pX[p % kTileW];
@@ -942,6 +960,7 @@ void k_vsd(VsdArgs a) {
         const double dist_t = dist_of(pX, pY, dtest);
         const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
         const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
+#endif
         const bool vg = visib19t(dist_t, dist_g, a.dthr);
         bool ve = visib19t(dist_t, dist_e, a.dthr);
         ve = ve || (vg && dist_e > 0.0);  // visibility.py:74
