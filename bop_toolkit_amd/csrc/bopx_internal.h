@@ -42,7 +42,11 @@ constexpr int kCostGtInfo = 3;  // k_vsd mode: one (gt) pose, silhouette + visib
 constexpr int kGtInfoCols = 11;  // all, visib, obj bbox x0 y0 x1 y1, visib bbox, valid
 constexpr int kTileW = BOPX_TILE_W;  // VSD screen tile (LDS-resident q pair)
 constexpr int kTileH = BOPX_TILE_H;
-constexpr int kTileStride = kTileW + 1;  // LDS row pitch of a q tile (dwords)
+#ifndef BOPX_TILE_STRIDE
+#define BOPX_TILE_STRIDE (BOPX_TILE_W + 1)
+#endif
+constexpr int kTileStride = BOPX_TILE_STRIDE;  // LDS row pitch of a q tile (dwords)
+static_assert(kTileStride > kTileW, "the row walk may touch the column right of a tile");
 constexpr float kGuardBand = 16384.0f;  // |u|,|v| limit of a rasterised vertex (px)
 
 struct ObjDesc {

@@ -761,7 +761,7 @@ void k_vsd(VsdArgs a) {
         wave_lds_sync();
         if (VSD_DIAG(4) && lane == 0) atomicAdd(&g_vsd_stats[1], (unsigned long long)kGroup);
         VSD_STAMP(9);
-        for (int c0 = 0; c0 < cnt; c0 += 64) {
+        for (int c0 = 0; c0 < (VSD_DIAG(64) ? 0 : cnt); c0 += 64) {
           // Set-up, one triangle per lane.
           RTri T;
           bool ok = false;
@@ -791,6 +791,15 @@ void k_vsd(VsdArgs a) {
           // extent >= 128 px (int64 edges) or an irregular sliver (clamped q):
           // walked by its own lane with the full spec arithmetic (r_raster)
           const bool fast = T.small & T.regular;
+          if VSD_DIAG(4) {
+            if (ok && !fast) {
+              atomicAdd(&g_vsd_stats[10], 1ull);
+              atomicAdd(&g_vsd_stats[11], (unsigned long long)(cc1 - cc0 + 1) * (rr1 - rr0 + 1));
+              if (!T.small) atomicAdd(&g_vsd_stats[13], 1ull);
+            }
+            if (lane == 0 && __builtin_amdgcn_ballot_w64(ok && !fast) != 0)
+              atomicAdd(&g_vsd_stats[12], 1ull);
+          }
           if (ok && !fast) {
             uint32_t* dep = s_dep[r];
             r_raster(T, cc0, cc1, rr0, rr1, [&](int col, int row, float q) {
@@ -811,7 +820,7 @@ void k_vsd(VsdArgs a) {
 #else
           if (rows) r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first, s_rec[wave][lane]);
 #endif
-          for (int wb = 0; wb < nrow; wb += kRowWin) {
+          for (int wb = 0; wb < (VSD_DIAG(32) ? 0 : nrow); wb += kRowWin) {
             wave_lds_sync();  // records written / previous window's owners consumed
             for (int k = max(first, wb); k < min(first + h, wb + kRowWin); ++k)
               s_own[wave][k - wb] = (uint8_t)lane;

@@ -413,7 +413,7 @@ __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* de
     const f32x2 q = __builtin_elementwise_fma(ga2, fdx, qrow2);
     const float q0 = q.x, q1 = q.y;
     frags += (m0 > 0) + ((i + 1 < w) & (m1 > 0));  // diagnostics (dead in the product build)
-#if BOPX_WALK_MASKED
+#if BOPX_WALK_MASKED == 1
     if constexpr (kNoAtomics) {
       asm volatile("" ::"v"(m0 > 0 ? q0 : 0.0f), "v"(m1 > 0 ? q1 : 0.0f), "v"(d + i));
     } else {
@@ -421,6 +421,11 @@ __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* de
       if (m0 > 0) atomicMax(d + i, __float_as_int(q0));
       if (m1 > 0) atomicMax(d + i + 1, __float_as_int(q1));
     }
+#elif BOPX_WALK_MASKED == 2
+    // wave-uniform skip of a column with no covered centre, unmasked otherwise
+    if (__builtin_amdgcn_ballot_w64(m0 > 0) != 0) atomicMax(d + i, m0 > 0 ? __float_as_int(q0) : 0);
+    if (__builtin_amdgcn_ballot_w64(m1 > 0) != 0)
+      atomicMax(d + i + 1, m1 > 0 ? __float_as_int(q1) : 0);
 #else
     atomicMax(d + i, m0 > 0 ? __float_as_int(q0) : 0);
     atomicMax(d + i + 1, m1 > 0 ? __float_as_int(q1) : 0);
