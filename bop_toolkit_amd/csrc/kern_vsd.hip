@@ -324,6 +324,12 @@ constexpr int kPixPerWave = (kTileH + kVsdWaves - 1) / kVsdWaves * kTileW;
 // walking lane with ds_bpermute: the workgroup then fits 3 per CU (LDS <= 54 KiB).
 // Measured (round 2, same box): 1 % slower than LDS records at 2 workgroups
 // per CU; at 3 per CU the 80-VGPR budget spills (+32 %). Off by default.
+// Row-item -> record lookup: start flags + ballot/mbcnt (one flag write per
+// record) instead of an owner byte per row item.
+#ifndef BOPX_WALK_FLAGS
+#define BOPX_WALK_FLAGS 1
+#endif
+static_assert(kRowWin == 4 * 64, "start flags are cleared one dword per lane");
 #ifndef BOPX_VSD_REGREC
 #define BOPX_VSD_REGREC 0
 #endif
@@ -417,7 +423,8 @@ void k_vsd(VsdArgs a) {
 #if !BOPX_VSD_REGREC
   __shared__ RRow s_rec[kVsdWaves][64];          // set-up triangles of the current chunk
 #endif
-  __shared__ uint8_t s_own[kVsdWaves][kRowWin];  // row item -> record (lane) of a window
+  // row item -> record (lane) of a window, or (BOPX_WALK_FLAGS) record start flags
+  __shared__ __attribute__((aligned(4))) uint8_t s_own[kVsdWaves][kRowWin];
   // Tile entry queue. RPT <= 2 (objects of <= 512 meshlets): 32-bit words
   // entry | far << 11 | rectangle in the tile at 2-px granularity (x0/2, x1/2,
   // y0/2, y1/2: 5 bits each from bit 12) for the occlusion test; RPT 4: 16-bit
@@ -817,13 +824,28 @@ void k_vsd(VsdArgs a) {
 #if BOPX_VSD_REGREC
           RRow own;  // this lane's record (defined in every lane: fetched with full exec)
           r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first, own);
+#elif BOPX_WALK_FLAGS
+          // records compacted by rank among the row-owning lanes (ascending first)
+          const uint64_t rbal = __builtin_amdgcn_ballot_w64(rows);
+          if (rows)
+            r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first,
+                       s_rec[wave][__builtin_amdgcn_mbcnt_hi(
+                           (uint32_t)(rbal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rbal, 0u))]);
 #else
           if (rows) r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first, s_rec[wave][lane]);
 #endif
+          int rec_base = 0;  // BOPX_WALK_FLAGS: records started before the current pass
           for (int wb = 0; wb < (VSD_DIAG(32) ? 0 : nrow); wb += kRowWin) {
             wave_lds_sync();  // records written / previous window's owners consumed
+#if BOPX_WALK_FLAGS && !BOPX_VSD_REGREC
+            // one start flag per record instead of one owner byte per row item
+            reinterpret_cast<uint32_t*>(&s_own[wave][0])[lane] = 0u;
+            wave_lds_sync();
+            if (rows && first >= wb && first < wb + kRowWin) s_own[wave][first - wb] = 1u;
+#else
             for (int k = max(first, wb); k < min(first + h, wb + kRowWin); ++k)
               s_own[wave][k - wb] = (uint8_t)lane;
+#endif
             wave_lds_sync();
             const int wn = min(nrow - wb, kRowWin);
 #if BOPX_VSD_REGREC
@@ -842,6 +864,27 @@ void k_vsd(VsdArgs a) {
                 }
               }
               if (valid) {
+                const int fr =
+                    VSD_DIAG(16) ? r_walk_row_max<true>(rec, wb + p - (int)(rec.meta >> 19),
+                                                        s_dep[(rec.meta >> 18) & 1u])
+                                 : r_walk_row_max(rec, wb + p - (int)(rec.meta >> 19),
+                                                  s_dep[(rec.meta >> 18) & 1u]);
+                if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
+              }
+            }
+#elif BOPX_WALK_FLAGS
+            // item p's record: the last one that starts at or before p, i.e. the
+            // start flags up to p (ballot + mbcnt) past those of earlier passes
+            for (int p0 = 0; p0 < wn; p0 += 64) {
+              const int p = p0 + lane;
+              const bool valid = p < wn;
+              const uint64_t M = __builtin_amdgcn_ballot_w64(valid && s_own[wave][valid ? p : 0] != 0);
+              const int owner = rec_base - 1 + (int)((M >> lane) & 1u) +
+                                (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+              rec_base += __popcll(M);
+              if (valid) {
+                const RRow rec = s_rec[wave][owner];
                 const int fr =
                     VSD_DIAG(16) ? r_walk_row_max<true>(rec, wb + p - (int)(rec.meta >> 19),
                                                         s_dep[(rec.meta >> 18) & 1u])
