@@ -117,7 +117,9 @@ __device__ __forceinline__ bool r_regular(float ga, float gb, int64_t area2, int
 // 2^10 a >= s  <=>  a >= ceil(s / 2^10), s = bw^2 + bh^2 < 2^31.
 __device__ __forceinline__ bool r_regular_small(float ga, float gb, uint32_t area2, uint32_t bw,
                                                 uint32_t bh) {
-  return fmaxf(fabsf(ga), fabsf(gb)) <= 0x1p64f && area2 >= (bw * bw + bh * bh + 1023u) >> 10;
+  // bw, bh < 2^15: full-rate 24-bit multiplies (exact)
+  return fmaxf(fabsf(ga), fabsf(gb)) <= 0x1p64f &&
+         area2 >= (__umul24(bw, bw) + __umul24(bh, bh) + 1023u) >> 10;
 }
 
 // Returns false for triangles with no fragment inside the pixel rectangle
