@@ -324,6 +324,9 @@ constexpr int kPixPerWave = (kTileH + kVsdWaves - 1) / kVsdWaves * kTileW;
 // walking lane with ds_bpermute: the workgroup then fits 3 per CU (LDS <= 54 KiB).
 // Measured (round 2, same box): 1 % slower than LDS records at 2 workgroups
 // per CU; at 3 per CU the 80-VGPR budget spills (+32 %). Off by default.
+#ifndef BOPX_WORD_PAIR
+#define BOPX_WORD_PAIR 1
+#endif
 // Row-item -> record lookup: start flags + ballot/mbcnt (one flag write per
 // record) instead of an owner byte per row item.
 #ifndef BOPX_WALK_FLAGS
@@ -671,17 +674,29 @@ void k_vsd(VsdArgs a) {
         int pose[kGroup];
         int ent[kGroup];
         uint32_t word[kGroup];
+#if BOPX_WORD_PAIR
+        // both queue words in flight before the first wait (distinct registers)
+        uint32_t wv[kGroup];
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g) {
+          const int q = min(base + g, nl - 1);
+          wv[g] = (uint32_t)s_list[q < nnear ? q : kListLen - 1 - (q - nnear)];
+        }
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g) word[g] = __builtin_amdgcn_readfirstlane(wv[g]);
+#else
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
           const int q = min(base + g, nl - 1);
           word[g] = __builtin_amdgcn_readfirstlane(
               (uint32_t)s_list[q < nnear ? q : kListLen - 1 - (q - nnear)]);
         }
+#endif
         int mlt[kGroup];
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
           const int e = (int)(word[g] & 0x7FFu);
-          pose[g] = __builtin_amdgcn_readfirstlane(e >= nm ? 1 : 0);  // uniform (SGPR)
+          pose[g] = e >= nm ? 1 : 0;  // uniform (SGPR): e came through readfirstlane
           mlt[g] = e - pose[g] * nm;
           ent[g] = e;
         }
@@ -841,7 +856,10 @@ void k_vsd(VsdArgs a) {
             // one start flag per record instead of one owner byte per row item
             reinterpret_cast<uint32_t*>(&s_own[wave][0])[lane] = 0u;
             wave_lds_sync();
-            if (rows && first >= wb && first < wb + kRowWin) s_own[wave][first - wb] = 1u;
+            // transposed: item i's flag at byte 4 (i % 64) + i / 64, so one dword
+            // read per lane holds its flags for the window's four passes
+            if (rows && first >= wb && first < wb + kRowWin)
+              s_own[wave][(((first - wb) & 63) << 2) | ((first - wb) >> 6)] = 1u;
 #else
             for (int k = max(first, wb); k < min(first + h, wb + kRowWin); ++k)
               s_own[wave][k - wb] = (uint8_t)lane;
@@ -875,10 +893,12 @@ void k_vsd(VsdArgs a) {
 #elif BOPX_WALK_FLAGS
             // item p's record: the last one that starts at or before p, i.e. the
             // start flags up to p (ballot + mbcnt) past those of earlier passes
+            const uint32_t fl4 = reinterpret_cast<const uint32_t*>(&s_own[wave][0])[lane];
             for (int p0 = 0; p0 < wn; p0 += 64) {
               const int p = p0 + lane;
               const bool valid = p < wn;
-              const uint64_t M = __builtin_amdgcn_ballot_w64(valid && s_own[wave][valid ? p : 0] != 0);
+              const uint64_t M =
+                  __builtin_amdgcn_ballot_w64(valid && ((fl4 >> (p0 >> 3)) & 0xFFu) != 0u);
               const int owner = rec_base - 1 + (int)((M >> lane) & 1u) +
                                 (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
