@@ -324,6 +324,11 @@ constexpr int kPixPerWave = (kTileH + kVsdWaves - 1) / kVsdWaves * kTileW;
 // walking lane with ds_bpermute: the workgroup then fits 3 per CU (LDS <= 54 KiB).
 // Measured (round 2, same box): 1 % slower than LDS records at 2 workgroups
 // per CU; at 3 per CU the 80-VGPR budget spills (+32 %). Off by default.
+// Next pass's record read issued before this pass's walk: +17 % (33 VGPRs
+// spill at 128; round 2), so off.
+#ifndef BOPX_WALK_PREFETCH
+#define BOPX_WALK_PREFETCH 0
+#endif
 #ifndef BOPX_WORD_PAIR
 #define BOPX_WORD_PAIR 1
 #endif
@@ -894,6 +899,35 @@ void k_vsd(VsdArgs a) {
             // item p's record: the last one that starts at or before p, i.e. the
             // start flags up to p (ballot + mbcnt) past those of earlier passes
             const uint32_t fl4 = reinterpret_cast<const uint32_t*>(&s_own[wave][0])[lane];
+#if BOPX_WALK_PREFETCH
+            // the next pass's record read is issued before this pass's walk (owners
+            // are known from the window's flags; always in [0, 63]: loads unmasked)
+            auto owner_of = [&](int p0, int& base) {
+              const uint64_t M = __builtin_amdgcn_ballot_w64(p0 + lane < wn &&
+                                                             ((fl4 >> (p0 >> 3)) & 0xFFu) != 0u);
+              const int o = base - 1 + (int)((M >> lane) & 1u) +
+                            (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+              base += __popcll(M);
+              return o;
+            };
+            RRow rec = s_rec[wave][owner_of(0, rec_base)];
+            for (int p0 = 0; p0 < wn; p0 += 64) {
+              RRow nxt;
+              if (p0 + 64 < wn) nxt = s_rec[wave][owner_of(p0 + 64, rec_base)];
+              const int p = p0 + lane;
+              if (p < wn) {
+                const int fr =
+                    VSD_DIAG(16) ? r_walk_row_max<true>(rec, wb + p - (int)(rec.meta >> 19),
+                                                        s_dep[(rec.meta >> 18) & 1u])
+                                 : r_walk_row_max(rec, wb + p - (int)(rec.meta >> 19),
+                                                  s_dep[(rec.meta >> 18) & 1u]);
+                if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
+              }
+              rec = nxt;
+            }
+            if (false)
+#endif
             for (int p0 = 0; p0 < wn; p0 += 64) {
               const int p = p0 + lane;
               const bool valid = p < wn;
