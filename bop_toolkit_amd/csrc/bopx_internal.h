@@ -6,8 +6,10 @@
 //   vtx   : float32x4    (x, y, z, 0) per vertex     (rasteriser, GL-like fp32)
 //   faces : uint32 x3 per triangle, re-ordered into meshlets of 64 triangles
 //           sorted by the Morton code of the triangle centroid
-//   mlet  : float32 x24 per meshlet: the 8 corners (xyz) of an oriented
-//           bounding box of the meshlet's float32 vertices (conservative culling)
+//   mlet  : float32 x32 per meshlet: the 8 corners (xyz) of an oriented
+//           bounding box of the meshlet's float32 vertices (conservative culling),
+//           then the normal cone (axis xyz, cos alpha) and bounding sphere
+//           (centre xyz, radius): back-facing classification (runtime.cpp meshlet_cone)
 //   syms  : float64 x12 per symmetry [R row-major | t]
 #pragma once
 #include <hip/hip_runtime.h>
@@ -26,6 +28,7 @@ typedef float f32x3 __attribute__((ext_vector_type(3)));
 
 constexpr int kMeshletTris = 64;    // one wave lane per triangle
 constexpr int kMeshletVerts = 64;   // unique vertices per meshlet (one per lane)
+constexpr int kMletFloats = 32;     // per-meshlet culling record (ObjDesc::mlet)
 #ifndef BOPX_MAX_MESHLETS
 #define BOPX_MAX_MESHLETS 1024
 #endif
@@ -53,7 +56,7 @@ struct ObjDesc {
   const double* pts;         // 3*nv, SoA
   const float4* vtx;         // nv
   const uint32_t* faces;     // 3*nf (meshlet order)
-  const float* mlet;         // 24*nm: object-space OBB corners per meshlet
+  const float* mlet;         // kMletFloats*nm: OBB corners, normal cone, sphere per meshlet
   const int4* mlet_info;     // nm: {first triangle, #triangles, first vertex slot, #vertices}
   const float4* mlet_vtx;    // nm x 64: meshlet-local vertex blocks, fixed stride
                              // (vertices shared by neighbouring meshlets are duplicated)

@@ -147,15 +147,46 @@ __device__ double step_threshold(double tau, double diam) {
 // Conservative pixel rectangle of one meshlet bounding box (8 object-space
 // corners, runtime.cpp obb_corners) under a pose. Any corner with Z <= 0 (or a
 // non-finite projection) gives the whole image.
+//
+// Also classifies the entry for the back-face occlusion test (VsdArgs::cull 3):
+// back = every triangle faces away from the camera (normal cone + bounding
+// sphere, runtime.cpp meshlet_cone; a heuristic: it only picks which entries
+// are tested), and qb = an upper bound of every fragment q = 1/Z the meshlet
+// can produce under this pose (the test's threshold; this one must be exact):
+//   * every vertex lies in the box, so its exact camera Z >= the smallest exact
+//     corner Z; the float32 evaluations of both (vertex in r_vertex, corner
+//     here) are within 6 u (|x| + |y| + |z| + |t_z|) of exact (u = 2^-24, |R_ij|
+//     <= m = max(1, |R_2j|)), and the L1 norm over the box peaks at a corner:
+//     zlo = zmin - 2^-19 (m rho1 + |t_z|) bounds every vertex Z from below
+//     (2.6x margin);
+//   * a vertex 1/Z is rcp_rn(Z) <= (1 + 2^-24) / zlo and every fragment q <=
+//     (1 + 2^-8) x its triangle's largest vertex 1/Z (spec v5, raster.h), so
+//     qb = rcp_rn(zlo) (1 + 2^-7) bounds them all (rounding included).
+// back is false (never tested) when some corner is not in front of the camera.
 __device__ __forceinline__ short4 meshlet_rect(gptr<const float> mb, const float* Rf,
-                                               const Cam32& c, int W, int H, float& zmin) {
+                                               const Cam32& c, int W, int H, float& zmin,
+                                               float& qb, bool& back) {
   float umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
   bool full = false;
   zmin = INFINITY;
-  // the 96 B of corners in six 16-B loads, all in flight before the first use
-  f32x4 cb[6];
+  // the 96 B of corners in six 16-B loads + cone and sphere, all in flight
+  // before the first use
+  f32x4 cb[kMletFloats / 4];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) cb[k] = *(gptr<const f32x4>)(mb + 4 * k);
+  for (int k = 0; k < kMletFloats / 4; ++k) cb[k] = *(gptr<const f32x4>)(mb + 4 * k);
+  {
+    const f32x4 cone = cb[6], sph = cb[7];
+    const float X = ((Rf[0] * sph.x + Rf[1] * sph.y) + Rf[2] * sph.z) + Rf[9];
+    const float Y = ((Rf[3] * sph.x + Rf[4] * sph.y) + Rf[5] * sph.z) + Rf[10];
+    const float Z = ((Rf[6] * sph.x + Rf[7] * sph.y) + Rf[8] * sph.z) + Rf[11];
+    const float ax = (Rf[0] * cone.x + Rf[1] * cone.y) + Rf[2] * cone.z;
+    const float ay = (Rf[3] * cone.x + Rf[4] * cone.y) + Rf[5] * cone.z;
+    const float az = (Rf[6] * cone.x + Rf[7] * cone.y) + Rf[8] * cone.z;
+    const float va = (X * ax + Y * ay) + Z * az, vv = (X * X + Y * Y) + Z * Z;
+    const float s = sqrtf(fmaxf(vv - va * va, 0.0f));
+    const float sina = sqrtf(fmaxf(1.0f - cone.w * cone.w, 0.0f));
+    back = cone.w > 0.0f && va * cone.w - s * sina > sph.w;
+  }
   float cf[24];
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
@@ -164,9 +195,11 @@ __device__ __forceinline__ short4 meshlet_rect(gptr<const float> mb, const float
     cf[4 * k + 2] = cb[k].z;
     cf[4 * k + 3] = cb[k].w;
   }
+  float rho1 = 0.0f;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const float x = cf[3 * k], y = cf[3 * k + 1], z = cf[3 * k + 2];
+    rho1 = fmaxf(rho1, (fabsf(x) + fabsf(y)) + fabsf(z));
     const float X = ((Rf[0] * x + Rf[1] * y) + Rf[2] * z) + Rf[9];
     const float Y = ((Rf[3] * x + Rf[4] * y) + Rf[5] * z) + Rf[10];
     const float Z = ((Rf[6] * x + Rf[7] * y) + Rf[8] * z) + Rf[11];
@@ -182,8 +215,17 @@ __device__ __forceinline__ short4 meshlet_rect(gptr<const float> mb, const float
       vmax = fmaxf(vmax, v);
     }
   }
-  if (full || !(umin == umin) || !(vmin == vmin) || !(umax == umax) || !(vmax == vmax))
+  {
+    // |R_2j| may exceed 1 for a non-rotation input: scale the L1 bound by it
+    const float m = fmaxf(fmaxf(fabsf(Rf[6]), fabsf(Rf[7])), fmaxf(fabsf(Rf[8]), 1.0f));
+    const float zlo = zmin - 0x1p-19f * (m * rho1 + fabsf(Rf[11]));
+    qb = rcp_rn(zlo > 0.0f ? zlo : 1.0f) * 1.0078125f;  // (1 + 2^-7) / zlo
+    back = back && !full && zlo > 0.0f && qb < 0x1p100f;
+  }
+  if (full || !(umin == umin) || !(vmin == vmin) || !(umax == umax) || !(vmax == vmax)) {
+    back = false;
     return make_short4(0, 0, (short)(W - 1), (short)(H - 1));
+  }
   // Column c is sampled at c + 0.5 and covered only if that centre is inside a
   // triangle, i.e. within [min, max] of the snapped vertex u (snap error
   // 1/512 px). The corners bound the vertices exactly; their float32
@@ -376,6 +418,15 @@ constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 // by that (raster.h), and q-buffer values only grow, so a value read while other
 // waves still write is a lower bound of the final one. The result is
 // bit-identical with or without the test (VsdArgs::cull, BOPX_VSD_CULL=0).
+// Back-face occlusion test (VsdArgs::cull == 3, off by default: +3.5 % on the
+// bench workload, round 2). Its claim-loop block stays compiled in either way:
+// the second loop latch (`continue` of a fully occluded group) changes the
+// register allocation of the whole claim loop from 128 VGPRs + 5 spilled to 114
+// without spills, -2.9 % k_vsd time with the test off (same-box A/B, round 2).
+// BOPX_VSD_BACKCULL=0 drops the block (and that allocation).
+#ifndef BOPX_VSD_BACKCULL
+#define BOPX_VSD_BACKCULL 1
+#endif
 #ifndef BOPX_VSD_PRIO
 #define BOPX_VSD_PRIO 3
 #endif
@@ -444,6 +495,10 @@ void k_vsd(VsdArgs a) {
   constexpr int kListLen = RPT * kVsdThreads;  // >= 2 * nm (launch_vsd)
   using ListT = typename std::conditional<kCull, uint32_t, uint16_t>::type;
   __shared__ __attribute__((aligned(4))) ListT s_list[kListLen];
+  // Back-face occlusion test (cull 3): per entry, its fragment bound qb as an
+  // 8-bit code below the pose's largest bound: qb <= s_qhi[pose] 2^(-code/64).
+  __shared__ uint8_t s_qb[kCull ? kListLen : 4];
+  __shared__ float s_qhi[2];
   __shared__ float s_zr[2][2];  // per pose: depth range of the meshlet corners (min, max)
   __shared__ int s_next;
   __shared__ __attribute__((aligned(16))) float s_pose[2][12];
@@ -513,13 +568,18 @@ void k_vsd(VsdArgs a) {
     s_roi[2] = s_roi[3] = -1;
     s_zr[0][0] = s_zr[1][0] = INFINITY;
     s_zr[0][1] = s_zr[1][1] = 0.0f;
+    s_qhi[0] = s_qhi[1] = 0.0f;
   }
   __syncthreads();
+  const bool cull_back = kCull && a.cull == 3;  // wave-uniform
 
   // 1. per-pose meshlet rectangles (kept in registers: entry tid + 512 j) + ROI,
   // and each entry's nearest corner depth (queue order, see BOPX_VSD_PRIO above).
   short4 rect[RPT];
   float zmin[RPT];
+  float qbv[RPT];           // fragment bound per entry (back-face test)
+  uint32_t back_bits = 0;   // bit j: entry tid + 512 j is back-facing
+  float qh[2] = {0.0f, 0.0f};  // per pose: largest bound of a back-facing entry
   int roi[4] = {INT32_MAX, INT32_MAX, -1, -1};
   float zr[4] = {INFINITY, -INFINITY, INFINITY, -INFINITY};  // pose 0 min, max; pose 1
 #pragma unroll
@@ -527,10 +587,17 @@ void k_vsd(VsdArgs a) {
     const int i = tid + j * kVsdThreads;
     rect[j] = make_short4(1, 1, 0, 0);
     zmin[j] = -INFINITY;
+    qbv[j] = 0.0f;
     if (i < 2 * nm && !(COST == kCostGtInfo && i < nm)) {  // GT-info: gt pose only
       const int r = i >= nm, m = i - r * nm;
-      rect[j] = meshlet_rect(g_mlet + 24 * (int64_t)m, s_pose[r], c32, W, H, zmin[j]);
+      bool bk = false;
+      rect[j] = meshlet_rect(g_mlet + kMletFloats * (int64_t)m, s_pose[r], c32, W, H, zmin[j],
+                             qbv[j], bk);
       if (rect[j].x <= rect[j].z && rect[j].y <= rect[j].w) {
+        if (bk) {
+          back_bits |= 1u << j;
+          qh[r] = fmaxf(qh[r], qbv[j]);
+        }
         roi[0] = min(roi[0], (int)rect[j].x);
         roi[1] = min(roi[1], (int)rect[j].y);
         roi[2] = max(roi[2], (int)rect[j].z);
@@ -558,6 +625,14 @@ void k_vsd(VsdArgs a) {
         int* z = reinterpret_cast<int*>(&s_zr[0][0]) + k;
         if (k & 1) atomicMax(z, __float_as_int(fmaxf(zr[k], 0.0f)));
         else atomicMin(z, __float_as_int(zr[k]));
+      }
+    }
+    if (cull_back) {
+      qh[0] = wave_max_nonneg_f32(qh[0]);
+      qh[1] = wave_max_nonneg_f32(qh[1]);
+      if (lane == 0) {
+        atomicMax(reinterpret_cast<int*>(&s_qhi[0]), __float_as_int(qh[0]));
+        atomicMax(reinterpret_cast<int*>(&s_qhi[1]), __float_as_int(qh[1]));
       }
     }
   }
@@ -589,6 +664,21 @@ void k_vsd(VsdArgs a) {
     const int r = i >= nm;
     const float zmid = 0.5f * (s_zr[r][0] + s_zr[r][1]);
     far_bits |= (uint32_t)(zmin[j] > zmid) << j;
+  }
+  if (cull_back) {
+    // back-facing entries take the "far" bit (tested, queued last); their
+    // bound as a conservative code: 2^(-code/64) >= qb / qhi (log/exp2 errors
+    // ~1e-6 against the 0.05 / 64 slack), clamped to [0, 255] (still >= qb)
+    far_bits = back_bits;
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int i = tid + j * kVsdThreads;
+      if ((back_bits >> j) & 1u) {
+        const float qhi = s_qhi[i >= nm];
+        const float cf = floorf(64.0f * (__log2f(qhi) - __log2f(qbv[j])) - 0.05f);
+        s_qb[i] = (uint8_t)fminf(fmaxf(cf, 0.0f), 255.0f);
+      }
+    }
   }
   double thr[NT];  // wave-uniform (SGPRs)
 #pragma unroll
@@ -646,7 +736,7 @@ void k_vsd(VsdArgs a) {
             word |= (far << 11) | (x0 << 12) | (x1 << 17) | (y0 << 22) | (y1 << 27);
           }
           bool front = !far;
-          if (a.qorder) {
+          if (a.qorder && !cull_back) {
             const int ow = min((int)rc.z, tx1) - max((int)rc.x, tx0) + 1;
             const int oh = min((int)rc.w, ty1) - max((int)rc.y, ty0) + 1;
             front = ow * oh >= kLptOverlap;
@@ -708,6 +798,30 @@ void k_vsd(VsdArgs a) {
           mlt[g] = e - pose[g] * nm;
           ent[g] = e;
         }
+        // Back-face occlusion test (cull 3), before any of the entry's data is
+        // fetched: skipped when every pixel of its rectangle in the tile already
+        // holds q >= its fragment bound. q values only grow, so a value read
+        // while other waves still write is a lower bound of the final one.
+        uint32_t dead = 0;  // wave-uniform: bit g = entry g skipped
+        if constexpr (kCull && BOPX_VSD_BACKCULL) {
+          if (cull_back) {
+#pragma unroll
+            for (int g = 0; g < kGroup; ++g) {
+              if (base + g >= nl) {
+                dead |= 1u << g;
+              } else if ((word[g] >> 11) & 1u) {
+                const float qbd = s_qhi[pose[g]] *
+                                  __builtin_amdgcn_exp2f(-(float)s_qb[ent[g]] * (1.0f / 64.0f));
+                const Region rg = make_region(word[g], tx1 - tx0 + 1, ty1 - ty0 + 1);
+                if (region_covered(s_dep[pose[g]], rg, 0, __float_as_uint(qbd), lane)) {
+                  dead |= 1u << g;
+                  if (VSD_DIAG(4) && lane == 0) atomicAdd(&g_vsd_stats[9], 1ull);
+                }
+              }
+            }
+            if (dead == (1u << kGroup) - 1u) continue;  // nothing left to draw
+          }
+        }
         // all loads of the group in flight before the first use
 #pragma unroll
         for (int g = 0; g < kGroup; ++g)
@@ -715,7 +829,8 @@ void k_vsd(VsdArgs a) {
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
           pk[g] = ld_off(g_mtri + mlt[g] * kMeshletTris, (uint32_t)lane * 4u);  // entry is valid
-          if (base + g >= nl) pk[g] = 0xFFFFFFFFu;  // (clamped duplicate, no triangles)
+          // (clamped duplicate or occluded: no triangles)
+          if (base + g >= nl || ((dead >> g) & 1u)) pk[g] = 0xFFFFFFFFu;
         }
         // occlusion test of far entries, part 1: the q reads of the region's
         // first 8 steps go out now, behind the vertex loads, and are compared
@@ -727,7 +842,7 @@ void k_vsd(VsdArgs a) {
           qmin[g] = 0xFFFFFFFFu;
           test[g] = false;
           if constexpr (kCull) {
-            test[g] = a.cull && ((word[g] >> 11) & 1u) && base + g < nl;
+            test[g] = (a.cull == 1 || a.cull == 2) && ((word[g] >> 11) & 1u) && base + g < nl;
             if (test[g])
               qmin[g] = region_min8(s_dep[pose[g]],
                                     make_region(word[g], tx1 - tx0 + 1, ty1 - ty0 + 1), 0, lane);

@@ -448,6 +448,55 @@ static void obb_corners(const std::vector<float4>& vtx, const std::vector<uint32
   }
 }
 
+// Normal cone + bounding sphere of one meshlet (8 floats appended to its 24
+// corner floats, kMletFloats per meshlet): unit axis a, cos(alpha), centre c,
+// radius r. Every triangle normal (outward: `sign` = orientation of the whole
+// mesh from its signed volume) lies within alpha of a, and every vertex within
+// r of c. k_vsd uses it only to classify (pose, meshlet) entries as back-facing
+// (tested for occlusion, queued last): a wrong class costs time, never a bit.
+// cos(alpha) = -2 marks a meshlet that is never back-facing (alpha >= 90 deg).
+static void meshlet_cone(const std::vector<float4>& vtx, const uint32_t* tri, int32_t ntri,
+                         double sign, std::vector<float>& out) {
+  const float* cr = out.data() + out.size() - 24;  // this meshlet's OBB corners
+  double c[3] = {0, 0, 0}, r = 0;
+  for (int k = 0; k < 8; ++k)
+    for (int i = 0; i < 3; ++i) c[i] += cr[3 * k + i] / 8.0;
+  for (int k = 0; k < 8; ++k) {
+    const double d[3] = {cr[3 * k] - c[0], cr[3 * k + 1] - c[1], cr[3 * k + 2] - c[2]};
+    r = std::max(r, std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]));
+  }
+  std::vector<double> nrm;
+  double ax[3] = {0, 0, 0};
+  for (int32_t t = 0; t < ntri; ++t) {
+    const float4 p0 = vtx[tri[3 * t]], p1 = vtx[tri[3 * t + 1]], p2 = vtx[tri[3 * t + 2]];
+    const double e1[3] = {(double)p1.x - p0.x, (double)p1.y - p0.y, (double)p1.z - p0.z};
+    const double e2[3] = {(double)p2.x - p0.x, (double)p2.y - p0.y, (double)p2.z - p0.z};
+    double n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                   e1[0] * e2[1] - e1[1] * e2[0]};
+    const double len = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    if (!(len > 0)) continue;  // degenerate: no fragments, no constraint
+    for (int i = 0; i < 3; ++i) {
+      n[i] *= sign / len;
+      ax[i] += n[i];
+      nrm.push_back(n[i]);
+    }
+  }
+  const double alen = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+  double cosa = -2.0;
+  if (alen > 0 && !nrm.empty()) {
+    for (int i = 0; i < 3; ++i) ax[i] /= alen;
+    cosa = 1.0;
+    for (size_t k = 0; k < nrm.size(); k += 3)
+      cosa = std::min(cosa, nrm[k] * ax[0] + nrm[k + 1] * ax[1] + nrm[k + 2] * ax[2]);
+    cosa -= 1e-6;  // rounding slack (a heuristic either way)
+    if (!(cosa > 0.0)) cosa = -2.0;
+  }
+  for (int i = 0; i < 3; ++i) out.push_back((float)ax[i]);
+  out.push_back((float)cosa);
+  for (int i = 0; i < 3; ++i) out.push_back((float)c[i]);
+  out.push_back((float)(r * (1.0 + 1e-6) + 1e-3));
+}
+
 // Meshlet partitions of the faces (host, once per object; the raster result
 // does not depend on them, only k_vsd's culling work does).
 // greedy: consecutive runs of the Morton order of the face centroids.
@@ -596,6 +645,15 @@ int bopx_add_object(bopx_ctx* c, int obj_id, const double* pts, int64_t nv,
     // words hold 8-bit local vertex indices a | b << 8 | c << 16.
     std::vector<int32_t> local(nv, -1);
     std::vector<uint32_t> touched;
+    // orientation of the mesh (signed volume): outward normals for the cones
+    double vol = 0.0;
+    for (int64_t t = 0; t < nf; ++t) {
+      const float4 p0 = vtx[faces[3 * t]], p1 = vtx[faces[3 * t + 1]], p2 = vtx[faces[3 * t + 2]];
+      vol += (double)p0.x * ((double)p1.y * p2.z - (double)p1.z * p2.y) +
+             (double)p0.y * ((double)p1.z * p2.x - (double)p1.x * p2.z) +
+             (double)p0.z * ((double)p1.x * p2.y - (double)p1.y * p2.x);
+    }
+    const double sign = vol < 0.0 ? -1.0 : 1.0;
     int64_t f = 0;
     for (const int32_t sz : msize) {
       const int32_t tri0 = (int32_t)f, vtx0 = (int32_t)mvtx.size();
@@ -615,6 +673,7 @@ int bopx_add_object(bopx_ctx* c, int obj_id, const double* pts, int64_t nv,
         mtri.push_back(pk);
       }
       obb_corners(vtx, touched, mlet);
+      meshlet_cone(vtx, fsorted.data() + 3 * (size_t)tri0, sz, sign, mlet);
       for (uint32_t v : touched) local[v] = -1;
       const float4 pad = mvtx[vtx0];
       while (mvtx.size() - vtx0 < (size_t)bopx::kMeshletVerts) mvtx.push_back(pad);
@@ -822,7 +881,11 @@ static float visib_thr32(double delta, int flags) {
 // k_vsd's occlusion test of far meshlet entries (bit-identical results either
 // way; off by default: on the bench workload its test cost equals the raster
 // work it saves). Read per call, so a test can compare the two:
-// BOPX_VSD_CULL=1 on, 0 off, 2 test only (timing).
+// BOPX_VSD_CULL=1 on, 0 off, 2 test only (timing), 3 back-face occlusion test
+// (meshlet normal cones: back-facing entries queued last and tested against
+// their corner bound before any of their data is fetched; round 2, same box:
+// 17 % of the entries skipped, 16 % fewer set-ups, but +3.5 % time — the test's
+// LDS round trips sit in the tile's tail, kern_vsd.hip).
 static int vsd_cull_enabled() {
   const char* e = getenv("BOPX_VSD_CULL");
   return e ? atoi(e) : 0;

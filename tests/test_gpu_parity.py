@@ -293,7 +293,8 @@ def _bumpy_mesh(seed, n_lat=40, n_lon=80, amp=0.35):
   return pts.astype(np.float32).astype(np.float64), faces
 
 
-@pytest.mark.parametrize("cull,qorder", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")])
+@pytest.mark.parametrize("cull,qorder", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0"),
+                                         ("3", "1")])
 def test_fused_vsd_occlusion_cull_exact(oracle_mod, monkeypatch, cull, qorder):
   """k_vsd's occlusion test of far meshlet entries (BOPX_VSD_CULL) and both
   tile entry-queue orders (BOPX_VSD_QORDER: large overlaps first / near first)
@@ -307,6 +308,22 @@ def test_fused_vsd_occlusion_cull_exact(oracle_mod, monkeypatch, cull, qorder):
   assert np.ptp(out) > 0.1
   flat = synth.superellipsoid(30, 60, (70.0, 50.0, 0.02), 0.9)
   _fused_vs_oracle(oracle_mod, 42, 24, 640, 480, synth.LMO_K, 0, 0, mesh=flat)
+
+
+def test_fused_vsd_backface_cull_open_and_flipped(oracle_mod, monkeypatch):
+  """The back-face occlusion test (BOPX_VSD_CULL=3) classifies meshlets with
+  normal cones of the mesh's orientation; it must stay bit-exact when that
+  classification is wrong: an open mesh (the inside of a bowl is visible) and
+  the same mesh with every triangle's winding flipped."""
+  from bop_toolkit_amd import synth
+  monkeypatch.setenv("BOPX_VSD_CULL", "3")
+  pts, faces = _bumpy_mesh(5)
+  cen = pts[faces].mean(1)
+  bowl = faces[cen[:, 2] < 0.3 * cen[:, 2].max()]
+  _fused_vs_oracle(oracle_mod, 43, 24, 640, 480, synth.YCBV_K, 0, 0, mesh=(pts, bowl),
+                   z_range=(500.0, 900.0))
+  _fused_vs_oracle(oracle_mod, 44, 24, 640, 480, synth.YCBV_K, 0, 0,
+                   mesh=(pts, np.ascontiguousarray(faces[:, ::-1])), z_range=(500.0, 900.0))
 
 
 def test_drop_in_vsd_with_hip_renderer(oracle_mod):
