@@ -36,7 +36,7 @@ constexpr int kMletFloats = 32;     // per-meshlet culling record (ObjDesc::mlet
 #define BOPX_TILE_W 64
 #define BOPX_TILE_H 64
 #endif
-constexpr int kMaxMeshlets = BOPX_MAX_MESHLETS;  // per object (VSD)
+constexpr int kMaxMeshlets = BOPX_MAX_MESHLETS;  // per object with rectangles in registers (VSD)
 constexpr int kMaxTaus = 16;
 constexpr int kVsdMaxTiles = 2048;  // k_vsd keeps 16-bit per-lane tau counters
 constexpr int kCostCover = 2;  // k_vsd mode: silhouette union/inter + bboxes (cus, cou_bb_proj)

@@ -468,6 +468,9 @@ constexpr int kVsdFirstClaim = BOPX_VSD_PRECLAIM ? kVsdWaves * kGroup : 0;
 // RPT: meshlet rectangles held per thread (1, 2 or 4): the launch picks the
 // smallest that covers 2 x the most meshlets of any registered object, so
 // objects of up to 16k triangles keep 6 fewer VGPRs live through the tile loop.
+// RPT 0 (objects of more than kMaxMeshlets meshlets, no size limit): the
+// rectangles are not kept but recomputed per tile, kListLen entries per round,
+// each round listed and rasterised into the same q tiles before the pixel pass.
 template <int COST, int RPT, int NT>
 // Workgroups per CU: 3 with register records and <= 512 meshlet entries
 // (6 waves per SIMD: VGPRs <= 80), else 2 (4 waves per SIMD: VGPRs <= 128).
@@ -491,8 +494,10 @@ void k_vsd(VsdArgs a) {
   // entry | far << 11 | rectangle in the tile at 2-px granularity (x0/2, x1/2,
   // y0/2, y1/2: 5 bits each from bit 12) for the occlusion test; RPT 4: 16-bit
   // entry indices, no occlusion test (the list would not fit the LDS budget).
-  constexpr bool kCull = RPT <= 2;
-  constexpr int kListLen = RPT * kVsdThreads;  // >= 2 * nm (launch_vsd)
+  constexpr bool kStream = RPT == 0;
+  constexpr int kR = kStream ? 4 : RPT;  // rectangles per thread and round
+  constexpr bool kCull = RPT >= 1 && RPT <= 2;
+  constexpr int kListLen = kR * kVsdThreads;  // >= 2 * nm (launch_vsd) unless kStream
   using ListT = typename std::conditional<kCull, uint32_t, uint16_t>::type;
   __shared__ __attribute__((aligned(4))) ListT s_list[kListLen];
   // Back-face occlusion test (cull 3): per entry, its fragment bound qb as an
@@ -575,16 +580,18 @@ void k_vsd(VsdArgs a) {
 
   // 1. per-pose meshlet rectangles (kept in registers: entry tid + 512 j) + ROI,
   // and each entry's nearest corner depth (queue order, see BOPX_VSD_PRIO above).
-  short4 rect[RPT];
-  float zmin[RPT];
-  float qbv[RPT];           // fragment bound per entry (back-face test)
+  short4 rect[kR];
+  float zmin[kR];
+  float qbv[kR];            // fragment bound per entry (back-face test)
   uint32_t back_bits = 0;   // bit j: entry tid + 512 j is back-facing
   float qh[2] = {0.0f, 0.0f};  // per pose: largest bound of a back-facing entry
   int roi[4] = {INT32_MAX, INT32_MAX, -1, -1};
   float zr[4] = {INFINITY, -INFINITY, INFINITY, -INFINITY};  // pose 0 min, max; pose 1
+  // (kStream: every entry, the rectangles are only reduced into the ROI here)
+  for (int i0 = 0; i0 < (kStream ? 2 * nm : 1); i0 += kListLen)
 #pragma unroll
-  for (int j = 0; j < RPT; ++j) {
-    const int i = tid + j * kVsdThreads;
+  for (int j = 0; j < kR; ++j) {
+    const int i = (kStream ? i0 : 0) + tid + j * kVsdThreads;
     rect[j] = make_short4(1, 1, 0, 0);
     zmin[j] = -INFINITY;
     qbv[j] = 0.0f;
@@ -712,7 +719,10 @@ void k_vsd(VsdArgs a) {
       // already zero, see the pixel pass). The queue counters were reset behind
       // the previous tile's raster-end barrier (or before the loop), so no
       // barrier is needed here: the previous tile's pixel-end barrier orders it.
-      if (!BOPX_VSD_EARLY_RESET) {
+      // kStream: one round per kListLen entries (a single round otherwise)
+      for (int e0 = 0; e0 < (kStream ? 2 * nm : 1); e0 += kListLen) {
+      if (kStream && e0 > 0) __syncthreads();  // every wave is done with the last round's queue
+      if (!BOPX_VSD_EARLY_RESET || kStream) {
         if (tid == 0) {
           s_nlist = 0;
           s_nsmall = 0;
@@ -722,8 +732,20 @@ void k_vsd(VsdArgs a) {
       }
       VSD_STAMP(0);
 #pragma unroll
-      for (int j = 0; j < RPT; ++j) {
-        const short4 rc = rect[j];
+      for (int j = 0; j < kR; ++j) {
+        short4 rc;
+        if constexpr (kStream) {  // recomputed (round e0, entry e0 + tid + 512 j)
+          const int i = e0 + tid + j * kVsdThreads;
+          rc = make_short4(1, 1, 0, 0);
+          if (i < 2 * nm && !(COST == kCostGtInfo && i < nm)) {
+            const int r = i >= nm, m = i - r * nm;
+            float zm, qq;
+            bool bk;
+            rc = meshlet_rect(g_mlet + kMletFloats * (int64_t)m, s_pose[r], c32, W, H, zm, qq, bk);
+          }
+        } else {
+          rc = rect[j];
+        }
         if (rc.x <= tx1 && rc.z >= tx0 && rc.y <= ty1 && rc.w >= ty0 && rc.x <= rc.z &&
             rc.y <= rc.w) {
           const uint32_t far = (far_bits >> j) & 1u;
@@ -793,7 +815,7 @@ void k_vsd(VsdArgs a) {
         int mlt[kGroup];
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
-          const int e = (int)(word[g] & 0x7FFu);
+          const int e = (kStream ? e0 : 0) + (int)(word[g] & 0x7FFu);
           pose[g] = e >= nm ? 1 : 0;  // uniform (SGPR): e came through readfirstlane
           mlt[g] = e - pose[g] * nm;
           ent[g] = e;
@@ -1094,6 +1116,7 @@ void k_vsd(VsdArgs a) {
         }
         wave_lds_sync();  // the staging area is rewritten by the next group
       }
+      }  // rounds (kStream)
       // Touch the test-depth lines of this wave's pixel rows (w, w + 8, ...)
       // while it waits for the other waves at the raster-end barrier: the
       // pixel pass then reads them from L2 instead of HBM. The empty asm below
@@ -1430,8 +1453,10 @@ hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s) {
     launch_vsd_rpt<1>(a, cost_type, s);
   else if (need <= 2 * kVsdThreads)
     launch_vsd_rpt<2>(a, cost_type, s);
-  else
+  else if (need <= kRectsPerThread * kVsdThreads)
     launch_vsd_rpt<kRectsPerThread>(a, cost_type, s);
+  else
+    launch_vsd_rpt<0>(a, cost_type, s);  // rectangles recomputed per tile (any size)
   return hipGetLastError();
 }
 

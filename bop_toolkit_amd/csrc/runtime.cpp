@@ -301,9 +301,6 @@ int map_slots(bopx_ctx* c, int64_t n, const int32_t* obj_ids, std::vector<int32_
       return fail(c, BOPX_E_INVALID, "obj_id %d has no symmetry set", obj_ids[i]);
     if (need_faces && o.nf <= 0)
       return fail(c, BOPX_E_INVALID, "obj_id %d has no faces", obj_ids[i]);
-    if (need_faces && o.nm > bopx::kMaxMeshlets)
-      return fail(c, BOPX_E_UNSUPPORTED, "obj_id %d: %lld meshlets > %d", obj_ids[i],
-                  (long long)o.nm, bopx::kMaxMeshlets);
     slots[i] = s;
   }
   return BOPX_OK;

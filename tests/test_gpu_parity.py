@@ -545,6 +545,33 @@ def test_fused_vsd_bit_exact_large_meshes(oracle_mod):
   _fused_vs_oracle(oracle_mod, 16, 6, 640, 480, synth.LMO_K, 150, 200)   # 60k tris: RPT 4
 
 
+def test_huge_mesh_streamed_rects(oracle_mod):
+  """An object beyond the register-resident limit (> 1024 meshlets, here
+  110k triangles): k_vsd recomputes the meshlet rectangles per tile and
+  rasterises them in rounds of 2048 entries (RPT 0). VSD and the silhouette
+  mode stay bit-exact; no size limit is left."""
+  from bop_toolkit_amd import _lib, synth
+  from bop_toolkit_amd._lib import _d, _i32, ptr
+  _fused_vs_oracle(oracle_mod, 19, 4, 640, 480, synth.LMO_K, 220, 250)
+  n = 4
+  rng, pts, faces, Rg, tg, Re, te_, K = _scene(20, n, n_lat=220, n_lon=250)
+  assert len(faces) > 64 * 1024
+  ctx = _lib.Context(0)
+  ctx.add_object(4, pts, faces)
+  fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+  pe = np.concatenate([Re.reshape(n, 9), te_], 1)
+  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
+  cam = np.array([[fx, fy, cx, cy]], np.float64)
+  out = np.empty((n, 10))
+  ctx.call("bopx_cover_batch", n, ptr(np.full(n, 4, np.int32), _i32), ptr(pe, _d), ptr(pg, _d),
+           ptr(np.zeros(n, np.int32), _i32), 1, 640, 480, ptr(cam, _d), ptr(out, _d))
+  for i in range(n):
+    de = oracle_mod.render_depth(pts, faces, Re[i], te_[i], fx, fy, cx, cy, 640, 480)
+    dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, 640, 480)
+    assert np.array_equal(out[i], _cover_ref(de, dg)), i
+  ctx.close()
+
+
 def test_fused_vsd_bit_exact_large_images(oracle_mod):
   """ITODD-like 1280x960 (delta 5, dataset_params.py) and HOPE-like 1920x1080
   frames: many tiles per tuple, bit-exact."""
