@@ -108,6 +108,14 @@ class BatchEvaluator:
     code = {"step": _lib.COST_STEP, "tlinear": _lib.COST_TLINEAR}.get(cost_type)
     if code is None:
       raise ValueError("Unknown pixel matching cost.")
+    if len(taus) > _lib.MAX_TAUS:  # one launch per MAX_TAUS thresholds (any number of taus)
+      out = self._out(n, len(taus)) if out is None else out
+      for k0 in range(0, len(taus), _lib.MAX_TAUS):
+        k1 = min(k0 + _lib.MAX_TAUS, len(taus))
+        out[:, k0:k1] = self.vsd(slots, pose_est, pose_gt, frame_idx, frames, cam, delta,
+                                 taus[k0:k1], diameters, normalized_by_diameter, cost_type,
+                                 delta_flags=delta_flags)
+      return out
     H, W = int(frames.shape[-2]), int(frames.shape[-1])
     out = self._out(n, len(taus)) if out is None else out
     self.ctx.call("bopx_vsd_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(frame_idx),

@@ -25,6 +25,12 @@ def _cost_code(cost_type):
   return {"step": _lib.COST_STEP, "tlinear": _lib.COST_TLINEAR}.get(cost_type)
 
 
+def _tau_chunks(n):
+  """[k0, k1) ranges of at most MAX_TAUS thresholds (one kernel call each; the
+  reference takes any number of taus)."""
+  return [(k0, min(k0 + _lib.MAX_TAUS, n)) for k0 in range(0, n, _lib.MAX_TAUS)]
+
+
 def vsd(R_est, t_est, R_gt, t_gt, depth_test, K, delta, taus, normalized_by_diameter,
         diameter, renderer, obj_id, cost_type="step"):
   """Visible Surface Discrepancy (pose_error.py:17-93).
@@ -36,8 +42,6 @@ def vsd(R_est, t_est, R_gt, t_gt, depth_test, K, delta, taus, normalized_by_diam
   Returns a list of len(taus) floats; [1.0] * len(taus) for an empty union.
   """
   taus = [float(t) for t in taus]
-  if len(taus) > _lib.MAX_TAUS:
-    raise ValueError("at most %d taus are supported" % _lib.MAX_TAUS)
   ctx = runtime.context()
   fx, fy, cx, cy = float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2])
   depth_test = np.ascontiguousarray(depth_test, np.float32)
@@ -53,9 +57,12 @@ def vsd(R_est, t_est, R_gt, t_gt, depth_test, K, delta, taus, normalized_by_diam
     fi = np.zeros(1, np.int32)
     cam = np.array([fx, fy, cx, cy], np.float64)
     dia = np.array([float(diameter)], np.float64)
-    ctx.call("bopx_vsd_batch", 1, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(fi, _i32),
-             ptr(depth_test, _f), 1, W, H, ptr(cam, _d), float(delta), flags, ptr(tau_arr, _d),
-             len(taus), int(bool(normalized_by_diameter)), ptr(dia, _d), code, ptr(out, _d))
+    for k0, k1 in _tau_chunks(len(taus)):  # the kernels take MAX_TAUS per call
+      part, o = np.ascontiguousarray(tau_arr[k0:k1]), np.empty(k1 - k0, np.float64)
+      ctx.call("bopx_vsd_batch", 1, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(fi, _i32),
+               ptr(depth_test, _f), 1, W, H, ptr(cam, _d), float(delta), flags, ptr(part, _d),
+               k1 - k0, int(bool(normalized_by_diameter)), ptr(dia, _d), code, ptr(o, _d))
+      out[k0:k1] = o
     return [float(e) for e in out]
   depth_est = renderer.render_object(obj_id, R_est, t_est, fx, fy, cx, cy)["depth"]
   depth_gt = renderer.render_object(obj_id, R_gt, t_gt, fx, fy, cx, cy)["depth"]
@@ -63,10 +70,13 @@ def vsd(R_est, t_est, R_gt, t_gt, depth_test, K, delta, taus, normalized_by_diam
   dg = np.ascontiguousarray(depth_gt, np.float32)
   if not taus:
     return []
-  ctx.call("bopx_vsd_from_depths", W, H, ptr(depth_test, _f), ptr(de, _f), ptr(dg, _f), fx, fy,
-           cx, cy, float(delta), flags, ptr(tau_arr, _d), len(taus),
-           int(bool(normalized_by_diameter)), float(diameter),
-           code if code is not None else 99, ptr(out, _d))
+  for k0, k1 in _tau_chunks(len(taus)):
+    part, o = np.ascontiguousarray(tau_arr[k0:k1]), np.empty(k1 - k0, np.float64)
+    ctx.call("bopx_vsd_from_depths", W, H, ptr(depth_test, _f), ptr(de, _f), ptr(dg, _f), fx,
+             fy, cx, cy, float(delta), flags, ptr(part, _d), k1 - k0,
+             int(bool(normalized_by_diameter)), float(diameter),
+             code if code is not None else 99, ptr(o, _d))
+    out[k0:k1] = o
   return [float(e) for e in out]
 
 

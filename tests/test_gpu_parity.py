@@ -326,6 +326,42 @@ def test_fused_vsd_backface_cull_open_and_flipped(oracle_mod, monkeypatch):
                    mesh=(pts, np.ascontiguousarray(faces[:, ::-1])), z_range=(500.0, 900.0))
 
 
+def test_vsd_more_taus_than_one_launch(oracle_mod):
+  """The reference takes any number of taus; the kernels take MAX_TAUS per
+  launch, so 25 thresholds run in two launches (drop-in with the HIP renderer,
+  drop-in with a foreign renderer, batched): bit-exact vs the oracle."""
+  import torch
+  from bop_toolkit_amd import pose_error as pe, synth
+  from bop_toolkit_amd.batch import BatchEvaluator
+  from bop_toolkit_amd.renderer import create_renderer
+  rng, pts, faces, Rg, tg, Re, te_, K = _scene(31, 3)
+  taus = list(np.linspace(0.02, 0.6, 25))
+  fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+  ren = create_renderer(640, 480, "hip", mode="depth")
+  ren.add_object_arrays(23, pts, faces)
+
+  class Foreign:
+    def render_object(self, obj_id, R, t, fx, fy, cx, cy):
+      return {"depth": oracle_mod.render_depth(pts, faces, R, t, fx, fy, cx, cy, 640, 480)}
+
+  ev = BatchEvaluator(0)
+  ev.add_object(23, pts, faces)
+  for i in range(3):
+    dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, 640, 480)
+    de = oracle_mod.render_depth(pts, faces, Re[i], te_[i], fx, fy, cx, cy, 640, 480)
+    dt = np.where(dg > 0, dg + 2.0, 0.0).astype(np.float32)
+    ref = oracle_mod.vsd_depths(dt, de, dg, fx, fy, cx, cy, 15.0, taus, True, 150.0)
+    for r in (ren, Foreign()):
+      assert pe.vsd(Re[i], te_[i].reshape(3, 1), Rg[i], tg[i].reshape(3, 1), dt, K, 15.0, taus,
+                    True, 150.0, r, 23, "step") == ref
+    T = lambda a, dt_=torch.float64: torch.as_tensor(np.asarray(a), dtype=dt_, device=ev.device)
+    out = ev.vsd(ev.slots([23]),
+                 T(np.concatenate([Re[i].reshape(9), te_[i]])[None]),
+                 T(np.concatenate([Rg[i].reshape(9), tg[i]])[None]), T([0], torch.int32),
+                 T(dt[None], torch.float32), T([[fx, fy, cx, cy]]), 15.0, taus, T([150.0]))
+    assert out.cpu().numpy()[0].tolist() == ref
+
+
 def test_drop_in_vsd_with_hip_renderer(oracle_mod):
   from bop_toolkit_amd import pose_error as pe, synth
   from bop_toolkit_amd.renderer import create_renderer
