@@ -212,9 +212,24 @@ def row_to_errors(et, row):
   return [float(row[0])]
 
 
+def todo_images(recs, todo):
+  """Sorted image ids of the tuples in todo (one test-depth frame each)."""
+  return sorted({recs[ri]["im_id"] for ri, _, _, _ in todo})
+
+
+def load_scene_depths(dp_split, scene_camera, scene_id, ims):
+  """Test depth of the images ims in mm, float32 (eval_calc_errors.py:240-243)."""
+  depths = inout.load_depths(dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id)
+                             for im_id in ims)
+  for k, im_id in enumerate(ims):
+    depths[k] *= scene_camera[im_id]["depth_scale"]  # float32 in place, :242-243
+  return depths
+
+
 def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, models_info,
-                   symmetric_ids, todo):
-  """Raw float64 rows [len(todo), C] of the GPU evaluation of todo."""
+                   symmetric_ids, todo, depths=None):
+  """Raw float64 rows [len(todo), C] of the GPU evaluation of todo (depths:
+  the frames of todo_images(recs, todo), or None to load them here)."""
   et = p["error_type"]
   dev = ev.device
   n = len(todo)
@@ -225,7 +240,7 @@ def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs
   slots = ev.slots(obj)
   d_pe, d_pg = T(pe, torch.float64), T(pg, torch.float64)
   if et in ("vsd", "cus"):
-    ims = sorted({recs[ri]["im_id"] for ri, _, _, _ in todo})
+    ims = todo_images(recs, todo)
     frame_of = {im: k for k, im in enumerate(ims)}
     cam = np.array([[K[0, 0], K[1, 1], K[0, 2], K[1, 2]]
                     for K in (scene_camera[im]["cam_K"] for im in ims)], np.float64)
@@ -234,10 +249,8 @@ def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs
     if et == "cus":
       W, H = dp_split["im_size"]
       return ev.cover(slots, d_pe, d_pg, fidx, T(cam, torch.float64), W, H)
-    depths = inout.load_depths(dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id)
-                               for im_id in ims)
-    for k, im_id in enumerate(ims):
-      depths[k] *= scene_camera[im_id]["depth_scale"]  # float32 in place, :242-243
+    if depths is None:
+      depths = load_scene_depths(dp_split, scene_camera, scene_id, ims)
     dia = np.array([models_info[o]["diameter"] for o in obj], np.float64)
     delta = p["vsd_deltas"][dataset]
     from . import runtime
@@ -283,19 +296,21 @@ def shard_todo(recs, todo, world, costs=None):
 
 
 def evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, models_info,
-             symmetric_ids, batch_fn=None):
+             symmetric_ids, batch_fn=None, planned=None):
   """errors dict per record. The gated-in tuples of the scene are evaluated as
   one GPU batch; under torch.distributed (world > 1) the scene's images are
   split over the ranks (LPT) and the rows gathered to rank 0 (RCCL), which
-  alone returns the errors (None elsewhere)."""
+  alone returns the errors (None elsewhere). planned: (errs, todo, depths)
+  prepared ahead by run() (single process), else computed here."""
   et = p["error_type"]
-  errs, todo = plan(p, recs, models_info)
+  errs, todo, depths = planned if planned is not None else plan(p, recs, models_info) + (None,)
   rank, world = _dist()
   if todo:
     batch_fn = batch_fn or evaluate_batch
     if world == 1:
+      kw = {"depths": depths} if depths is not None else {}
       rows = batch_fn(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
-                      models_info, symmetric_ids, todo)
+                      models_info, symmetric_ids, todo, **kw)
     else:
       from . import shard
       mine = shard_todo(recs, todo, world)[rank]
@@ -355,37 +370,58 @@ def run(p, device=0):
     targets_org, ests_org = organize(targets, ests)
     sym_ids = set(dp_model["symmetric_obj_ids"] or [])
     ests_counter = 0
-    for scene_id, scene_targets in targets_org.items():
+    single = _dist()[1] == 1
+
+    def prepare(scene_id, scene_targets):
+      # host side of one scene: annotations, records, gates and (VSD) the
+      # test-depth PNGs, decoded while the previous scene runs and is saved
       scene_camera = inout.load_scene_camera(
           dp_split["scene_camera_tpath"].format(scene_id=scene_id))
       scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
-      log("Calculating error {} - method: {}, dataset: {}{}, scene: {}".format(
-          et, method, dataset, split_type_str, scene_id))
       recs, n_ests = scene_records(p, scene_id, scene_targets, ests_org, scene_gt)
-      ests_counter += n_ests
-      errs = evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
-                      models_info, sym_ids) if recs else []
-      if errs is None or _dist()[0] != 0:  # rank 0 writes (also for a scene with no records)
-        continue
-      scene_errs = [{"im_id": r["im_id"], "obj_id": r["obj_id"], "est_id": r["est_id"],
-                     "score": r["score"], "errors": e} for r, e in zip(recs, errs)]
+      planned = None
+      if single and recs:
+        errs, todo = plan(p, recs, models_info)
+        depths = None
+        if et == "vsd" and todo:
+          depths = load_scene_depths(dp_split, scene_camera, scene_id, todo_images(recs, todo))
+        planned = (errs, todo, depths)
+      return scene_camera, recs, n_ests, planned
 
-      def save(sign, content):
-        path = p["out_errors_tpath"].format(eval_path=p["eval_path"], result_name=result_name,
-                                           error_sign=sign, scene_id=scene_id)
-        os.makedirs(os.path.dirname(path), exist_ok=True)
-        log("Saving errors to: {}".format(path))
-        inout.save_json(path, content)
-        written.append(path)
+    from concurrent.futures import ThreadPoolExecutor
+    scenes = list(targets_org.items())
+    with ThreadPoolExecutor(1) as ahead:
+      nxt = ahead.submit(prepare, *scenes[0]) if scenes else None
+      for k, (scene_id, scene_targets) in enumerate(scenes):
+        scene_camera, recs, n_ests, planned = nxt.result()
+        if k + 1 < len(scenes):
+          nxt = ahead.submit(prepare, *scenes[k + 1])
+        log("Calculating error {} - method: {}, dataset: {}{}, scene: {}".format(
+            et, method, dataset, split_type_str, scene_id))
+        ests_counter += n_ests
+        errs = evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
+                        models_info, sym_ids, planned=planned) if recs else []
+        if errs is None or _dist()[0] != 0:  # rank 0 writes (also for a scene with no records)
+          continue
+        scene_errs = [{"im_id": r["im_id"], "obj_id": r["obj_id"], "est_id": r["est_id"],
+                       "score": r["score"], "errors": e} for r, e in zip(recs, errs)]
 
-      if et == "vsd":
-        for k, tau in enumerate(p["vsd_taus"]):
-          sign = misc.get_error_signature(et, p["n_top"], vsd_delta=p["vsd_deltas"][dataset],
-                                          vsd_tau=tau)
-          save(sign, [dict(e, errors={g: [v[k]] for g, v in e["errors"].items()})
-                      for e in scene_errs])
-      else:
-        save(misc.get_error_signature(et, p["n_top"]), scene_errs)
+        def save(sign, content):
+          path = p["out_errors_tpath"].format(eval_path=p["eval_path"], result_name=result_name,
+                                             error_sign=sign, scene_id=scene_id)
+          os.makedirs(os.path.dirname(path), exist_ok=True)
+          log("Saving errors to: {}".format(path))
+          inout.save_json(path, content)
+          written.append(path)
+
+        if et == "vsd":
+          for ti, tau in enumerate(p["vsd_taus"]):
+            sign = misc.get_error_signature(et, p["n_top"], vsd_delta=p["vsd_deltas"][dataset],
+                                            vsd_tau=tau)
+            save(sign, [dict(e, errors={g: [v[ti]] for g, v in e["errors"].items()})
+                        for e in scene_errs])
+        else:
+          save(misc.get_error_signature(et, p["n_top"]), scene_errs)
     log("Calculation of errors for {} estimates took {}s.".format(
         ests_counter, time.time() - time_start))
   log("Done.")
