@@ -217,13 +217,25 @@ def todo_images(recs, todo):
   return sorted({recs[ri]["im_id"] for ri, _, _, _ in todo})
 
 
-def load_scene_depths(dp_split, scene_camera, scene_id, ims):
-  """Test depth of the images ims in mm, float32 (eval_calc_errors.py:240-243)."""
-  depths = inout.load_depths(dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id)
-                             for im_id in ims)
-  for k, im_id in enumerate(ims):
-    depths[k] *= scene_camera[im_id]["depth_scale"]  # float32 in place, :242-243
-  return depths
+def load_scene_depths(dp_split, scene_camera, scene_id, ims, torch=None):
+  """Test depth of the images ims in mm, float32 (eval_calc_errors.py:240-243),
+  decoded straight into one (n, H, W) array — page-locked when torch is given,
+  so the upload to the GPU is one DMA — or a list when the sizes differ."""
+  paths = [dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id) for im_id in ims]
+  scales = [scene_camera[im_id]["depth_scale"] for im_id in ims]  # float32 in place, :242-243
+  W, H = dp_split["im_size"]
+  if torch is not None and torch.cuda.is_available() and os.environ.get("BOPX_PIN", "1") != "0":
+    buf = torch.empty((len(ims), H, W), dtype=torch.float32, pin_memory=True)
+    try:
+      inout.load_depths(paths, scales=scales, out=buf.numpy())
+      return buf
+    except ValueError:
+      pass  # a frame of another size: per-frame arrays below
+  buf = np.empty((len(ims), H, W), np.float32)
+  try:
+    return inout.load_depths(paths, scales=scales, out=buf)
+  except ValueError:
+    return inout.load_depths(paths, scales=scales)
 
 
 def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, models_info,
@@ -250,11 +262,14 @@ def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs
       W, H = dp_split["im_size"]
       return ev.cover(slots, d_pe, d_pg, fidx, T(cam, torch.float64), W, H)
     if depths is None:
-      depths = load_scene_depths(dp_split, scene_camera, scene_id, ims)
+      depths = load_scene_depths(dp_split, scene_camera, scene_id, ims, torch)
+    if isinstance(depths, list):
+      depths = np.stack(depths)
+    d_frames = depths.to(dev, non_blocking=True) if torch.is_tensor(depths) else T(depths, torch.float32)
     dia = np.array([models_info[o]["diameter"] for o in obj], np.float64)
     delta = p["vsd_deltas"][dataset]
     from . import runtime
-    return ev.vsd(slots, d_pe, d_pg, fidx, T(np.stack(depths), torch.float32),
+    return ev.vsd(slots, d_pe, d_pg, fidx, d_frames,
                   T(cam, torch.float64), delta, p["vsd_taus"], T(dia, torch.float64),
                   normalized_by_diameter=p["vsd_normalized_by_diameter"], cost_type="step",
                   delta_flags=runtime.delta_flags(delta))
@@ -384,7 +399,8 @@ def run(p, device=0):
         errs, todo = plan(p, recs, models_info)
         depths = None
         if et == "vsd" and todo:
-          depths = load_scene_depths(dp_split, scene_camera, scene_id, todo_images(recs, todo))
+          depths = load_scene_depths(dp_split, scene_camera, scene_id, todo_images(recs, todo),
+                                     torch)
         planned = (errs, todo, depths)
       return scene_camera, recs, n_ests, planned
 

@@ -273,14 +273,31 @@ def load_bop_results(path, version="bop19"):
   return results
 
 
-def load_depths(paths, workers=None):
+def load_depths(paths, workers=None, scales=None, out=None):
   """load_depth of many files, decoded in a thread pool (Pillow's PNG/TIFF
-  decoders release the GIL), in input order."""
+  decoders release the GIL), in input order. scales: per-file factor applied
+  in float32 in place (`depth *= depth_scale`, eval_calc_errors.py:242-243).
+  out: an (n, H, W) float32 array the frames are written into (returned);
+  a frame of another size raises ValueError. Else a list of arrays."""
   from concurrent.futures import ThreadPoolExecutor
   paths = list(paths)
+
+  def one(k):
+    d = load_depth(paths[k])
+    if scales is not None:
+      d *= scales[k]
+    if out is None:
+      return d
+    if d.shape != out.shape[1:]:
+      raise ValueError("depth image %s is %s, expected %s" % (paths[k], d.shape, out.shape[1:]))
+    out[k] = d
+    return None
+
   if len(paths) <= 1:
-    return [load_depth(p) for p in paths]
-  import os
-  n = workers or min(16, os.cpu_count() or 1, len(paths))
-  with ThreadPoolExecutor(n) as pool:
-    return list(pool.map(load_depth, paths))
+    res = [one(k) for k in range(len(paths))]
+  else:
+    import os
+    n = workers or min(16, os.cpu_count() or 1, len(paths))
+    with ThreadPoolExecutor(n) as pool:
+      res = list(pool.map(one, range(len(paths))))
+  return out if out is not None else res
