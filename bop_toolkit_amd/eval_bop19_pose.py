@@ -100,12 +100,17 @@ def evaluate(p, device=0, calc_errors=True):
     dataset = str(result_name.split("_")[1].split("-")[0])
     ests = inout.load_bop_results(os.path.join(p["results_path"], result_filename))
     avg_time = average_time_per_image(ests)
-    jobs, owner = [], []
+    owner = []
+    # every (folder, threshold) setting is independent: an error type's folders
+    # are scored in a process pool while the next error type runs on the GPU
+    n_folders = sum(len(e["vsd_taus"]) if e["type"] == "vsd" else 1 for e in p["errors"])
+    scorer = ecs.FolderScorer(n_folders) if ece._dist()[0] == 0 else None
     for error in p["errors"]:
       if calc_errors:
         ece.run(ece.parse_args(errors_argv(p, error, result_filename)), device)
       if ece._dist()[0] != 0:  # scores are host bookkeeping on rank 0
         continue
+      jobs = []
       if error["type"] == "vsd":
         signs = [misc.get_error_signature("vsd", error["n_top"],
                                           vsd_delta=error["vsd_deltas"][dataset], vsd_tau=tau)
@@ -123,10 +128,10 @@ def evaluate(p, device=0, calc_errors=True):
             for th in error["correct_th"]]
         jobs.append((error_dir_path, sps))
         owner.append(error["type"])
+      scorer.submit(jobs)
     if ece._dist()[0] != 0:
       continue
-    # every (folder, threshold) setting is independent: folders in parallel
-    folder_scores = ecs.score_folders(jobs)
+    folder_scores = scorer.results()
     average_recalls = {}
     for error in p["errors"]:
       recalls = [s["recall"] for o, fs in zip(owner, folder_scores) if o == error["type"]

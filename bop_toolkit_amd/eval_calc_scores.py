@@ -174,6 +174,43 @@ def _score_job(job):
   return [score_error_dir(sp, error_dir_path, cache=cache, do_print=do_print)[0] for sp in sps]
 
 
+class FolderScorer:
+  """score_folders in stages: submit(jobs) queues a group of folders (scored
+  at once by the pool while the caller goes on, e.g. computes the next error
+  type's folders on the GPU), results() returns every group's scores in
+  submission order. The spawned pool starts with the first submit (not
+  earlier: its interpreters would compete with the caller's own host work)."""
+
+  def __init__(self, n_folders, workers=None, do_print=True):
+    if workers is None:
+      workers = int(os.environ.get("BOPX_SCORE_WORKERS", "0")) or \
+          min(n_folders, os.cpu_count() or 1, 16)
+    self.do_print = do_print
+    self.workers = workers if n_folders > 1 else 1
+    self.pool = None
+    self.pending = []
+
+  def submit(self, jobs):
+    args = [(path, sps, self.do_print) for path, sps in jobs]
+    if self.pool is None and self.workers > 1:
+      import multiprocessing as mp
+      self.pool = mp.get_context("spawn").Pool(self.workers)
+    if self.pool is None:
+      self.pending.append([_score_job(a) for a in args])
+    else:
+      self.pending.append(self.pool.map_async(_score_job, args, chunksize=1))
+
+  def results(self):
+    out = []
+    for r in self.pending:
+      out.extend(r if isinstance(r, list) else r.get())
+    if self.pool is not None:
+      self.pool.close()
+      self.pool.join()
+      self.pool = None
+    return out
+
+
 def score_folders(jobs, workers=None, do_print=True):
   """Scores of several errors folders, each at several settings: jobs is a
   list of (error_dir_path, [params per setting]); returns the scores dicts in
