@@ -494,6 +494,8 @@ void k_vsd(VsdArgs a) {
   // entry | far << 11 | rectangle in the tile at 2-px granularity (x0/2, x1/2,
   // y0/2, y1/2: 5 bits each from bit 12) for the occlusion test; RPT 4: 16-bit
   // entry indices, no occlusion test (the list would not fit the LDS budget).
+  // row-walk atomics (raster.h BOPX_WALK_MASKED): per instantiation by default
+  constexpr int kWalkMasked = BOPX_WALK_MASKED >= 0 ? BOPX_WALK_MASKED : (RPT == 1 ? 0 : 1);
   constexpr bool kStream = RPT == 0;
   constexpr int kR = kStream ? 4 : RPT;  // rectangles per thread and round
   constexpr bool kCull = RPT >= 1 && RPT <= 2;
@@ -1028,9 +1030,9 @@ void k_vsd(VsdArgs a) {
               }
               if (valid) {
                 const int fr =
-                    VSD_DIAG(16) ? r_walk_row_max<true>(rec, wb + p - (int)(rec.meta >> 19),
+                    VSD_DIAG(16) ? r_walk_row_max<true, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
                                                         s_dep[(rec.meta >> 18) & 1u])
-                                 : r_walk_row_max(rec, wb + p - (int)(rec.meta >> 19),
+                                 : r_walk_row_max<false, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
                                                   s_dep[(rec.meta >> 18) & 1u]);
                 if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
               }
@@ -1058,9 +1060,9 @@ void k_vsd(VsdArgs a) {
               const int p = p0 + lane;
               if (p < wn) {
                 const int fr =
-                    VSD_DIAG(16) ? r_walk_row_max<true>(rec, wb + p - (int)(rec.meta >> 19),
+                    VSD_DIAG(16) ? r_walk_row_max<true, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
                                                         s_dep[(rec.meta >> 18) & 1u])
-                                 : r_walk_row_max(rec, wb + p - (int)(rec.meta >> 19),
+                                 : r_walk_row_max<false, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
                                                   s_dep[(rec.meta >> 18) & 1u]);
                 if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
               }
@@ -1080,9 +1082,9 @@ void k_vsd(VsdArgs a) {
               if (valid) {
                 const RRow rec = s_rec[wave][owner];
                 const int fr =
-                    VSD_DIAG(16) ? r_walk_row_max<true>(rec, wb + p - (int)(rec.meta >> 19),
+                    VSD_DIAG(16) ? r_walk_row_max<true, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
                                                         s_dep[(rec.meta >> 18) & 1u])
-                                 : r_walk_row_max(rec, wb + p - (int)(rec.meta >> 19),
+                                 : r_walk_row_max<false, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
                                                   s_dep[(rec.meta >> 18) & 1u]);
                 if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
               }
@@ -1103,9 +1105,9 @@ void k_vsd(VsdArgs a) {
             for (int p = lane; p < wn; p += 64) {
               const RRow rec = s_rec[wave][s_own[wave][p]];
               const int fr =
-                  VSD_DIAG(16) ? r_walk_row_max<true>(rec, wb + p - (int)(rec.meta >> 19),
+                  VSD_DIAG(16) ? r_walk_row_max<true, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
                                                       s_dep[(rec.meta >> 18) & 1u])
-                               : r_walk_row_max(rec, wb + p - (int)(rec.meta >> 19),
+                               : r_walk_row_max<false, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
                                                 s_dep[(rec.meta >> 18) & 1u]);
               if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
             }

@@ -29,8 +29,15 @@
 
 namespace bopx {
 
+// Row-walk atomics (r_walk_row_max's MASKED): 0 = every column issues its
+// atomicMax (0, a no-op on the non-negative q bits, where the centre is
+// outside), 1 = only covered centres (exec-masked), 2 = skipped per column
+// when no lane covers it. -1 (default): k_vsd picks per instantiation. Round 2,
+// same box, 3 reps each: with 1-rect-per-thread objects (the bench shard) 0 is
+// 0.9 % faster than 1 (no exec-mask save/restore around each atomic); with the
+// 2-rect instantiation (T-LESS-like config) 1 is 1.2 % faster; 2 is 1.9 % slower.
 #ifndef BOPX_WALK_MASKED
-#define BOPX_WALK_MASKED 1
+#define BOPX_WALK_MASKED -1
 #endif
 #ifndef BOPX_RCP_BALLOT
 #define BOPX_RCP_BALLOT 1
@@ -379,7 +386,7 @@ __device__ __forceinline__ RRow r_fetch_row(const RRow& own, int owner) {
 // q <= 0 are dropped" without a compare. No exec-mask branches in the loop body.
 // dep: the pose's q tile (row pitch kTileStride). Returns the fragment count
 // (diagnostics).
-template <bool kNoAtomics = false>  // kNoAtomics: timing ablation only (diag builds)
+template <bool kNoAtomics = false, int MASKED = 1>  // kNoAtomics: timing ablation (diag builds)
 __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* dep) {
   // j < 64 and the tile row tr < 64 always; the masks (no-ops) tell the
   // compiler so, which keeps every multiply below on the full-rate 24-bit path.
@@ -415,23 +422,22 @@ __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* de
     const f32x2 q = __builtin_elementwise_fma(ga2, fdx, qrow2);
     const float q0 = q.x, q1 = q.y;
     frags += (m0 > 0) + ((i + 1 < w) & (m1 > 0));  // diagnostics (dead in the product build)
-#if BOPX_WALK_MASKED == 1
     if constexpr (kNoAtomics) {
       asm volatile("" ::"v"(m0 > 0 ? q0 : 0.0f), "v"(m1 > 0 ? q1 : 0.0f), "v"(d + i));
-    } else {
+    } else if constexpr (MASKED == 1) {
       // only covered centres touch LDS (fewer bank conflicts on the scattered rows)
       if (m0 > 0) atomicMax(d + i, __float_as_int(q0));
       if (m1 > 0) atomicMax(d + i + 1, __float_as_int(q1));
-    }
-#elif BOPX_WALK_MASKED == 2
-    // wave-uniform skip of a column with no covered centre, unmasked otherwise
-    if (__builtin_amdgcn_ballot_w64(m0 > 0) != 0) atomicMax(d + i, m0 > 0 ? __float_as_int(q0) : 0);
-    if (__builtin_amdgcn_ballot_w64(m1 > 0) != 0)
+    } else if constexpr (MASKED == 2) {
+      // wave-uniform skip of a column with no covered centre, unmasked otherwise
+      if (__builtin_amdgcn_ballot_w64(m0 > 0) != 0)
+        atomicMax(d + i, m0 > 0 ? __float_as_int(q0) : 0);
+      if (__builtin_amdgcn_ballot_w64(m1 > 0) != 0)
+        atomicMax(d + i + 1, m1 > 0 ? __float_as_int(q1) : 0);
+    } else {
+      atomicMax(d + i, m0 > 0 ? __float_as_int(q0) : 0);
       atomicMax(d + i + 1, m1 > 0 ? __float_as_int(q1) : 0);
-#else
-    atomicMax(d + i, m0 > 0 ? __float_as_int(q0) : 0);
-    atomicMax(d + i + 1, m1 > 0 ? __float_as_int(q1) : 0);
-#endif
+    }
     e[0] = f0 + sx[0];
     e[1] = f1 + sx[1];
     e[2] = f2 + sx[2];
