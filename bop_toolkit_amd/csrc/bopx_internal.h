@@ -120,8 +120,9 @@ struct OrderCost {  // VSD inputs of the cost classes (pe == nullptr: order by s
   const double* dia;
   const int32_t* slot_rank;  // pe == nullptr: key = slot_rank[slot] (slots by descending cost)
 };
+// keys: n int32 of scratch (the per-tuple sort keys)
 hipError_t launch_order_by_slot(const int32_t* slots, int64_t n, int ns, int32_t* order,
-                                hipStream_t s, const OrderCost* cost = nullptr);
+                                int32_t* keys, hipStream_t s, const OrderCost* cost = nullptr);
 hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s);  // or kCostCover
 hipError_t launch_cover_depths(int W, int H, const float* de, const float* dg,
                                long long* acc /* kCoverCols, device */, hipStream_t s);

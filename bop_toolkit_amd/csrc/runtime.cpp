@@ -149,9 +149,10 @@ int make_order(bopx_ctx* c, int64_t n, const int32_t* slots, hipStream_t s, Laun
   if (!on || n < kOrderMinTuples || n > INT32_MAX ||
       (int64_t)c->objs.size() > bopx::kOrderMaxSlots)
     return BOPX_OK;
-  HIPCHK(c, hipMallocAsync((void**)&o.p, (size_t)n * sizeof(int32_t), s));
+  // order (n) + sort-key scratch (n), one stream-ordered allocation
+  HIPCHK(c, hipMallocAsync((void**)&o.p, 2 * (size_t)n * sizeof(int32_t), s));
   o.s = s;
-  HIPCHK(c, bopx::launch_order_by_slot(slots, n, (int)c->objs.size(), o.p, s, cost));
+  HIPCHK(c, bopx::launch_order_by_slot(slots, n, (int)c->objs.size(), o.p, o.p + n, s, cost));
   return BOPX_OK;
 }
 
