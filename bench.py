@@ -325,9 +325,13 @@ def main():
   # (its tail, LDS-bound residency) instead of queueing behind it.
   side = torch.cuda.Stream(device=ev.device) if os.environ.get("BOPX_BENCH_OVERLAP") else None
 
+  # HIP events of every timed step, created before the timed region (event
+  # creation is a runtime call per event; only record() runs inside it)
+  pool = [{k: [torch.cuda.Event(enable_timing=True) for _ in range(2)] for k in ktime}
+          for _ in range(args.steps)]
+
   def step(timed):
-    e = {k: [torch.cuda.Event(enable_timing=True) for _ in range(2)] for k in ktime} \
-        if timed else None
+    e = pool[len(marks)] if timed else None
     run = {
         "vsd": lambda: ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"],
                               d["frames"], d["cam"], DELTA, TAUS, d["diameters"], out=out_vsd),
