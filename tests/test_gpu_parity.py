@@ -608,6 +608,42 @@ def test_huge_mesh_streamed_rects(oracle_mod):
   ctx.close()
 
 
+def test_gt_masks_huge_mesh_vs_oracle(oracle_mod):
+  """GT-info mode (calc_gt_masks canvas) on an object beyond the register-
+  resident limit (RPT 0): silhouette and visible-part masks and counts equal
+  the oracle raster + bop19 visibility on the same test depth."""
+  from bop_toolkit_amd import _lib
+  from bop_toolkit_amd._lib import _d, _f, _i32, _u8, ptr
+  n, W, H = 3, 640, 480
+  rng, pts, faces, Rg, tg, Re, te_, K = _scene(21, n, n_lat=220, n_lon=250)
+  fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+  ctx = _lib.Context(0)
+  ctx.add_object(4, pts, faces)
+  frames, dgs = [], []
+  for i in range(n):
+    dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, W, H)
+    dt = np.where(dg > 0, dg + rng.normal(0, 8.0, dg.shape), 1600.0).astype(np.float32)
+    dt[rng.random(dt.shape) < 0.1] = 0.0
+    frames.append(np.round(dt).astype(np.float32))
+    dgs.append(dg)
+  frames = np.stack(frames)
+  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
+  cam = np.tile([fx, fy, cx, cy], (n, 1)).astype(np.float64)
+  out = np.empty((n, 11))
+  masks = np.zeros((n, 2, H, W), np.uint8)
+  ctx.call("bopx_gt_info_batch", n, ptr(np.full(n, 4, np.int32), _i32), ptr(pg, _d),
+           ptr(np.arange(n, dtype=np.int32), _i32), ptr(frames, _f), n, W, H, ptr(cam, _d), 15.0,
+           0, 1, ptr(out, _d), ptr(masks, _u8))
+  for i in range(n):
+    d_t = oracle_mod.dist_im(frames[i], fx, fy, cx, cy)
+    d_g = oracle_mod.dist_im(dgs[i], fx, fy, cx, cy)
+    vis = oracle_mod.visib_mask(d_t, d_g, 15.0)
+    assert np.array_equal(masks[i, 0] > 0, dgs[i] > 0), i
+    assert np.array_equal(masks[i, 1] > 0, vis), i
+    assert out[i, 0] == (dgs[i] > 0).sum() and out[i, 1] == vis.sum(), i
+  ctx.close()
+
+
 def test_fused_vsd_bit_exact_large_images(oracle_mod):
   """ITODD-like 1280x960 (delta 5, dataset_params.py) and HOPE-like 1920x1080
   frames: many tiles per tuple, bit-exact."""
