@@ -87,6 +87,38 @@ def errors_argv(p, error, result_filename):
   return argv
 
 
+def _errors_and_scores(p, result_filename, result_name, dataset, device, calc_errors, scorer,
+                       owner):
+  """Error files of every error type (GPU), each type's folders handed to the
+  scorer as soon as they are written; the scores of every folder (rank 0),
+  None elsewhere. owner receives the error type of each folder."""
+  for error in p["errors"]:
+    if calc_errors:
+      ece.run(ece.parse_args(errors_argv(p, error, result_filename)), device)
+    if scorer is None:  # scores are host bookkeeping on rank 0
+      continue
+    jobs = []
+    if error["type"] == "vsd":
+      signs = [misc.get_error_signature("vsd", error["n_top"],
+                                        vsd_delta=error["vsd_deltas"][dataset], vsd_tau=tau)
+               for tau in error["vsd_taus"]]
+    else:
+      signs = [misc.get_error_signature(error["type"], error["n_top"])]
+    for sign in dict.fromkeys(signs):
+      error_dir_path = os.path.join(result_name, sign)
+      sps = [ecs.parse_args([
+          "--error_dir_paths={}".format(error_dir_path),
+          "--eval_path={}".format(p["eval_path"]),
+          "--targets_filename={}".format(p["targets_filename"]),
+          "--visib_gt_min={}".format(p["visib_gt_min"]),
+          "--correct_th_{}={}".format(error["type"], ",".join(map(str, th)))])
+          for th in error["correct_th"]]
+      jobs.append((error_dir_path, sps))
+      owner.append(error["type"])
+    scorer.submit(jobs)
+  return scorer.results() if scorer is not None else None
+
+
 def evaluate(p, device=0, calc_errors=True):
   """Evaluate every result file; returns {result_name: final_scores}.
   calc_errors=False scores errors_*.json already present under eval_path."""
@@ -105,33 +137,14 @@ def evaluate(p, device=0, calc_errors=True):
     # are scored in a process pool while the next error type runs on the GPU
     n_folders = sum(len(e["vsd_taus"]) if e["type"] == "vsd" else 1 for e in p["errors"])
     scorer = ecs.FolderScorer(n_folders) if ece._dist()[0] == 0 else None
-    for error in p["errors"]:
-      if calc_errors:
-        ece.run(ece.parse_args(errors_argv(p, error, result_filename)), device)
-      if ece._dist()[0] != 0:  # scores are host bookkeeping on rank 0
-        continue
-      jobs = []
-      if error["type"] == "vsd":
-        signs = [misc.get_error_signature("vsd", error["n_top"],
-                                          vsd_delta=error["vsd_deltas"][dataset], vsd_tau=tau)
-                 for tau in error["vsd_taus"]]
-      else:
-        signs = [misc.get_error_signature(error["type"], error["n_top"])]
-      for sign in dict.fromkeys(signs):
-        error_dir_path = os.path.join(result_name, sign)
-        sps = [ecs.parse_args([
-            "--error_dir_paths={}".format(error_dir_path),
-            "--eval_path={}".format(p["eval_path"]),
-            "--targets_filename={}".format(p["targets_filename"]),
-            "--visib_gt_min={}".format(p["visib_gt_min"]),
-            "--correct_th_{}={}".format(error["type"], ",".join(map(str, th)))])
-            for th in error["correct_th"]]
-        jobs.append((error_dir_path, sps))
-        owner.append(error["type"])
-      scorer.submit(jobs)
+    try:
+      folder_scores = _errors_and_scores(p, result_filename, result_name, dataset, device,
+                                         calc_errors, scorer, owner)
+    finally:
+      if scorer is not None:
+        scorer.close()
     if ece._dist()[0] != 0:
       continue
-    folder_scores = scorer.results()
     average_recalls = {}
     for error in p["errors"]:
       recalls = [s["recall"] for o, fs in zip(owner, folder_scores) if o == error["type"]

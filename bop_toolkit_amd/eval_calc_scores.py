@@ -201,14 +201,20 @@ class FolderScorer:
       self.pending.append(self.pool.map_async(_score_job, args, chunksize=1))
 
   def results(self):
-    out = []
-    for r in self.pending:
-      out.extend(r if isinstance(r, list) else r.get())
+    try:
+      out = []
+      for r in self.pending:
+        out.extend(r if isinstance(r, list) else r.get())
+      return out
+    finally:
+      self.close()
+
+  def close(self):
+    """Stops the pool (after results(), or on an error: terminates it)."""
     if self.pool is not None:
-      self.pool.close()
+      self.pool.terminate()
       self.pool.join()
       self.pool = None
-    return out
 
 
 def score_folders(jobs, workers=None, do_print=True):
