@@ -130,7 +130,8 @@ def evaluate(p, device=0, calc_errors=True):
     t0 = time.time()
     result_name = os.path.splitext(os.path.basename(result_filename))[0]
     dataset = str(result_name.split("_")[1].split("-")[0])
-    ests = inout.load_bop_results(os.path.join(p["results_path"], result_filename))
+    ests = ece.cached_load(inout.load_bop_results,
+                           os.path.join(p["results_path"], result_filename))
     avg_time = average_time_per_image(ests)
     owner = []
     # every (folder, threshold) setting is independent: an error type's folders

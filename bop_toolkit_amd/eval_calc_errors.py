@@ -97,6 +97,26 @@ def log(s):
   misc.log(s)
 
 
+# Parsed annotation / model / result files, shared by the error types of one
+# process (eval_bop19_pose runs VSD, MSSD and MSPD over the same files): keyed
+# by path, size and mtime, so an edited file is read again. Callers treat the
+# returned objects as read-only.
+_FILE_CACHE = {}
+_FILE_CACHE_MAX = 512
+
+
+def cached_load(loader, path, **kw):
+  st = os.stat(path)
+  key = (loader.__name__, os.path.abspath(path), st.st_size, st.st_mtime_ns,
+         tuple(sorted(kw.items())))
+  hit = _FILE_CACHE.get(key)
+  if hit is None:
+    if len(_FILE_CACHE) >= _FILE_CACHE_MAX:
+      _FILE_CACHE.pop(next(iter(_FILE_CACHE)))
+    hit = _FILE_CACHE[key] = loader(path, **kw)
+  return hit
+
+
 # ----------------------------------------------------------------- enumeration
 def organize(targets, ests):
   """targets_org[scene][im][obj] = target; ests_org[scene][im][obj] = [est]
@@ -163,7 +183,7 @@ class Models:
       path = dp_model["model_tpath"].format(obj_id=obj_id)
       if not os.path.exists(path):
         continue
-      m = inout.load_ply(path)
+      m = cached_load(inout.load_ply, path)
       syms = None
       if need_syms:
         syms = misc.get_symmetry_transformations(models_info[obj_id], p["max_sym_disc_step"])
@@ -370,7 +390,7 @@ def run(p, device=0):
     et = p["error_type"]
     models_info = None
     if et in ("ad", "add", "adi", "vsd", "mssd", "mspd", "cus"):
-      models_info = inout.load_json(dp_model["models_info_path"], keys_to_int=True)
+      models_info = cached_load(inout.load_json, dp_model["models_info_path"], keys_to_int=True)
     if et not in ("re", "te", "rete"):
       if ev is None:
         ev = BatchEvaluator(device)
@@ -379,9 +399,9 @@ def run(p, device=0):
       ev.objects.clear()
       log("Loading object models...")
       Models(ev, p, dp_model, models_info)
-    targets = inout.load_json(os.path.join(dp_split["base_path"], p["targets_filename"]))
+    targets = cached_load(inout.load_json, os.path.join(dp_split["base_path"], p["targets_filename"]))
     log("Loading pose estimates...")
-    ests = inout.load_bop_results(os.path.join(p["results_path"], result_filename))
+    ests = cached_load(inout.load_bop_results, os.path.join(p["results_path"], result_filename))
     targets_org, ests_org = organize(targets, ests)
     sym_ids = set(dp_model["symmetric_obj_ids"] or [])
     ests_counter = 0
@@ -390,9 +410,10 @@ def run(p, device=0):
     def prepare(scene_id, scene_targets):
       # host side of one scene: annotations, records, gates and (VSD) the
       # test-depth PNGs, decoded while the previous scene runs and is saved
-      scene_camera = inout.load_scene_camera(
-          dp_split["scene_camera_tpath"].format(scene_id=scene_id))
-      scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+      scene_camera = cached_load(inout.load_scene_camera,
+                                 dp_split["scene_camera_tpath"].format(scene_id=scene_id))
+      scene_gt = cached_load(inout.load_scene_gt,
+                             dp_split["scene_gt_tpath"].format(scene_id=scene_id))
       recs, n_ests = scene_records(p, scene_id, scene_targets, ests_org, scene_gt)
       planned = None
       if single and recs:
