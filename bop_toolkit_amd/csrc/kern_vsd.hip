@@ -377,6 +377,15 @@ constexpr int kPixPerWave = (kTileH + kVsdWaves - 1) / kVsdWaves * kTileW;
 #ifndef BOPX_WORD_PAIR
 #define BOPX_WORD_PAIR 1
 #endif
+// Walk record read as three 16-B LDS reads (ds_read_b128) instead of the
+// compiler's b96 + 3 x read2_b32 split: -2.0 % (same box, 3 reps, round 2).
+#ifndef BOPX_REC128
+#define BOPX_REC128 1
+#endif
+// Record write as three 16-B LDS writes (experiment).
+#ifndef BOPX_REC128W
+#define BOPX_REC128W 0
+#endif
 // Row-item -> record lookup: start flags + ballot/mbcnt (one flag write per
 // record) instead of an owner byte per row item.
 #ifndef BOPX_WALK_FLAGS
@@ -990,9 +999,24 @@ void k_vsd(VsdArgs a) {
           // records compacted by rank among the row-owning lanes (ascending first)
           const uint64_t rbal = __builtin_amdgcn_ballot_w64(rows);
           if (rows)
+#if BOPX_REC128W
+          {
+            RRow rr;
+            r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first, rr);
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4* src = reinterpret_cast<const u32x4*>(&rr);
+            u32x4* dst = reinterpret_cast<u32x4*>(&s_rec[wave][__builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(rbal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rbal, 0u))]);
+            const u32x4 w0 = src[0], w1 = src[1], w2 = src[2];
+            dst[0] = w0;
+            dst[1] = w1;
+            dst[2] = w2;
+          }
+#else
             r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first,
                        s_rec[wave][__builtin_amdgcn_mbcnt_hi(
                            (uint32_t)(rbal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rbal, 0u))]);
+#endif
 #else
           if (rows) r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first, s_rec[wave][lane]);
 #endif
@@ -1080,7 +1104,21 @@ void k_vsd(VsdArgs a) {
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
               rec_base += __popcll(M);
               if (valid) {
+#if BOPX_REC128
+                // the 48-B record as three 16-B LDS reads
+                RRow rec;
+                {
+                  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                  const u32x4* src = reinterpret_cast<const u32x4*>(&s_rec[wave][owner]);
+                  u32x4* dst = reinterpret_cast<u32x4*>(&rec);
+                  const u32x4 r0 = src[0], r1 = src[1], r2 = src[2];
+                  dst[0] = r0;
+                  dst[1] = r1;
+                  dst[2] = r2;
+                }
+#else
                 const RRow rec = s_rec[wave][owner];
+#endif
                 const int fr =
                     VSD_DIAG(16) ? r_walk_row_max<true, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
                                                         s_dep[(rec.meta >> 18) & 1u])
