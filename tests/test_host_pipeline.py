@@ -1,0 +1,73 @@
+"""Host plumbing of the caller scripts (no GPU): the batched depth loader, the
+per-process file cache shared by the error-type passes, the staged folder
+scorer and the tau chunking of the VSD entry points."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+from bop_toolkit_amd import eval_calc_errors as ece
+from bop_toolkit_amd import eval_calc_scores as ecs
+from bop_toolkit_amd import inout, pose_error
+
+
+def _png(path, a):
+  from PIL import Image
+  Image.fromarray(a.astype(np.uint16)).save(path)
+
+
+def test_load_depths_scales_and_out(tmp_path):
+  """Scaled in float32 in place (eval_calc_errors.py:242-243) and written into a
+  caller array; a frame of another size raises instead of being written."""
+  rng = np.random.default_rng(3)
+  frames = [rng.integers(0, 60000, (6, 8)) for _ in range(5)]
+  paths = []
+  for k, f in enumerate(frames):
+    paths.append(str(tmp_path / ("%d.png" % k)))
+    _png(paths[-1], f)
+  scales = [0.1, 1.0, 0.25, 0.1, 2.0]
+  ref = []
+  for f, sc in zip(frames, scales):
+    d = f.astype(np.float32)
+    d *= sc
+    ref.append(d)
+  got = inout.load_depths(paths, scales=scales)
+  assert all(np.array_equal(a, b) and a.dtype == np.float32 for a, b in zip(got, ref))
+  out = np.full((5, 6, 8), -1.0, np.float32)
+  assert inout.load_depths(paths, scales=scales, out=out) is out
+  assert np.array_equal(out, np.stack(ref))
+  with pytest.raises(ValueError):
+    inout.load_depths(paths, out=np.empty((5, 6, 9), np.float32))
+
+
+def test_cached_load_rereads_changed_files(tmp_path):
+  path = tmp_path / "a.json"
+  path.write_text('{"1": [1, 2]}')
+  a = ece.cached_load(inout.load_json, str(path), keys_to_int=True)
+  assert a == {1: [1, 2]}
+  assert ece.cached_load(inout.load_json, str(path), keys_to_int=True) is a  # cached
+  assert ece.cached_load(inout.load_json, str(path)) == {"1": [1, 2]}  # other kwargs
+  time.sleep(0.01)
+  path.write_text('{"1": [3]}')
+  os.utime(path, ns=(time.time_ns(), time.time_ns() + 10 ** 7))
+  assert ece.cached_load(inout.load_json, str(path), keys_to_int=True) == {1: [3]}
+
+
+def test_folder_scorer_in_order_without_pool(monkeypatch):
+  """One worker: groups scored at submit time, results in submission order;
+  close() is idempotent."""
+  monkeypatch.setattr(ecs, "_score_job", lambda job: [job[0] + ":" + s for s in job[1]])
+  fs = ecs.FolderScorer(3, workers=1)
+  fs.submit([("a", ["1", "2"])])
+  fs.submit([("b", ["1"]), ("c", [])])
+  assert fs.results() == [["a:1", "a:2"], ["b:1"], []]
+  fs.close()
+
+
+def test_tau_chunks():
+  assert pose_error._tau_chunks(0) == []
+  assert pose_error._tau_chunks(10) == [(0, 10)]
+  assert pose_error._tau_chunks(16) == [(0, 16)]
+  assert pose_error._tau_chunks(25) == [(0, 16), (16, 25)]
+  assert pose_error._tau_chunks(33) == [(0, 16), (16, 32), (32, 33)]
