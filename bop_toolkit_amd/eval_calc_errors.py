@@ -452,11 +452,18 @@ def run(p, device=0):
           written.append(path)
 
         if et == "vsd":
-          for ti, tau in enumerate(p["vsd_taus"]):
+          # one file per tau (:401-415), all written from one encoding per record
+          paths = []
+          for tau in p["vsd_taus"]:
             sign = misc.get_error_signature(et, p["n_top"], vsd_delta=p["vsd_deltas"][dataset],
                                             vsd_tau=tau)
-            save(sign, [dict(e, errors={g: [v[ti]] for g, v in e["errors"].items()})
-                        for e in scene_errs])
+            paths.append(p["out_errors_tpath"].format(eval_path=p["eval_path"],
+                                                      result_name=result_name, error_sign=sign,
+                                                      scene_id=scene_id))
+            os.makedirs(os.path.dirname(paths[-1]), exist_ok=True)
+            log("Saving errors to: {}".format(paths[-1]))
+          inout.save_json_per_value(paths, scene_errs, len(paths))
+          written.extend(paths)
         else:
           save(misc.get_error_signature(et, p["n_top"]), scene_errs)
     log("Calculation of errors for {} estimates took {}s.".format(

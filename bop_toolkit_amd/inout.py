@@ -196,6 +196,44 @@ def save_json(path, content):
       json.dump(content, f, sort_keys=True)
 
 
+def _json_float(v):
+  """json.dumps of one float (float.__repr__, NaN / Infinity spelled as json does)."""
+  if v != v:
+    return "NaN"
+  if v in (float("inf"), float("-inf")):
+    return "Infinity" if v > 0 else "-Infinity"
+  return float.__repr__(v)
+
+
+def save_json_per_value(paths, records, n_values):
+  """save_json(paths[k], [dict(r, errors={g: [r["errors"][g][k]]})  for r in
+  records]) for every k < n_values, byte for byte, without building the
+  n_values x len(records) dicts: each record's line is encoded once around its
+  error values (the VSD per-tau files, eval_calc_errors.py:401-415). Records:
+  {'errors': {int gt_id: [n_values floats]}, 'est_id', 'im_id', 'obj_id',
+  'score'} — exactly these keys, as the caller builds them."""
+  parts = []  # per record: (text before each value ..., text after the last)
+  for r in records:
+    if set(r) != {"errors", "est_id", "im_id", "obj_id", "score"}:
+      raise ValueError("unexpected record keys %s" % sorted(r))
+    gids = sorted(r["errors"])  # json sort_keys orders the int keys numerically
+    pre = []
+    for j, g in enumerate(gids):
+      pre.append(('{"errors": {' if j == 0 else "], ") + _dumps(str(g)) + ": [")
+    tail = ("]" if gids else "") + '}, "est_id": ' + _dumps(r["est_id"]) + ', "im_id": ' + \
+        _dumps(r["im_id"]) + ', "obj_id": ' + _dumps(r["obj_id"]) + ', "score": ' + \
+        _dumps(r["score"]) + "}"
+    if not gids:
+      pre, tail = [], '{"errors": {' + tail
+    parts.append((pre, [r["errors"][g] for g in gids], tail))
+  for k in range(n_values):
+    lines = []
+    for pre, vals, tail in parts:
+      lines.append("  " + "".join(p_ + _json_float(float(v[k])) for p_, v in zip(pre, vals)) + tail)
+    with open(paths[k], "w") as f:
+      f.write("[\n" + ",\n".join(lines) + ("\n]" if lines else "]"))
+
+
 def load_json(path, keys_to_int=False):
   """JSON file; with keys_to_int, object keys that are (signed) integers
   become ints (inout.py:66-82)."""

@@ -71,3 +71,28 @@ def test_tau_chunks():
   assert pose_error._tau_chunks(16) == [(0, 16)]
   assert pose_error._tau_chunks(25) == [(0, 16), (16, 25)]
   assert pose_error._tau_chunks(33) == [(0, 16), (16, 32), (32, 33)]
+
+
+def test_save_json_per_value_bytes(tmp_path):
+  """The per-tau VSD files written from one encoding per record are the bytes
+  save_json writes for the per-tau record lists (several GTs with int keys
+  ordered numerically, none, inf, int scores)."""
+  import random
+  rnd = random.Random(1)
+  recs = []
+  for _ in range(200):
+    gids = rnd.sample(range(15), rnd.choice([0, 1, 1, 2, 3, 11]))
+    recs.append({"errors": {g: [rnd.choice([rnd.random(), 1.0, 0.0, float("inf"), 1 / 3, 1e-20])
+                                for _ in range(4)] for g in gids},
+                 "est_id": rnd.randint(0, 5), "im_id": rnd.randint(0, 3000),
+                 "obj_id": rnd.randint(1, 30), "score": rnd.choice([rnd.random(), 1, -2.0])})
+  paths = [str(tmp_path / ("f%d.json" % k)) for k in range(4)]
+  inout.save_json_per_value(paths, recs, 4)
+  for k in range(4):
+    ref = str(tmp_path / ("r%d.json" % k))
+    inout.save_json(ref, [dict(e, errors={g: [v[k]] for g, v in e["errors"].items()})
+                          for e in recs])
+    assert open(ref).read() == open(paths[k]).read(), k
+  inout.save_json_per_value([str(tmp_path / "e.json")], [], 1)
+  inout.save_json(str(tmp_path / "re.json"), [])
+  assert open(tmp_path / "e.json").read() == open(tmp_path / "re.json").read()
