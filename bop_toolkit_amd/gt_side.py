@@ -65,31 +65,53 @@ def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_ba
   im_ids = my_images(scene_gt, rank, world)
   res = {}
   dev = ev.device
-  for i0 in range(0, len(im_ids), im_batch):
-    ims = im_ids[i0:i0 + im_batch]
-    frames = inout.load_depths(_depth_path(dp_split, scene_id, im_id) for im_id in ims)
-    cam, obj, pose, fidx, owner = [], [], [], [], []
-    for k, im_id in enumerate(ims):
-      frames[k] *= scene_camera[im_id]["depth_scale"]  # float32 in place, calc_gt_info.py:99-100
-      K = scene_camera[im_id]["cam_K"]
-      cam.append((K[0, 0], K[1, 1], K[0, 2], K[1, 2]))
-      for gt in scene_gt[im_id]:
-        obj.append(gt["obj_id"])
-        pose.append(np.concatenate([gt["cam_R_m2c"].reshape(9), gt["cam_t_m2c"].reshape(3)]))
-        fidx.append(k)
-        owner.append(im_id)
-      res[im_id] = []
-    if not obj:
-      continue
-    T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
-    rows, mk = ev.gt_info(ev.slots(obj), T(np.stack(pose), torch.float64),
-                          T(np.array(fidx, np.int32), torch.int32),
-                          T(np.stack(frames), torch.float32), T(np.array(cam), torch.float64),
-                          delta, canvas_scale, masks, runtime.delta_flags(delta))
-    rows = rows.cpu().numpy()
-    mk = mk.cpu().numpy() if mk is not None else None
-    for j, im_id in enumerate(owner):
-      res[im_id].append((rows[j], None if mk is None else mk[j]))
+  W, H = dp_split["im_size"]
+
+  def load(ims):
+    # test depth in mm (float32 in place, calc_gt_info.py:99-100), decoded into
+    # one page-locked buffer while the previous batch runs
+    paths = [_depth_path(dp_split, scene_id, im_id) for im_id in ims]
+    scales = [scene_camera[im_id]["depth_scale"] for im_id in ims]
+    if torch.cuda.is_available():
+      buf = torch.empty((len(ims), H, W), dtype=torch.float32, pin_memory=True)
+      try:
+        inout.load_depths(paths, scales=scales, out=buf.numpy())
+        return buf
+      except ValueError:
+        pass  # a frame of another size
+    return np.stack(inout.load_depths(paths, scales=scales))
+
+  from concurrent.futures import ThreadPoolExecutor
+  batches = [im_ids[i0:i0 + im_batch] for i0 in range(0, len(im_ids), im_batch)]
+  with ThreadPoolExecutor(1) as ahead:
+    nxt = ahead.submit(load, batches[0]) if batches else None
+    for bi, ims in enumerate(batches):
+      frames = nxt.result()
+      if bi + 1 < len(batches):
+        nxt = ahead.submit(load, batches[bi + 1])
+      cam, obj, pose, fidx, owner = [], [], [], [], []
+      for k, im_id in enumerate(ims):
+        K = scene_camera[im_id]["cam_K"]
+        cam.append((K[0, 0], K[1, 1], K[0, 2], K[1, 2]))
+        for gt in scene_gt[im_id]:
+          obj.append(gt["obj_id"])
+          pose.append(np.concatenate([gt["cam_R_m2c"].reshape(9), gt["cam_t_m2c"].reshape(3)]))
+          fidx.append(k)
+          owner.append(im_id)
+        res[im_id] = []
+      if not obj:
+        continue
+      T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+      d_frames = (frames.to(dev, non_blocking=True) if torch.is_tensor(frames)
+                  else T(frames, torch.float32))
+      rows, mk = ev.gt_info(ev.slots(obj), T(np.stack(pose), torch.float64),
+                            T(np.array(fidx, np.int32), torch.int32), d_frames,
+                            T(np.array(cam), torch.float64), delta, canvas_scale, masks,
+                            runtime.delta_flags(delta))
+      rows = rows.cpu().numpy()
+      mk = mk.cpu().numpy() if mk is not None else None
+      for j, im_id in enumerate(owner):
+        res[im_id].append((rows[j], None if mk is None else mk[j]))
   return res
 
 
