@@ -245,10 +245,55 @@ def load_json(path, keys_to_int=False):
 
 def load_depth(path):
   """16-bit depth image (PNG, or TIFF for ITODD) as float32 (inout.py:39-46;
-  the reference reads it with imageio, here with Pillow)."""
+  the reference reads it with imageio). 16-bit grayscale PNGs go through the
+  native decoder (libbopx_io.so), other files through Pillow."""
+  return load_depths([path])[0]
+
+
+def _load_depth_pillow(path):
   from PIL import Image
   with Image.open(path) as im:
     return np.asarray(im).astype(np.float32)
+
+
+_IO_LIB = None
+_PNG_SIG = b"\x89PNG\r\n\x1a\n"
+
+
+def _io_lib():
+  """ctypes handle of bop_toolkit_amd/lib/libbopx_io.so (include/bopx_io.h)."""
+  global _IO_LIB
+  if _IO_LIB is None:
+    import ctypes
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libbopx_io.so")
+    if not os.path.exists(path):
+      raise RuntimeError("%s is missing: build it with `make -C bop_toolkit_amd/csrc` "
+                         "(or __graft_entry__.build())" % path)
+    lib = ctypes.CDLL(path)
+    lib.bopx_load_depth_pngs.argtypes = [
+        ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_float),
+        ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    lib.bopx_load_depth_pngs.restype = ctypes.c_int
+    lib.bopx_io_backend.restype = ctypes.c_int
+    _IO_LIB = lib
+  return _IO_LIB
+
+
+def _png16_shape(path):
+  """(h, w) when `path` is a 16-bit grayscale non-interlaced PNG (the layout
+  the native decoder handles), else None."""
+  try:
+    with open(path, "rb") as f:
+      hd = f.read(29)
+  except OSError:
+    return None
+  if len(hd) < 29 or hd[:8] != _PNG_SIG or hd[12:16] != b"IHDR":
+    return None
+  if hd[24] != 16 or hd[25] != 0 or hd[28] != 0:
+    return None
+  return int.from_bytes(hd[20:24], "big"), int.from_bytes(hd[16:20], "big")
 
 
 def load_cam_params(path):
@@ -312,30 +357,74 @@ def load_bop_results(path, version="bop19"):
 
 
 def load_depths(paths, workers=None, scales=None, out=None):
-  """load_depth of many files, decoded in a thread pool (Pillow's PNG/TIFF
-  decoders release the GIL), in input order. scales: per-file factor applied
-  in float32 in place (`depth *= depth_scale`, eval_calc_errors.py:242-243).
-  out: an (n, H, W) float32 array the frames are written into (returned);
-  a frame of another size raises ValueError. Else a list of arrays."""
+  """load_depth of many files, in input order. scales: per-file depth_scale,
+  applied as one float32 multiply (`depth *= depth_scale` with the JSON float,
+  eval_calc_errors.py:242-243). out: an (n, H, W) float32 array the frames are
+  written into (returned); a frame of another size raises ValueError. Else a
+  list of arrays.
+
+  16-bit grayscale PNGs (every BOP depth map) are read and decoded by one call
+  into libbopx_io.so on `workers` native threads, straight into `out`; other
+  files (ITODD's TIFF, 8-bit or interlaced PNGs) and files the native decoder
+  rejects go through Pillow in a thread pool, which also raises Pillow's own
+  errors for corrupt files."""
+  import ctypes
+  import os
   from concurrent.futures import ThreadPoolExecutor
-  paths = list(paths)
+  paths = [os.fspath(p) for p in paths]
+  n = len(paths)
+  sc = None if scales is None else [float(s) for s in scales]
+  if out is not None and len(out) < n:
+    raise ValueError("out holds %d frames, %d paths given" % (len(out), n))
+  direct = (out is not None and out.dtype == np.float32 and out.ndim == 3
+            and out.flags["C_CONTIGUOUS"])
+  res = [None] * n
+  shapes = [_png16_shape(p) for p in paths]
+  native = [k for k in range(n) if shapes[k] is not None]
+  for k in native:
+    if out is not None and shapes[k] != tuple(out.shape[1:]):
+      raise ValueError("depth image %s is %s, expected %s" % (paths[k], shapes[k],
+                                                              tuple(out.shape[1:])))
+  nw = workers or min(16, os.cpu_count() or 1, max(n, 1))
+  pil = [k for k in range(n) if shapes[k] is None]
+  if native:
+    m = len(native)
+    dst = (ctypes.c_void_p * m)()
+    for i, k in enumerate(native):
+      if direct:
+        dst[i] = out.ctypes.data + k * out.strides[0]
+      else:
+        res[k] = np.empty(shapes[k], np.float32)
+        dst[i] = res[k].ctypes.data
+    status = (ctypes.c_int * m)()
+    _io_lib().bopx_load_depth_pngs(
+        (ctypes.c_char_p * m)(*[os.fsencode(paths[k]) for k in native]), m,
+        (ctypes.c_int * m)(*[shapes[k][0] for k in native]),
+        (ctypes.c_int * m)(*[shapes[k][1] for k in native]),
+        None if sc is None else (ctypes.c_float * m)(*[sc[k] for k in native]),
+        dst, nw, status)
+    for i, k in enumerate(native):
+      if status[i] != 0:
+        pil.append(k)  # Pillow decodes it or raises its own error
+      elif out is not None and not direct:
+        out[k] = res[k]
+    pil.sort()
 
   def one(k):
-    d = load_depth(paths[k])
-    if scales is not None:
-      d *= scales[k]
+    d = _load_depth_pillow(paths[k])
+    if sc is not None:
+      d *= np.float32(sc[k])
     if out is None:
-      return d
+      res[k] = d
+      return
     if d.shape != out.shape[1:]:
       raise ValueError("depth image %s is %s, expected %s" % (paths[k], d.shape, out.shape[1:]))
     out[k] = d
-    return None
 
-  if len(paths) <= 1:
-    res = [one(k) for k in range(len(paths))]
+  if len(pil) <= 1:
+    for k in pil:
+      one(k)
   else:
-    import os
-    n = workers or min(16, os.cpu_count() or 1, len(paths))
-    with ThreadPoolExecutor(n) as pool:
-      res = list(pool.map(one, range(len(paths))))
+    with ThreadPoolExecutor(min(nw, len(pil))) as pool:
+      list(pool.map(one, pil))
   return out if out is not None else res

@@ -49,3 +49,17 @@ def test_no_gpu_fails_loudly():
     pytest.skip("GPU present")
   with pytest.raises(_lib.BopxError):
     _lib.Context(0)
+
+
+IO_HEADER = os.path.join(REPO, "include", "bopx_io.h")
+IO_LIB = os.path.join(REPO, "bop_toolkit_amd", "lib", "libbopx_io.so")
+
+
+def test_io_library_exports_every_declared_symbol():
+  """libbopx_io.so (host depth decoder) exports what include/bopx_io.h declares."""
+  src = re.sub(r"/\*.*?\*/", "", open(IO_HEADER).read(), flags=re.S)
+  syms = sorted(set(re.findall(r"\b(bopx_[a-z0-9_]+)\s*\(", src)))
+  assert syms == ["bopx_decode_depth_png", "bopx_io_backend", "bopx_load_depth_pngs"]
+  assert os.path.exists(IO_LIB), "libbopx_io.so not built (make -C bop_toolkit_amd/csrc)"
+  L = ctypes.CDLL(IO_LIB)
+  assert not [s for s in syms if not hasattr(L, s)]
