@@ -107,8 +107,9 @@ hipError_t launch_sym_error(int mode, const ObjDesc* objs, int max_ns, int64_t n
 hipError_t launch_mean_error(int mode, const ObjDesc* objs, int64_t n, const int32_t* slots,
                              const double* pe, const double* pg, const double* K, double* out,
                              const int32_t* order, hipStream_t s);  // mode 0 = ADD, 1 = PROJ
-hipError_t launch_adi(const ObjDesc* objs, int64_t n, const int32_t* slots, const double* pe,
-                      const double* pg, double* out, const int32_t* order, hipStream_t s);
+hipError_t launch_adi(const ObjDesc* objs, int max_nv, int64_t n, const int32_t* slots,
+                      const double* pe, const double* pg, double* out, const int32_t* order,
+                      hipStream_t s);
 // order: nullptr (block k takes tuple k) or a launch order from launch_order_by_slot
 constexpr int kOrderMaxSlots = 16383;  // LDS buckets of k_order_by_slot
 constexpr int kOrderCostClasses = 48;  // half-octave classes of the projected area (VSD order)

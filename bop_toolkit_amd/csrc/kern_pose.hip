@@ -15,6 +15,7 @@
 // squared distances (sqrt is monotone, so one sqrt per tuple), reduced through
 // LDS; min over symmetries likewise. Reductions run in a fixed order:
 // results are deterministic.
+#include <algorithm>
 #include <cstdlib>
 
 #include "bopx_internal.h"
@@ -547,21 +548,63 @@ __global__ __launch_bounds__(kPoseThreads) void k_mean_error(const ObjDesc* __re
 // holds kAdiQ GT-pose query vertices in registers and sweeps the tile
 // (broadcast LDS reads). cKDTree returns the exact NN distance, so the result
 // matches up to the float64 rounding of the transforms.
+//
+// Small batches (fewer tuples than the chip has workgroup slots) split each
+// tuple's estimate cloud into point ranges, one workgroup per (tuple, range):
+// every range's per-query minimum squared distance is merged with a 64-bit
+// atomicMin on the non-negative double bits (exact, order-independent), and
+// k_adi_finish forms the mean. Both paths sum the NN distances in the same
+// fixed structure (adi_chunk_sum per 1,024-query chunk, chunks in order), so
+// a tuple's ADI is the same double whatever the split.
 constexpr int kAdiTile = 512;
 constexpr int kAdiQ = 4;
+constexpr int kAdiChunk = kPoseThreads * kAdiQ;  // queries per sweep
 
+// Sum of one chunk's NN distances: per thread its kAdiQ queries in order, the
+// wave's lanes by the xor butterfly, the waves in order. Same value in every
+// thread. s_part: kPoseThreads / 64 doubles.
+__device__ __forceinline__ double adi_chunk_sum(const double (&best)[kAdiQ], int q0, int nv,
+                                                double* s_part) {
+  const int tid = threadIdx.x;
+  double v = 0.0;
+#pragma unroll
+  for (int q = 0; q < kAdiQ; ++q)
+    if (q0 + q * kPoseThreads + tid < nv) v += sqrt(best[q]);
+  v = wave_sum(v);
+  __syncthreads();  // previous chunk's readers are done with s_part
+  if ((tid & 63) == 0) s_part[tid >> 6] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int w = 0; w < kPoseThreads / 64; ++w) t += s_part[w];
+  return t;
+}
+
+// SPLIT = false: one workgroup per tuple, writes out[b].
+// SPLIT = true: workgroup (tuple, part) sweeps estimate points of range `part`
+// of nsplit and merges per-query minima into best2[b * stride + i].
+template <bool SPLIT>
 __global__ __launch_bounds__(kPoseThreads) void k_adi(const ObjDesc* __restrict__ objs,
                                                       const int32_t* __restrict__ slots,
                                                       const double* __restrict__ pe,
                                                       const double* __restrict__ pg,
                                                       double* __restrict__ out,
-                                                      const int32_t* __restrict__ order) {
+                                                      const int32_t* __restrict__ order,
+                                                      int nsplit, int64_t stride,
+                                                      double* __restrict__ best2) {
   __shared__ double s_e[3][kAdiTile];
   __shared__ double s_part[kPoseThreads / 64];
-  const int64_t b = order ? (int64_t)order[blockIdx.x] : (int64_t)blockIdx.x;
+  const int64_t u = SPLIT ? (int64_t)blockIdx.x / nsplit : (int64_t)blockIdx.x;
+  const int part = SPLIT ? (int)(blockIdx.x % (unsigned)nsplit) : 0;
+  const int64_t b = order ? (int64_t)order[u] : u;
   const int tid = threadIdx.x;
   const ObjDesc o = objs[slots[b]];
   const int nv = o.nv;
+  // this workgroup's estimate points [js, je)
+  const int per = SPLIT ? (nv + nsplit - 1) / nsplit : nv;
+  const int js = SPLIT ? min(nv, part * per) : 0;
+  const int je = SPLIT ? min(nv, js + per) : nv;
+  if (SPLIT && js >= je) return;  // workgroup-uniform
   double E[12], G[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
@@ -582,8 +625,8 @@ __global__ __launch_bounds__(kPoseThreads) void k_adi(const ObjDesc* __restrict_
   const double* __restrict__ px = o.pts;
   const double* __restrict__ py = o.pts + nv;
   const double* __restrict__ pz = o.pts + 2 * (int64_t)nv;
-  double sum = 0.0;
-  for (int q0 = 0; q0 < nv; q0 += kPoseThreads * kAdiQ) {
+  double total = 0.0;
+  for (int q0 = 0; q0 < nv; q0 += kAdiChunk) {
     double qx[kAdiQ], qy[kAdiQ], qz[kAdiQ], best[kAdiQ];
 #pragma unroll
     for (int q = 0; q < kAdiQ; ++q) {
@@ -595,8 +638,8 @@ __global__ __launch_bounds__(kPoseThreads) void k_adi(const ObjDesc* __restrict_
       qz[q] = aff(Ga, 2, x, y, z);
       best[q] = INFINITY;
     }
-    for (int j0 = 0; j0 < nv; j0 += kAdiTile) {
-      const int nj = min(kAdiTile, nv - j0);
+    for (int j0 = js; j0 < je; j0 += kAdiTile) {
+      const int nj = min(kAdiTile, je - j0);
       __syncthreads();
       for (int j = tid; j < nj; j += kPoseThreads) {
         const double x = px[j0 + j], y = py[j0 + j], z = pz[j0 + j];
@@ -620,18 +663,41 @@ __global__ __launch_bounds__(kPoseThreads) void k_adi(const ObjDesc* __restrict_
         for (int q = 0; q < kAdiQ; ++q) best[q] = fmin(best[q], d2(j, q));
       }
     }
+    if constexpr (SPLIT) {
+      // fmin never yields NaN here and d2 >= +0, so the bits order like the values
 #pragma unroll
-    for (int q = 0; q < kAdiQ; ++q)
-      if (q0 + q * kPoseThreads + tid < nv) sum += sqrt(best[q]);
+      for (int q = 0; q < kAdiQ; ++q) {
+        const int i = q0 + q * kPoseThreads + tid;
+        if (i < nv)
+          atomicMin((unsigned long long*)&best2[b * stride + i],
+                    (unsigned long long)__double_as_longlong(best[q]));
+      }
+    } else {
+      total += adi_chunk_sum(best, q0, nv, s_part);
+    }
   }
-  sum = wave_sum(sum);
-  if ((tid & 63) == 0) s_part[tid >> 6] = sum;
-  __syncthreads();
-  if (tid == 0) {
-    double t = 0.0;
-    for (int w = 0; w < kPoseThreads / 64; ++w) t += s_part[w];
-    out[b] = t / (double)nv;
+  if (!SPLIT && tid == 0) out[b] = total / (double)nv;
+}
+
+__global__ __launch_bounds__(kPoseThreads) void k_adi_finish(const ObjDesc* __restrict__ objs,
+                                                             const int32_t* __restrict__ slots,
+                                                             int64_t stride,
+                                                             const double* __restrict__ best2,
+                                                             double* __restrict__ out) {
+  __shared__ double s_part[kPoseThreads / 64];
+  const int64_t b = blockIdx.x;
+  const int nv = objs[slots[b]].nv;
+  double total = 0.0;
+  for (int q0 = 0; q0 < nv; q0 += kAdiChunk) {
+    double best[kAdiQ];
+#pragma unroll
+    for (int q = 0; q < kAdiQ; ++q) {
+      const int i = q0 + q * kPoseThreads + threadIdx.x;
+      best[q] = i < nv ? best2[b * stride + i] : 0.0;
+    }
+    total += adi_chunk_sum(best, q0, nv, s_part);
   }
+  if (threadIdx.x == 0) out[b] = total / (double)nv;
 }
 
 hipError_t launch_sym_error(int mode, const ObjDesc* objs, int max_ns, int64_t n,
@@ -671,12 +737,42 @@ hipError_t launch_mean_error(int mode, const ObjDesc* objs, int64_t n, const int
   return hipGetLastError();
 }
 
-hipError_t launch_adi(const ObjDesc* objs, int64_t n, const int32_t* slots, const double* pe,
-                      const double* pg, double* out, const int32_t* order, hipStream_t s) {
+hipError_t launch_adi(const ObjDesc* objs, int max_nv, int64_t n, const int32_t* slots,
+                      const double* pe, const double* pg, double* out, const int32_t* order,
+                      hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_adi, dim3((unsigned)n), dim3(kPoseThreads), 0, s, objs, slots, pe, pg,
-                     out, order);
-  return hipGetLastError();
+  // BOPX_ADI_SPLIT: ranges per tuple (0 / unset = automatic; tests force values)
+  const char* env = getenv("BOPX_ADI_SPLIT");
+  int nsplit = env ? atoi(env) : 0;
+  if (nsplit <= 0) {
+    // fill ~kAdiWorkgroups workgroups, ranges of >= kAdiMinRange points
+    constexpr int64_t kAdiWorkgroups = 2048, kAdiMinRange = 128;
+    nsplit = (int)std::min<int64_t>((kAdiWorkgroups + n - 1) / n,
+                                    (max_nv + kAdiMinRange - 1) / kAdiMinRange);
+  }
+  nsplit = std::max(1, std::min(nsplit, std::max(max_nv, 1)));
+  // the per-query scratch is n x max_nv doubles: only for small batches
+  const int64_t stride = max_nv;
+  if (nsplit > 1 && (n * nsplit > 0x7FFFFFFF || n * stride > ((int64_t)1 << 26))) nsplit = 1;
+  if (nsplit == 1) {
+    hipLaunchKernelGGL(k_adi<false>, dim3((unsigned)n), dim3(kPoseThreads), 0, s, objs, slots,
+                       pe, pg, out, order, 1, (int64_t)0, (double*)nullptr);
+    return hipGetLastError();
+  }
+  double* best2 = nullptr;
+  hipError_t e = hipMallocAsync((void**)&best2, (size_t)(n * stride) * sizeof(double), s);
+  if (e != hipSuccess) return e;
+  // 0xFF bytes: above the bits of every non-negative double (the +inf start)
+  e = hipMemsetAsync(best2, 0xFF, (size_t)(n * stride) * sizeof(double), s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_adi<true>, dim3((unsigned)(n * nsplit)), dim3(kPoseThreads), 0, s, objs,
+                       slots, pe, pg, out, order, nsplit, stride, best2);
+    hipLaunchKernelGGL(k_adi_finish, dim3((unsigned)n), dim3(kPoseThreads), 0, s, objs, slots,
+                       stride, (const double*)best2, out);
+    e = hipGetLastError();
+  }
+  const hipError_t f = hipFreeAsync(best2, s);
+  return e != hipSuccess ? e : f;
 }
 
 // ---------------------------------------------------------------------------

@@ -56,6 +56,7 @@ struct bopx_ctx {
   int32_t* d_rank = nullptr;  // slot -> rank by descending symmetry-error cost (nv * ns)
   size_t desc_cap = 0;
   int max_nf = 0;
+  int max_nv = 0;  // most vertices of a live object (ADI scratch stride)
   int max_ns = 0;  // most symmetries of a live object (MSSD/MSPD grid)
   int max_nm = 0;  // most meshlets of a live object (k_vsd rect registers)
   DevBuf ws;  // scratch for host-buffer calls
@@ -164,7 +165,7 @@ bopx::OrderCost sym_order_cost(const bopx_ctx* c) {
 
 int sync_desc(bopx_ctx* c) {
   std::vector<ObjDesc> h(c->objs.size());
-  int max_nf = 0, max_ns = 0, max_nm = 0;
+  int max_nf = 0, max_nv = 0, max_ns = 0, max_nm = 0;
   for (size_t i = 0; i < c->objs.size(); ++i) {
     const Object& o = c->objs[i];
     ObjDesc d{};
@@ -184,12 +185,14 @@ int sync_desc(bopx_ctx* c) {
       d.nm = (int)o.nm;
       d.ns = (int)o.ns;
       max_nf = std::max(max_nf, (int)o.nf);
+      max_nv = std::max(max_nv, (int)o.nv);
       max_ns = std::max(max_ns, (int)o.ns);
       max_nm = std::max(max_nm, (int)o.nm);
     }
     h[i] = d;
   }
   c->max_nf = max_nf;
+  c->max_nv = max_nv;
   c->max_ns = max_ns;
   c->max_nm = max_nm;
   if (h.size() > c->desc_cap) {
@@ -779,7 +782,7 @@ static int point_batch(bopx_ctx* c, int kind, int64_t n, const int32_t* obj_ids,
     e = bopx::launch_sym_error(kind, c->d_desc, c->max_ns, n, d_s, d_pe, d_pg, d_K, d_out, ord.p,
                                s);
   else if (kind == 3)
-    e = bopx::launch_adi(c->d_desc, n, d_s, d_pe, d_pg, d_out, ord.p, s);
+    e = bopx::launch_adi(c->d_desc, c->max_nv, n, d_s, d_pe, d_pg, d_out, ord.p, s);
   else
     e = bopx::launch_mean_error(kind == 2 ? 0 : 1, c->d_desc, n, d_s, d_pe, d_pg, d_K, d_out,
                                 ord.p, s);
@@ -850,7 +853,7 @@ int bopx_adi_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doubl
   hipStream_t s = pick_stream(c, stream);
   LaunchOrder ord;
   if (int r = make_order(c, n, slots, s, ord)) return r;
-  HIPCHK(c, bopx::launch_adi(c->d_desc, n, slots, pe, pg, out, ord.p, s));
+  HIPCHK(c, bopx::launch_adi(c->d_desc, c->max_nv, n, slots, pe, pg, out, ord.p, s));
   return BOPX_OK;
 }
 

@@ -711,3 +711,35 @@ def test_launch_order_large_batch(oracle_mod):
   assert np.array_equal(full["vsd"][sub], ref_vsd)
   np.testing.assert_allclose(full["mssd"][sub], ref_mssd, rtol=0, atol=TOL)
   np.testing.assert_allclose(full["mspd"][sub], ref_mspd, rtol=0, atol=TOL)
+
+
+def test_adi_split_bit_identical(monkeypatch):
+  """ADI's point-range split for small batches (k_adi<true> + k_adi_finish,
+  per-query minima merged by atomicMin) gives the same double as one workgroup
+  per tuple, for every split count, and matches the oracle (cKDTree-pinned)."""
+  from bop_toolkit_amd import _lib, synth
+  from oracle import oracle
+  rng = np.random.default_rng(41)
+  c = _lib.Context(0)
+  objs = {}
+  for oid, (nl, nn) in {1: (3, 5), 2: (20, 40), 3: (50, 60), 4: (30, 100)}.items():
+    pts, faces = synth.superellipsoid(nl, nn, tuple(rng.uniform(30, 90, 3)), 0.7)
+    c.add_object(oid, pts, faces)
+    objs[oid] = pts
+  n = 37
+  ids = rng.integers(1, 5, n).astype(np.int32)
+  Rg, tg = synth.gt_poses(rng, n)
+  Re, te = synth.perturb(rng, Rg, tg)
+  pe = np.concatenate([Re.reshape(n, 9), te], 1)
+  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
+  outs = {}
+  for split in ("1", "2", "3", "7", "64", "100000", None):
+    if split is None:
+      monkeypatch.delenv("BOPX_ADI_SPLIT", raising=False)
+    else:
+      monkeypatch.setenv("BOPX_ADI_SPLIT", split)
+    outs[split] = _batch(c, "bopx_adi_batch", ids, pe, pg)
+  for split, o in outs.items():
+    assert np.array_equal(o.view(np.uint64), outs["1"].view(np.uint64)), split
+  want = np.array([oracle.adi(objs[int(ids[i])], pe[i], pg[i]) for i in range(n)])
+  assert np.max(np.abs(outs[None] - want) / np.maximum(1.0, np.abs(want))) < 1e-9
