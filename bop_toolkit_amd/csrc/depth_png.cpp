@@ -90,6 +90,7 @@ struct Worker {
   // Inflate a zlib stream into exactly `out_n` bytes (the stream must end there).
   bool inflate_exact(const uint8_t* in, size_t in_n, uint8_t* out, size_t out_n) {
     if (ld) return deflate_lib().zlib(ld, in, in_n, out, out_n, nullptr) == 0;
+    if (in_n > 0xFFFFFFFFu || out_n > 0xFFFFFFFFu) return false;  // zlib's 32-bit counters
     z_stream zs;
     std::memset(&zs, 0, sizeof zs);
     if (inflateInit(&zs) != Z_OK) return false;

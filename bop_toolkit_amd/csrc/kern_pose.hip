@@ -761,7 +761,12 @@ hipError_t launch_adi(const ObjDesc* objs, int max_nv, int64_t n, const int32_t*
   }
   double* best2 = nullptr;
   hipError_t e = hipMallocAsync((void**)&best2, (size_t)(n * stride) * sizeof(double), s);
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess) {  // no room for the scratch: one workgroup per tuple (same result)
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(k_adi<false>, dim3((unsigned)n), dim3(kPoseThreads), 0, s, objs, slots,
+                       pe, pg, out, order, 1, (int64_t)0, (double*)nullptr);
+    return hipGetLastError();
+  }
   // 0xFF bytes: above the bits of every non-negative double (the +inf start)
   e = hipMemsetAsync(best2, 0xFF, (size_t)(n * stride) * sizeof(double), s);
   if (e == hipSuccess) {
