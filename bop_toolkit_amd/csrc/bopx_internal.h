@@ -92,7 +92,8 @@ struct VsdArgs {
   uint8_t* masks;    // GT-info mode, optional: n x 2 x img_h x img_w (mask, mask_visib)
   const int32_t* order;  // optional launch order (launch_order_by_slot): block k takes tuple order[k]
   int ablate;  // BOPX_VSD_ABLATE, read only by -DBOPX_VSD_DIAG=1 builds (kern_vsd.hip)
-  int cull;    // k_vsd occlusion test of far meshlet entries (BOPX_VSD_CULL, default 0)
+  int cull;    // k_vsd occlusion test (BOPX_VSD_CULL; default -1 = back-face test for objects of
+               // more than kCullAutoMeshlets meshlets)
   int qorder;  // k_vsd tile entry-queue order (BOPX_VSD_QORDER): 1 = large overlaps first
                // (default), 0 = near entries first; results are identical either way
   double taus[kMaxTaus];

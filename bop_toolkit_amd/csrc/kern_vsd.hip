@@ -458,6 +458,8 @@ constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 // q bits), so both orders give bit-identical results
 // (test_fused_vsd_occlusion_cull_exact runs both).
 constexpr int kLptOverlap = kTileW * kTileH / 4;
+// BOPX_VSD_CULL unset: back-face occlusion test for objects above this many meshlets
+constexpr int kCullAutoMeshlets = 256;
 
 // Tile loop barriers and the entry queue. Each wave's first entry group is
 // pre-assigned (no claim round trip for it): -0.9 % (same-box A/B, round 2).
@@ -587,7 +589,12 @@ void k_vsd(VsdArgs a) {
     s_qhi[0] = s_qhi[1] = 0.0f;
   }
   __syncthreads();
-  const bool cull_back = kCull && a.cull == 3;  // wave-uniform
+  // back-face occlusion test: forced (3) or automatic (-1) for objects of many
+  // meshlets, where overdraw per tile is high enough for the skipped entries to
+  // pay for the test (tools/gpu_cull_size.sh, configs[3] workload, same box,
+  // 2 reps, k_vsd time cull on vs off: 10k triangles +3.2 %, 15k +0.9 %,
+  // 20k -1.1 %, 25k -2.0 %, 30k -3.2 %; T-LESS-like configs[4] -2.8 %)
+  const bool cull_back = kCull && (a.cull == 3 || (a.cull < 0 && nm > kCullAutoMeshlets));
 
   // 1. per-pose meshlet rectangles (kept in registers: entry tid + 512 j) + ROI,
   // and each entry's nearest corner depth (queue order, see BOPX_VSD_PRIO above).

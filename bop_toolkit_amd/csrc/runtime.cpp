@@ -880,16 +880,15 @@ static float visib_thr32(double delta, int flags) {
 }
 
 // k_vsd's occlusion test of far meshlet entries (bit-identical results either
-// way; off by default: on the bench workload its test cost equals the raster
-// work it saves). Read per call, so a test can compare the two:
-// BOPX_VSD_CULL=1 on, 0 off, 2 test only (timing), 3 back-face occlusion test
-// (meshlet normal cones: back-facing entries queued last and tested against
-// their corner bound before any of their data is fetched; round 2, same box:
-// 17 % of the entries skipped, 16 % fewer set-ups, but +3.5 % time — the test's
-// LDS round trips sit in the tile's tail, kern_vsd.hip).
+// way). Read per call, so a test can compare the modes: BOPX_VSD_CULL=1 on,
+// 0 off, 2 test only (timing), 3 back-face occlusion test (meshlet normal
+// cones: back-facing entries queued last and tested against their corner bound
+// before any of their data is fetched), unset = -1: the back-face test for the
+// tuples whose object has more than kCullAutoMeshlets meshlets (kern_vsd.hip;
+// it costs +3.2 % on 10k-triangle meshes and saves 3 % on 30k-triangle ones).
 static int vsd_cull_enabled() {
   const char* e = getenv("BOPX_VSD_CULL");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : -1;
 }
 
 // k_vsd tile entry-queue order (kern_vsd.hip kLptOverlap): 1 = large overlaps

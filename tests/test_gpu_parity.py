@@ -743,3 +743,47 @@ def test_adi_split_bit_identical(monkeypatch):
     assert np.array_equal(o.view(np.uint64), outs["1"].view(np.uint64)), split
   want = np.array([oracle.adi(objs[int(ids[i])], pe[i], pg[i]) for i in range(n)])
   assert np.max(np.abs(outs[None] - want) / np.maximum(1.0, np.abs(want))) < 1e-9
+
+
+def test_auto_backface_cull_all_modes(oracle_mod, monkeypatch):
+  """BOPX_VSD_CULL unset: objects of more than 256 meshlets (here 30k
+  triangles) take the back-face occlusion test automatically. Silhouette and
+  GT-info modes run the same tile loop, so they are checked too: identical to
+  the test switched off (BOPX_VSD_CULL=0) and to the oracle raster."""
+  from bop_toolkit_amd import _lib
+  from bop_toolkit_amd._lib import _d, _f, _i32, _u8, ptr
+  n, W, H = 6, 640, 480
+  rng, pts, faces, Rg, tg, Re, te_, K = _scene(47, n, n_lat=100, n_lon=150)
+  assert len(faces) > 256 * 64
+  fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+  pe = np.concatenate([Re.reshape(n, 9), te_], 1)
+  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
+  cam = np.tile([fx, fy, cx, cy], (n, 1)).astype(np.float64)
+  ids, fi = np.full(n, 4, np.int32), np.arange(n, dtype=np.int32)
+  dgs = [oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, W, H)
+         for i in range(n)]
+  frames = np.stack([np.where(d > 0, d + 3.0, 1500.0) for d in dgs]).astype(np.float32)
+  res = {}
+  for cull in (None, "0"):
+    if cull is None:
+      monkeypatch.delenv("BOPX_VSD_CULL", raising=False)
+    else:
+      monkeypatch.setenv("BOPX_VSD_CULL", cull)
+    ctx = _lib.Context(0)
+    ctx.add_object(4, pts, faces)
+    cov = np.empty((n, 10))
+    ctx.call("bopx_cover_batch", n, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(fi, _i32), n,
+             W, H, ptr(cam, _d), ptr(cov, _d))
+    info = np.empty((n, 11))
+    masks = np.zeros((n, 2, H, W), np.uint8)
+    ctx.call("bopx_gt_info_batch", n, ptr(ids, _i32), ptr(pg, _d), ptr(fi, _i32),
+             ptr(frames, _f), n, W, H, ptr(cam, _d), 15.0, 0, 1, ptr(info, _d), ptr(masks, _u8))
+    ctx.close()
+    res[cull] = (cov, info, masks)
+  for a, b in zip(res[None], res["0"]):
+    assert np.array_equal(a, b)
+  cov, info, masks = res[None]
+  for i in range(n):
+    de = oracle_mod.render_depth(pts, faces, Re[i], te_[i], fx, fy, cx, cy, W, H)
+    assert np.array_equal(cov[i], _cover_ref(de, dgs[i])), i
+    assert np.array_equal(masks[i, 0] > 0, dgs[i] > 0), i
