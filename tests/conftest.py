@@ -15,6 +15,12 @@ if REPO not in sys.path:
 
 def pytest_configure(config):
   config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and libbopx.so")
+  # the host-only depth decoder (g++, seconds) is built on demand, like the oracle
+  io_lib = os.path.join(REPO, "bop_toolkit_amd", "lib", "libbopx_io.so")
+  if not os.path.exists(io_lib):
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "bop_toolkit_amd", "csrc"),
+                    "../lib/libbopx_io.so"], check=False)
 
 
 @pytest.fixture(scope="session")
