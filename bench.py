@@ -68,6 +68,8 @@ def parse():
   ap.add_argument("--objects", type=int, default=None)
   ap.add_argument("--n-lat", type=int, default=None)
   ap.add_argument("--n-lon", type=int, default=None)
+  ap.add_argument("--axes-scale", type=float, default=1.0,
+                  help="object size factor (design experiments; 1 = the configuration's)")
   ap.add_argument("--cpu-seconds", type=float, default=10.0,
                   help="target wall time of the CPU-baseline sample")
   ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -88,7 +90,7 @@ def build_objects(ev, args, torch):
   rng = np.random.default_rng(args.seed)
   objs = []
   for o in range(args.objects):
-    axes = tuple(rng.uniform(30.0, 100.0, 3))
+    axes = tuple(args.axes_scale * rng.uniform(30.0, 100.0, 3))
     pts, faces = synth.superellipsoid(args.n_lat, args.n_lon, axes, float(rng.uniform(0.5, 1.0)))
     # exact diameter (max pairwise distance) on the host, in row chunks: set-up
     # only, kept off the GPU so the profile holds the measured kernels alone
@@ -435,7 +437,8 @@ def main():
                                        len(o["syms"]) for o in objs)))), W, H,
                                    args.cfg["K"].split("_")[0], n),
                    "global_batch": n * world, "parallelism": "image-sharded x%d" % world,
-                   "roi_mean_px": round(cost["roi_mean"], 1)},
+                   "roi_mean_px": round(cost["roi_mean"], 1),
+                   **({"axes_scale": args.axes_scale} if args.axes_scale != 1.0 else {})},
         "roofline": roof, "kernels": kernels, "cpu_baseline": cpu}
     print(json.dumps(line), flush=True)
   if world > 1:

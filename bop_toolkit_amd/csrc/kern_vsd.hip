@@ -460,6 +460,7 @@ constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 constexpr int kLptOverlap = kTileW * kTileH / 4;
 // BOPX_VSD_CULL unset: back-face occlusion test for objects above this many meshlets
 constexpr int kCullAutoMeshlets = 256;
+constexpr int kCullAutoDensity = 12;  // ... and at least this many meshlets per ROI tile
 
 // Tile loop barriers and the entry queue. Each wave's first entry group is
 // pre-assigned (no claim round trip for it): -0.9 % (same-box A/B, round 2).
@@ -593,8 +594,11 @@ void k_vsd(VsdArgs a) {
   // meshlets, where overdraw per tile is high enough for the skipped entries to
   // pay for the test (tools/gpu_cull_size.sh, configs[3] workload, same box,
   // 2 reps, k_vsd time cull on vs off: 10k triangles +3.2 %, 15k +0.9 %,
-  // 20k -1.1 %, 25k -2.0 %, 30k -3.2 %; T-LESS-like configs[4] -2.8 %)
-  const bool cull_back = kCull && (a.cull == 3 || (a.cull < 0 && nm > kCullAutoMeshlets));
+  // 20k -1.1 %, 25k -2.0 %, 30k -3.2 %; T-LESS-like configs[4] -2.8 %); the
+  // on-screen density condition is applied once the ROI is known (below)
+  // (tools/gpu_cull_density.sh: 30k triangles at 1.5x size -1.4 %, 2x +1 %;
+  // 10k triangles at 0.5x / 0.7x size still +1.8 % / +1.2 %)
+  const bool cull_maybe = kCull && (a.cull == 3 || (a.cull < 0 && nm > kCullAutoMeshlets));
 
   // 1. per-pose meshlet rectangles (kept in registers: entry tid + 512 j) + ROI,
   // and each entry's nearest corner depth (queue order, see BOPX_VSD_PRIO above).
@@ -652,7 +656,7 @@ void k_vsd(VsdArgs a) {
         else atomicMin(z, __float_as_int(zr[k]));
       }
     }
-    if (cull_back) {
+    if (cull_maybe) {
       qh[0] = wave_max_nonneg_f32(qh[0]);
       qh[1] = wave_max_nonneg_f32(qh[1]);
       if (lane == 0) {
@@ -681,6 +685,12 @@ void k_vsd(VsdArgs a) {
   for (int i = tid; i < 2 * kTileStride * kTileH; i += kVsdThreads) (&s_dep[0][0])[i] = 0u;
   __syncthreads();
   const int rx0 = s_roi[0], ry0 = s_roi[1], rx1 = s_roi[2], ry1 = s_roi[3];
+  // automatic mode also asks for meshlets dense on screen: >= kCullAutoDensity
+  // per ROI tile (a 30k-triangle object drawn large, 10 per tile, loses 1 %)
+  const int roi_tiles = rx0 <= rx1 && ry0 <= ry1
+                            ? ((rx1 - rx0 + kTileW) / kTileW) * ((ry1 - ry0 + kTileH) / kTileH)
+                            : 0;
+  const bool cull_back = cull_maybe && (a.cull == 3 || nm >= kCullAutoDensity * roi_tiles);
   // far half of each pose's depth range (wave-uniform thresholds)
   uint32_t far_bits = 0;
 #pragma unroll
