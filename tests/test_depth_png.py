@@ -171,3 +171,17 @@ def test_ancillary_chunk_skipped_and_zlib_backend_identical(tmp_path):
   env = dict(os.environ, BOPX_IO_ZLIB="1")
   subprocess.check_call([sys.executable, "-c", code], env=env)
   assert np.array_equal(np.load(str(tmp_path / "z.npy")), _pillow(p))
+
+
+def test_scale_is_one_float32_multiply(tmp_path):
+  """depth_scale is applied as float32(sample) * float32(scale) for every scalar
+  type — what the reference's `depth *= depth_scale` does with its JSON float
+  (and, under its NumPy < 1.24, with a numpy float64 too)."""
+  rng = np.random.default_rng(13)
+  p = str(tmp_path / "s.png")
+  img = _depth(rng, 16, 16)
+  write_png16(p, img)
+  for s in (0.1, np.float64(0.1), np.float32(0.1), 1.0 / 3.0, 7):
+    got = inout.load_depths([p], scales=[s])[0]
+    want = img.astype(np.float32) * np.float32(s)
+    assert got.dtype == np.float32 and np.array_equal(got, want), s
