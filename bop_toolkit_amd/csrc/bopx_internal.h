@@ -96,8 +96,16 @@ struct VsdArgs {
                // more than kCullAutoMeshlets meshlets)
   int qorder;  // k_vsd tile entry-queue order (BOPX_VSD_QORDER): 1 = large overlaps first
                // (default), 0 = near entries first; results are identical either way
+  // Tile-parallel mode (VSD costs only): `split` workgroups per tuple, workgroup
+  // s walking ROI tiles s, s + split, ...; each writes one row of kVsdPartCols
+  // doubles to `part` and k_vsd_combine reduces the rows in split order. Set by
+  // launch_vsd (small batches, BOPX_VSD_SPLIT), 1 = one workgroup per tuple.
+  int split;
+  double* part;
   double taus[kMaxTaus];
 };
+constexpr int kVsdPartCols = 2 + 2 * kMaxTaus;  // union, inter, cnt[kMaxTaus], lin[kMaxTaus]
+constexpr int kVsdMaxSplit = 16;
 
 // Launchers (kernels in kern_pose.hip / kern_vsd.hip). All return hipError_t of
 // the launch; inputs are device pointers.

@@ -529,7 +529,11 @@ void k_vsd(VsdArgs a) {
   uint32_t(*s_cnt)[2 + kMaxTaus] = reinterpret_cast<uint32_t(*)[2 + kMaxTaus]>(&s_dep[0][0]);
   double(*s_lin)[kMaxTaus] = reinterpret_cast<double(*)[kMaxTaus]>(&s_dep[1][0]);
 
-  const int64_t b = a.order ? (int64_t)a.order[blockIdx.x] : (int64_t)blockIdx.x;
+  // tile-parallel mode: workgroup (tuple k, split sp) of a.split per tuple
+  const int S = a.split;
+  const int64_t kb = S > 1 ? (int64_t)(blockIdx.x / (unsigned)S) : (int64_t)blockIdx.x;
+  const int sp = S > 1 ? (int)(blockIdx.x - kb * S) : 0;
+  const int64_t b = a.order ? (int64_t)a.order[kb] : kb;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   RVtx* const w_stage = reinterpret_cast<RVtx*>(&s_wscr[wave][0]);
@@ -740,7 +744,7 @@ void k_vsd(VsdArgs a) {
     const int ntx = (rx1 - rx0 + kTileW) / kTileW, nty = (ry1 - ry0 + kTileH) / kTileH;
     if (VSD_DIAG(4) && tid == 0) atomicAdd(&g_vsd_stats[0], (unsigned long long)(ntx * nty));
     VSD_STAMP(6);
-    for (int t = 0; t < ntx * nty; ++t) {
+    for (int t = sp; t < ntx * nty; t += S) {
       const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
       const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
       // 2a. list the (pose, meshlet) entries touching the tile (the q tiles are
@@ -1449,6 +1453,22 @@ void k_vsd(VsdArgs a) {
       }
       return;
     }
+    if (S > 1) {  // partial row of this split; k_vsd_combine applies the formula
+      double* row = a.part + ((int64_t)b * S + sp) * kVsdPartCols;
+      row[0] = (double)un;
+      row[1] = (double)in;
+      for (int k = 0; k < a.n_tau; ++k) {
+        uint64_t cnt = 0;
+        double sum = 0.0;
+        for (int w = 0; w < kVsdWaves; ++w) {
+          cnt += s_cnt[w][2 + k];
+          sum += s_lin[w][k];
+        }
+        row[2 + k] = (double)cnt;
+        row[2 + kMaxTaus + k] = sum;
+      }
+      return;
+    }
     double* out = a.out + b * (int64_t)a.n_tau;
     for (int k = 0; k < a.n_tau; ++k) {
       if (un == 0) {
@@ -1479,9 +1499,48 @@ hipError_t read_vsd_stats(unsigned long long* out, int reset) {
 
 constexpr int kBopTaus = 10;  // eval_calc_errors.py:47, np.arange(0.05, 0.51, 0.05)
 
+// Tile-parallel mode, second pass: one workgroup per tuple stages its split
+// rows in LDS (one round of loads, not a dependent chain per row), then thread
+// k sums tau k's rows in split order (counts exact in float64; tlinear sums in
+// a fixed order) and applies pose_error.py:85-91 like the one-workgroup path.
+constexpr int kCombineThreads = 256;
+__global__ __launch_bounds__(kCombineThreads) void k_vsd_combine(
+    int S, int n_tau, int cost_type, const double* __restrict__ part, double* __restrict__ out) {
+  __shared__ double s_row[kVsdMaxSplit * kVsdPartCols];
+  const int64_t b = blockIdx.x;
+  const double* row = part + b * S * kVsdPartCols;
+  for (int i = threadIdx.x; i < S * kVsdPartCols; i += kCombineThreads) s_row[i] = row[i];
+  __syncthreads();
+  const int k = threadIdx.x;
+  if (k >= n_tau) return;
+  double un = 0.0, in = 0.0, acc = 0.0;
+  const int col = (cost_type == 0 ? 2 : 2 + kMaxTaus) + k;
+  for (int s = 0; s < S; ++s) {
+    un += s_row[s * kVsdPartCols];
+    in += s_row[s * kVsdPartCols + 1];
+    acc += s_row[s * kVsdPartCols + col];
+  }
+  out[b * n_tau + k] = un == 0.0 ? 1.0 : (acc + (un - in)) / un;
+}
+
+// Workgroups per tuple: small batches (fewer than 256 tuples, one workgroup
+// per CU or less) split each tuple's ROI tiles over up to kVsdMaxSplit
+// workgroups; BOPX_VSD_SPLIT=k forces k (1 = off). VSD costs only.
+static int vsd_split(int64_t n, int cost_type) {
+  if (cost_type != 0 && cost_type != 1) return 1;
+  static const int force = [] {
+    const char* e = getenv("BOPX_VSD_SPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  if (force > 0) return force < kVsdMaxSplit ? force : kVsdMaxSplit;
+  if (n >= 256) return 1;
+  const int64_t s = 256 / n;
+  return (int)(s < kVsdMaxSplit ? s : kVsdMaxSplit);
+}
+
 template <int RPT>
 static void launch_vsd_rpt(const VsdArgs& a, int cost_type, hipStream_t s) {
-  dim3 grid((unsigned)a.n), block(kVsdThreads);
+  dim3 grid((unsigned)(a.n * a.split)), block(kVsdThreads);
 #if BOPX_VSD_DIAG
   // occupancy experiment (diag builds): unused dynamic LDS per workgroup
   static const unsigned dyn = [] {
@@ -1503,8 +1562,21 @@ static void launch_vsd_rpt(const VsdArgs& a, int cost_type, hipStream_t s) {
     hipLaunchKernelGGL((k_vsd<kCostGtInfo, RPT, kMaxTaus>), grid, block, 0, s, a);
 }
 
-hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s) {
-  if (a.n <= 0) return hipSuccess;
+hipError_t launch_vsd(const VsdArgs& a_in, int cost_type, hipStream_t s) {
+  if (a_in.n <= 0) return hipSuccess;
+  VsdArgs a = a_in;
+  a.split = vsd_split(a.n, cost_type);
+  a.part = nullptr;
+  if (a.split > 1) {
+    // stream-ordered scratch, freed behind the combine pass; without it the
+    // launch keeps one workgroup per tuple
+    const size_t bytes = (size_t)a.n * a.split * kVsdPartCols * sizeof(double);
+    if (hipMallocAsync((void**)&a.part, bytes, s) != hipSuccess) {
+      (void)hipGetLastError();
+      a.part = nullptr;
+      a.split = 1;
+    }
+  }
   const int need = 2 * a.max_nm;
   if (need <= kVsdThreads)
     launch_vsd_rpt<1>(a, cost_type, s);
@@ -1514,6 +1586,15 @@ hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s) {
     launch_vsd_rpt<kRectsPerThread>(a, cost_type, s);
   else
     launch_vsd_rpt<0>(a, cost_type, s);  // rectangles recomputed per tile (any size)
+  if (a.split > 1) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_vsd_combine, dim3((unsigned)a.n), dim3(kCombineThreads), 0, s, a.split,
+                       a.n_tau, cost_type, (const double*)a.part, a.out);
+    e = hipGetLastError();
+    const hipError_t f = hipFreeAsync(a.part, s);
+    return e != hipSuccess ? e : f;
+  }
   return hipGetLastError();
 }
 

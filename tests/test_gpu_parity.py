@@ -232,6 +232,50 @@ def _fused_vs_oracle(oracle_mod, seed, n, W, H, K, n_lat, n_lon, delta=15.0, cos
   return out
 
 
+def test_fused_vsd_tile_parallel_matches_one_workgroup():
+  """Tile-parallel mode (kern_vsd.hip vsd_split: batches below 256 tuples split
+  each tuple's ROI tiles over up to 16 workgroups, k_vsd_combine sums the rows)
+  against the one-workgroup-per-tuple launch of a 320-tuple batch: step cost
+  bit-identical, tlinear within 1e-13 (its float64 sums change order)."""
+  from bop_toolkit_amd import _lib, synth
+  from bop_toolkit_amd._lib import _d, _f, _i32, ptr
+  n, nf, W, H = 320, 8, 640, 480
+  rng, pts, faces, Rg, tg, Re, te_, K = _scene(41, n, n_lat=30, n_lon=60,
+                                              z_range=(330.0, 900.0))
+  ctx = _lib.Context(0)
+  ctx.add_object(3, pts, faces)
+  fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+  frames = np.round(rng.uniform(300.0, 1300.0, (nf, H, W))).astype(np.float32)
+  frames[rng.random(frames.shape) < 0.1] = 0.0
+  taus = np.arange(0.05, 0.51, 0.05)
+  ids = np.full(n, 3, np.int32)
+  pe = np.concatenate([Re.reshape(n, 9), te_], 1)
+  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
+  fi = (np.arange(n) % nf).astype(np.int32)
+  cam = np.tile([fx, fy, cx, cy], (nf, 1)).astype(np.float64)
+  dia = np.full(n, 150.0)
+
+  def run(lo, hi, code):
+    m = hi - lo
+    out = np.empty((m, len(taus)))
+    ctx.call("bopx_vsd_batch", m, ptr(ids[lo:hi], _i32), ptr(pe[lo:hi].copy(), _d),
+             ptr(pg[lo:hi].copy(), _d), ptr(fi[lo:hi].copy(), _i32), ptr(frames, _f), nf, W, H,
+             ptr(cam, _d), 15.0, 0, ptr(taus, _d), len(taus), 1, ptr(dia[lo:hi].copy(), _d),
+             code, ptr(out, _d))
+    return out
+
+  for code in (0, 1):
+    full = run(0, n, code)
+    assert np.ptp(full) > 0.1
+    parts = [run(0, 1, code), run(1, 25, code), run(25, 100, code)]
+    got = np.concatenate(parts)
+    if code == 0:
+      assert np.array_equal(got, full[:100])
+    else:
+      np.testing.assert_allclose(got, full[:100], rtol=0, atol=1e-13)
+  ctx.close()
+
+
 def test_fused_vsd_bit_exact_lmo(oracle_mod):
   from bop_toolkit_amd import synth
   out = _fused_vs_oracle(oracle_mod, 11, 40, 640, 480, synth.LMO_K, 30, 60)
