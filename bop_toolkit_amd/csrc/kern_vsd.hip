@@ -1523,9 +1523,17 @@ __global__ __launch_bounds__(kCombineThreads) void k_vsd_combine(
   out[b * n_tau + k] = un == 0.0 ? 1.0 : (acc + (un - in)) / un;
 }
 
-// Workgroups per tuple: small batches (fewer than 256 tuples, one workgroup
-// per CU or less) split each tuple's ROI tiles over up to kVsdMaxSplit
-// workgroups; BOPX_VSD_SPLIT=k forces k (1 = off). VSD costs only.
+// Workgroups per tuple: batches of fewer than kVsdSplitBelow tuples split each
+// tuple's ROI tiles over S = clamp(kVsdSplitTarget / n, 4, 16) workgroups, so
+// the last tuples' tiles spread over the CUs instead of trailing;
+// BOPX_VSD_SPLIT=k forces k (1 = off). VSD costs only. Measured
+// (tools/split_sweep.py, wall ms per bopx_vsd_batch call, 5k-vertex object,
+// profiles/r02_split/split_sweep.jsonl) — best S per batch size: 32-64 tuples
+// 16, 128 8, 192-768 4 (768: S = 1 / 2 / 4 1.06 / 0.90 / 0.86 ms), 1,024 a tie
+// (0.92 / 0.91 / 1.03), from 1,536 S = 1 (1.23 / 1.27 / 1.47; the 12,504-tuple
+// bench: 9.38 / 10.0 / 11.4 ms for k_vsd).
+constexpr int64_t kVsdSplitTarget = 1024;
+constexpr int64_t kVsdSplitBelow = 1024;
 static int vsd_split(int64_t n, int cost_type) {
   if (cost_type != 0 && cost_type != 1) return 1;
   static const int force = [] {
@@ -1533,9 +1541,9 @@ static int vsd_split(int64_t n, int cost_type) {
     return e ? atoi(e) : 0;
   }();
   if (force > 0) return force < kVsdMaxSplit ? force : kVsdMaxSplit;
-  if (n >= 256) return 1;
-  const int64_t s = 256 / n;
-  return (int)(s < kVsdMaxSplit ? s : kVsdMaxSplit);
+  if (n >= kVsdSplitBelow) return 1;
+  const int64_t s = kVsdSplitTarget / n;
+  return (int)(s < 4 ? 4 : s > kVsdMaxSplit ? kVsdMaxSplit : s);
 }
 
 template <int RPT>

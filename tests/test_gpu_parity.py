@@ -233,13 +233,13 @@ def _fused_vs_oracle(oracle_mod, seed, n, W, H, K, n_lat, n_lon, delta=15.0, cos
 
 
 def test_fused_vsd_tile_parallel_matches_one_workgroup():
-  """Tile-parallel mode (kern_vsd.hip vsd_split: batches below 256 tuples split
+  """Tile-parallel mode (kern_vsd.hip vsd_split: batches below 1,024 tuples split
   each tuple's ROI tiles over up to 16 workgroups, k_vsd_combine sums the rows)
-  against the one-workgroup-per-tuple launch of a 320-tuple batch: step cost
+  against the one-workgroup-per-tuple launch of a 1,100-tuple batch: step cost
   bit-identical, tlinear within 1e-13 (its float64 sums change order)."""
   from bop_toolkit_amd import _lib, synth
   from bop_toolkit_amd._lib import _d, _f, _i32, ptr
-  n, nf, W, H = 320, 8, 640, 480
+  n, nf, W, H = 1100, 8, 640, 480
   rng, pts, faces, Rg, tg, Re, te_, K = _scene(41, n, n_lat=30, n_lon=60,
                                               z_range=(330.0, 900.0))
   ctx = _lib.Context(0)
@@ -267,12 +267,13 @@ def test_fused_vsd_tile_parallel_matches_one_workgroup():
   for code in (0, 1):
     full = run(0, n, code)
     assert np.ptp(full) > 0.1
-    parts = [run(0, 1, code), run(1, 25, code), run(25, 100, code)]
+    # splits 16, 16, 13 and 4 workgroups per tuple
+    parts = [run(0, 1, code), run(1, 25, code), run(25, 100, code), run(100, 400, code)]
     got = np.concatenate(parts)
     if code == 0:
-      assert np.array_equal(got, full[:100])
+      assert np.array_equal(got, full[:400])
     else:
-      np.testing.assert_allclose(got, full[:100], rtol=0, atol=1e-13)
+      np.testing.assert_allclose(got, full[:400], rtol=0, atol=1e-13)
   ctx.close()
 
 

@@ -15,3 +15,7 @@ BOPX_VSD_SPLIT=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_ou
 for d in prof_split prof_nosplit; do echo "== $d"; find gpurun_out/$d -name "*kernel_stats.csv" -exec grep -h "k_vsd\|Name" {} \; ; done
 timeout -k 10 300 python bench.py > gpurun_out/bench_split.json 2> gpurun_out/bench_split.err || { tail -30 gpurun_out/bench_split.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/bench_split.json'));print(round(d['value']), {k:round(v['ms'],3) for k,v in d['kernels'].items()})"
+timeout -k 10 200 python tools/split_sweep.py 1,4,16,32,64,128,192,256,384,512,768,1024,1536 > gpurun_out/split_sweep_auto3.json 2> gpurun_out/split_sweep.err || { tail -20 gpurun_out/split_sweep.err; exit 1; }
+cat gpurun_out/split_sweep_auto3.json
+timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; cat gpurun_out/smoke.log; exit 1; }
+tail -2 gpurun_out/smoke.log
