@@ -96,7 +96,7 @@ struct VsdArgs {
                // more than kCullAutoMeshlets meshlets)
   int qorder;  // k_vsd tile entry-queue order (BOPX_VSD_QORDER): 1 = large overlaps first
                // (default), 0 = near entries first; results are identical either way
-  // Tile-parallel mode (VSD costs only): `split` workgroups per tuple, workgroup
+  // Tile-parallel mode (every cost mode): `split` workgroups per tuple, workgroup
   // s walking ROI tiles s, s + split, ...; each writes one row of kVsdPartCols
   // doubles to `part` and k_vsd_combine reduces the rows in split order. Set by
   // launch_vsd (small batches, BOPX_VSD_SPLIT), 1 = one workgroup per tuple.

@@ -1435,7 +1435,9 @@ void k_vsd(VsdArgs a) {
     }
     if constexpr (COST == kCostCover || COST == kCostGtInfo) {
       // cover: union, inter, 8 bbox values; GT info: all, visib, 8 bbox values, valid
-      double* out = a.out + b * (int64_t)(COST == kCostCover ? kCoverCols : kGtInfoCols);
+      // tile-parallel mode: the same columns as a partial row (k_vsd_combine)
+      double* out = S > 1 ? a.part + ((int64_t)b * S + sp) * kVsdPartCols
+                          : a.out + b * (int64_t)(COST == kCostCover ? kCoverCols : kGtInfoCols);
       out[0] = (double)un;
       out[1] = (double)in;
       if (COST == kCostGtInfo) {
@@ -1512,6 +1514,19 @@ __global__ __launch_bounds__(kCombineThreads) void k_vsd_combine(
   for (int i = threadIdx.x; i < S * kVsdPartCols; i += kCombineThreads) s_row[i] = row[i];
   __syncthreads();
   const int k = threadIdx.x;
+  if (cost_type == kCostCover || cost_type == kCostGtInfo) {
+    // counts summed (exact), bounding boxes min / max (empty = INT_MAX, -1)
+    const int cols = cost_type == kCostCover ? kCoverCols : kGtInfoCols;
+    if (k >= cols) return;
+    double v = s_row[k];
+    for (int s = 1; s < S; ++s) {
+      const double o = s_row[s * kVsdPartCols + k];
+      if (k < 2 || k == 10) v += o;
+      else v = ((k - 2) & 2) ? fmax(v, o) : fmin(v, o);
+    }
+    out[b * cols + k] = v;
+    return;
+  }
   if (k >= n_tau) return;
   double un = 0.0, in = 0.0, acc = 0.0;
   const int col = (cost_type == 0 ? 2 : 2 + kMaxTaus) + k;
@@ -1526,7 +1541,8 @@ __global__ __launch_bounds__(kCombineThreads) void k_vsd_combine(
 // Workgroups per tuple: batches of fewer than kVsdSplitBelow tuples split each
 // tuple's ROI tiles over S = clamp(kVsdSplitTarget / n, 4, 16) workgroups, so
 // the last tuples' tiles spread over the CUs instead of trailing;
-// BOPX_VSD_SPLIT=k forces k (1 = off). VSD costs only. Measured
+// BOPX_VSD_SPLIT=k forces k (1 = off). Every cost mode (VSD, silhouette
+// cover, GT info: each ROI tile and its mask pixels belong to one split). Measured
 // (tools/split_sweep.py, wall ms per bopx_vsd_batch call, 5k-vertex object,
 // profiles/r02_split/split_sweep.jsonl) — best S per batch size: 32-64 tuples
 // 16, 128 8, 192-768 4 (768: S = 1 / 2 / 4 1.06 / 0.90 / 0.86 ms), 1,024 a tie
@@ -1535,7 +1551,6 @@ __global__ __launch_bounds__(kCombineThreads) void k_vsd_combine(
 constexpr int64_t kVsdSplitTarget = 1024;
 constexpr int64_t kVsdSplitBelow = 1024;
 static int vsd_split(int64_t n, int cost_type) {
-  if (cost_type != 0 && cost_type != 1) return 1;
   static const int force = [] {
     const char* e = getenv("BOPX_VSD_SPLIT");
     return e ? atoi(e) : 0;

@@ -236,7 +236,8 @@ def test_fused_vsd_tile_parallel_matches_one_workgroup():
   """Tile-parallel mode (kern_vsd.hip vsd_split: batches below 1,024 tuples split
   each tuple's ROI tiles over up to 16 workgroups, k_vsd_combine sums the rows)
   against the one-workgroup-per-tuple launch of a 1,100-tuple batch: step cost
-  bit-identical, tlinear within 1e-13 (its float64 sums change order)."""
+  bit-identical, tlinear within 1e-13 (its float64 sums change order), the
+  silhouette cover mode bit-identical."""
   from bop_toolkit_amd import _lib, synth
   from bop_toolkit_amd._lib import _d, _f, _i32, ptr
   n, nf, W, H = 1100, 8, 640, 480
@@ -274,6 +275,17 @@ def test_fused_vsd_tile_parallel_matches_one_workgroup():
       assert np.array_equal(got, full[:400])
     else:
       np.testing.assert_allclose(got, full[:400], rtol=0, atol=1e-13)
+  # silhouette cover mode (bboxes min / max over the splits, counts summed)
+  def cover(lo, hi):
+    out = np.empty((hi - lo, 10))
+    ctx.call("bopx_cover_batch", hi - lo, ptr(ids[lo:hi], _i32), ptr(pe[lo:hi].copy(), _d),
+             ptr(pg[lo:hi].copy(), _d), ptr(fi[lo:hi].copy(), _i32), nf, W, H, ptr(cam, _d),
+             ptr(out, _d))
+    return out
+  full = cover(0, n)
+  assert (full[:, 0] > 0).all()
+  got = np.concatenate([cover(0, 1), cover(1, 25), cover(25, 100), cover(100, 400)])
+  assert np.array_equal(got, full[:400])
   ctx.close()
 
 
