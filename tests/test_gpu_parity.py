@@ -286,6 +286,18 @@ def test_fused_vsd_tile_parallel_matches_one_workgroup():
   assert (full[:, 0] > 0).all()
   got = np.concatenate([cover(0, 1), cover(1, 25), cover(25, 100), cover(100, 400)])
   assert np.array_equal(got, full[:400])
+
+  # GT-info mode on the calc_gt_info canvas (3x the image, calc_gt_info.py:66-73)
+  def gt_info(lo, hi):
+    out = np.empty((hi - lo, 11))
+    ctx.call("bopx_gt_info_batch", hi - lo, ptr(ids[lo:hi], _i32), ptr(pg[lo:hi].copy(), _d),
+             ptr(fi[lo:hi].copy(), _i32), ptr(frames, _f), nf, W, H, ptr(cam, _d), 15.0, 0, 3,
+             ptr(out, _d), None)
+    return out
+  full = gt_info(0, n)
+  assert (full[:, 0] > 0).all() and (full[:, 1] > 0).any()
+  got = np.concatenate([gt_info(0, 1), gt_info(1, 25), gt_info(25, 100), gt_info(100, 400)])
+  assert np.array_equal(got, full[:400])
   ctx.close()
 
 
