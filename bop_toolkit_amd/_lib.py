@@ -112,6 +112,12 @@ def ptr(a, ct):
   return a.ctypes.data_as(ct) if a is not None else None
 
 
+def cast_ptr(addr, ct):
+  """Pointer of type ct at a raw address (an offset into an array whose
+  lifetime the caller holds)."""
+  return ctypes.cast(addr, ct)
+
+
 def device_count():
   n = _I(0)
   load().bopx_device_count(ctypes.byref(n))

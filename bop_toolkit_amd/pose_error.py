@@ -31,6 +31,24 @@ def _tau_chunks(n):
   return [(k0, min(k0 + _lib.MAX_TAUS, n)) for k0 in range(0, n, _lib.MAX_TAUS)]
 
 
+# Per-call constants of the fused VSD path (inputs the library only reads): the
+# one-tuple frame index, obj_id arrays and tau chunks, with their ctypes
+# pointers made once (numpy's .ctypes costs ~4 us per array and call).
+_ZERO_I32 = np.zeros(1, np.int32)
+_ZERO_I32_P = ptr(_ZERO_I32, _i32)
+_CONST_CACHE = {}
+
+
+def _const(key, make, ct):
+  hit = _CONST_CACHE.get(key)
+  if hit is None:
+    if len(_CONST_CACHE) > 256:
+      _CONST_CACHE.clear()
+    arr = make()
+    hit = _CONST_CACHE[key] = (arr, ptr(arr, ct))
+  return hit[1]
+
+
 def vsd(R_est, t_est, R_gt, t_gt, depth_test, K, delta, taus, normalized_by_diameter,
         diameter, renderer, obj_id, cost_type="step"):
   """Visible Surface Discrepancy (pose_error.py:17-93).
@@ -51,19 +69,29 @@ def vsd(R_est, t_est, R_gt, t_gt, depth_test, K, delta, taus, normalized_by_diam
   out = np.empty(len(taus), np.float64)
   code = _cost_code(cost_type)
   if isinstance(renderer, RendererHIP) and renderer.ctx is ctx and code is not None and taus:
-    ids = np.array([obj_id], np.int32)
-    pe = runtime.pose12(R_est, t_est)
-    pg = runtime.pose12(R_gt, t_gt)
-    fi = np.zeros(1, np.int32)
-    cam = np.array([fx, fy, cx, cy], np.float64)
-    dia = np.array([float(diameter)], np.float64)
-    for k0, k1 in _tau_chunks(len(taus)):  # the kernels take MAX_TAUS per call
-      part, o = np.ascontiguousarray(tau_arr[k0:k1]), np.empty(k1 - k0, np.float64)
-      ctx.call("bopx_vsd_batch", 1, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(fi, _i32),
-               ptr(depth_test, _f), 1, W, H, ptr(cam, _d), float(delta), flags, ptr(part, _d),
-               k1 - k0, int(bool(normalized_by_diameter)), ptr(dia, _d), code, ptr(o, _d))
-      out[k0:k1] = o
-    return [float(e) for e in out]
+    oid = int(obj_id)
+    p_ids = _const(("id", oid), lambda: np.array([oid], np.int32), _i32)
+    # pose_est | pose_gt | cam | diameter | results in one float64 block
+    nt = len(taus)
+    blk = np.empty(29 + nt, np.float64)
+    blk[0:9] = np.asarray(R_est, np.float64).reshape(9)
+    blk[9:12] = np.asarray(t_est, np.float64).reshape(3)
+    blk[12:21] = np.asarray(R_gt, np.float64).reshape(9)
+    blk[21:24] = np.asarray(t_gt, np.float64).reshape(3)
+    blk[24:28] = (fx, fy, cx, cy)
+    blk[28] = float(diameter)
+    base = blk.ctypes.data
+    step = blk.itemsize
+    p_pe, p_pg = _lib.cast_ptr(base, _d), _lib.cast_ptr(base + 12 * step, _d)
+    p_cam, p_dia = _lib.cast_ptr(base + 24 * step, _d), _lib.cast_ptr(base + 28 * step, _d)
+    p_dep = ptr(depth_test, _f)
+    for k0, k1 in _tau_chunks(nt):  # the kernels take MAX_TAUS per call
+      key = ("taus", tau_arr[k0:k1].tobytes())  # bit-exact (signed zeros, NaNs)
+      p_tau = _const(key, lambda: np.ascontiguousarray(tau_arr[k0:k1]), _d)
+      ctx.call("bopx_vsd_batch", 1, p_ids, p_pe, p_pg, _ZERO_I32_P, p_dep, 1, W, H, p_cam,
+               float(delta), flags, p_tau, k1 - k0, int(bool(normalized_by_diameter)), p_dia,
+               code, _lib.cast_ptr(base + (29 + k0) * step, _d))
+    return blk[29:].tolist()
   depth_est = renderer.render_object(obj_id, R_est, t_est, fx, fy, cx, cy)["depth"]
   depth_gt = renderer.render_object(obj_id, R_gt, t_gt, fx, fy, cx, cy)["depth"]
   de = np.ascontiguousarray(depth_est, np.float32)
