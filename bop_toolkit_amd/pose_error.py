@@ -111,16 +111,22 @@ def vsd(R_est, t_est, R_gt, t_gt, depth_test, K, delta, taus, normalized_by_diam
 def _point_error(name, R_est, t_est, R_gt, t_gt, pts, syms=None, K=None):
   ctx = runtime.context()
   oid = runtime.resident_object(pts, syms)
-  ids = np.array([oid], np.int32)
-  pe = runtime.pose12(R_est, t_est)
-  pg = runtime.pose12(R_gt, t_gt)
-  out = np.empty(1, np.float64)
+  p_ids = _const(("id", oid), lambda: np.array([oid], np.int32), _i32)
+  # pose_est | pose_gt | K | result in one float64 block (see vsd)
+  blk = np.empty(34, np.float64)
+  blk[0:9] = np.asarray(R_est, np.float64).reshape(9)
+  blk[9:12] = np.asarray(t_est, np.float64).reshape(3)
+  blk[12:21] = np.asarray(R_gt, np.float64).reshape(9)
+  blk[21:24] = np.asarray(t_gt, np.float64).reshape(3)
+  base, step = blk.ctypes.data, blk.itemsize
+  p_pe, p_pg = _lib.cast_ptr(base, _d), _lib.cast_ptr(base + 12 * step, _d)
+  p_out = _lib.cast_ptr(base + 33 * step, _d)
   if K is not None:
-    Km = np.ascontiguousarray(K, np.float64).reshape(9)
-    ctx.call(name, 1, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(Km, _d), ptr(out, _d))
+    blk[24:33] = np.asarray(K, np.float64).reshape(9)
+    ctx.call(name, 1, p_ids, p_pe, p_pg, _lib.cast_ptr(base + 24 * step, _d), p_out)
   else:
-    ctx.call(name, 1, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(out, _d))
-  return np.float64(out[0])
+    ctx.call(name, 1, p_ids, p_pe, p_pg, p_out)
+  return np.float64(blk[33])
 
 
 def mssd(R_est, t_est, R_gt, t_gt, pts, syms):
