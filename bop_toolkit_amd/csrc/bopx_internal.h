@@ -100,7 +100,10 @@ struct VsdArgs {
   // s walking ROI tiles s, s + split, ...; each writes one row of kVsdPartCols
   // doubles to `part` and k_vsd_combine reduces the rows in split order. Set by
   // launch_vsd (small batches, BOPX_VSD_SPLIT), 1 = one workgroup per tuple.
+  // Tuples [0, split_from) of the launch order take one workgroup each, the
+  // rest `split` each (0 for small batches; the tail of a large one otherwise).
   int split;
+  int64_t split_from;
   double* part;
   double taus[kMaxTaus];
 };

@@ -529,10 +529,14 @@ void k_vsd(VsdArgs a) {
   uint32_t(*s_cnt)[2 + kMaxTaus] = reinterpret_cast<uint32_t(*)[2 + kMaxTaus]>(&s_dep[0][0]);
   double(*s_lin)[kMaxTaus] = reinterpret_cast<double(*)[kMaxTaus]>(&s_dep[1][0]);
 
-  // tile-parallel mode: workgroup (tuple k, split sp) of a.split per tuple
-  const int S = a.split;
-  const int64_t kb = S > 1 ? (int64_t)(blockIdx.x / (unsigned)S) : (int64_t)blockIdx.x;
-  const int sp = S > 1 ? (int)(blockIdx.x - kb * S) : 0;
+  // tile-parallel mode: workgroup (tuple kb, split sp); tuples from
+  // a.split_from on take a.split workgroups each, earlier ones one (S = 1)
+  const int64_t n0 = a.split_from;
+  const bool tail = a.split > 1 && (int64_t)blockIdx.x >= n0;
+  const int S = tail ? a.split : 1;
+  const int64_t j = tail ? ((int64_t)blockIdx.x - n0) / S : 0;  // split-tuple index
+  const int64_t kb = tail ? n0 + j : (int64_t)blockIdx.x;
+  const int sp = tail ? (int)((int64_t)blockIdx.x - n0 - j * S) : 0;
   const int64_t b = a.order ? (int64_t)a.order[kb] : kb;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
@@ -1436,7 +1440,7 @@ void k_vsd(VsdArgs a) {
     if constexpr (COST == kCostCover || COST == kCostGtInfo) {
       // cover: union, inter, 8 bbox values; GT info: all, visib, 8 bbox values, valid
       // tile-parallel mode: the same columns as a partial row (k_vsd_combine)
-      double* out = S > 1 ? a.part + ((int64_t)b * S + sp) * kVsdPartCols
+      double* out = S > 1 ? a.part + (j * S + sp) * kVsdPartCols
                           : a.out + b * (int64_t)(COST == kCostCover ? kCoverCols : kGtInfoCols);
       out[0] = (double)un;
       out[1] = (double)in;
@@ -1456,7 +1460,7 @@ void k_vsd(VsdArgs a) {
       return;
     }
     if (S > 1) {  // partial row of this split; k_vsd_combine applies the formula
-      double* row = a.part + ((int64_t)b * S + sp) * kVsdPartCols;
+      double* row = a.part + (j * S + sp) * kVsdPartCols;
       row[0] = (double)un;
       row[1] = (double)in;
       for (int k = 0; k < a.n_tau; ++k) {
@@ -1507,10 +1511,12 @@ constexpr int kBopTaus = 10;  // eval_calc_errors.py:47, np.arange(0.05, 0.51, 0
 // a fixed order) and applies pose_error.py:85-91 like the one-workgroup path.
 constexpr int kCombineThreads = 256;
 __global__ __launch_bounds__(kCombineThreads) void k_vsd_combine(
-    int S, int n_tau, int cost_type, const double* __restrict__ part, double* __restrict__ out) {
+    int S, int n_tau, int cost_type, const double* __restrict__ part, double* __restrict__ out,
+    const int32_t* __restrict__ order, int64_t n0) {
   __shared__ double s_row[kVsdMaxSplit * kVsdPartCols];
-  const int64_t b = blockIdx.x;
-  const double* row = part + b * S * kVsdPartCols;
+  const int64_t j = blockIdx.x, kb = n0 + j;  // split tuple j of the launch order
+  const int64_t b = order ? (int64_t)order[kb] : kb;
+  const double* row = part + j * S * kVsdPartCols;
   for (int i = threadIdx.x; i < S * kVsdPartCols; i += kCombineThreads) s_row[i] = row[i];
   __syncthreads();
   const int k = threadIdx.x;
@@ -1550,20 +1556,33 @@ __global__ __launch_bounds__(kCombineThreads) void k_vsd_combine(
 // bench: 9.38 / 10.0 / 11.4 ms for k_vsd).
 constexpr int64_t kVsdSplitTarget = 1024;
 constexpr int64_t kVsdSplitBelow = 1024;
-static int vsd_split(int64_t n, int cost_type) {
+// Large batches: the last BOPX_VSD_TAIL tuples of the launch order (the
+// cheapest under the cost-class order) take kVsdTailSplit workgroups each, so
+// the launch's tail drains in smaller pieces.
+constexpr int kVsdTailSplit = 4;
+static int vsd_split(int64_t n, int cost_type, int64_t& split_from) {
   static const int force = [] {
     const char* e = getenv("BOPX_VSD_SPLIT");
     return e ? atoi(e) : 0;
   }();
+  static const int64_t tail = [] {
+    const char* e = getenv("BOPX_VSD_TAIL");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  split_from = 0;
   if (force > 0) return force < kVsdMaxSplit ? force : kVsdMaxSplit;
-  if (n >= kVsdSplitBelow) return 1;
+  if (n >= kVsdSplitBelow) {
+    if (tail <= 0) return 1;
+    split_from = tail < n ? n - tail : 0;
+    return kVsdTailSplit;
+  }
   const int64_t s = kVsdSplitTarget / n;
   return (int)(s < 4 ? 4 : s > kVsdMaxSplit ? kVsdMaxSplit : s);
 }
 
 template <int RPT>
 static void launch_vsd_rpt(const VsdArgs& a, int cost_type, hipStream_t s) {
-  dim3 grid((unsigned)(a.n * a.split)), block(kVsdThreads);
+  dim3 grid((unsigned)(a.split_from + (a.n - a.split_from) * a.split)), block(kVsdThreads);
 #if BOPX_VSD_DIAG
   // occupancy experiment (diag builds): unused dynamic LDS per workgroup
   static const unsigned dyn = [] {
@@ -1588,16 +1607,18 @@ static void launch_vsd_rpt(const VsdArgs& a, int cost_type, hipStream_t s) {
 hipError_t launch_vsd(const VsdArgs& a_in, int cost_type, hipStream_t s) {
   if (a_in.n <= 0) return hipSuccess;
   VsdArgs a = a_in;
-  a.split = vsd_split(a.n, cost_type);
+  a.split = vsd_split(a.n, cost_type, a.split_from);
   a.part = nullptr;
   if (a.split > 1) {
     // stream-ordered scratch, freed behind the combine pass; without it the
     // launch keeps one workgroup per tuple
-    const size_t bytes = (size_t)a.n * a.split * kVsdPartCols * sizeof(double);
+    const size_t bytes =
+        (size_t)(a.n - a.split_from) * a.split * kVsdPartCols * sizeof(double);
     if (hipMallocAsync((void**)&a.part, bytes, s) != hipSuccess) {
       (void)hipGetLastError();
       a.part = nullptr;
       a.split = 1;
+      a.split_from = 0;
     }
   }
   const int need = 2 * a.max_nm;
@@ -1612,8 +1633,9 @@ hipError_t launch_vsd(const VsdArgs& a_in, int cost_type, hipStream_t s) {
   if (a.split > 1) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_vsd_combine, dim3((unsigned)a.n), dim3(kCombineThreads), 0, s, a.split,
-                       a.n_tau, cost_type, (const double*)a.part, a.out);
+    hipLaunchKernelGGL(k_vsd_combine, dim3((unsigned)(a.n - a.split_from)), dim3(kCombineThreads),
+                       0, s, a.split, a.n_tau, cost_type, (const double*)a.part, a.out, a.order,
+                       a.split_from);
     e = hipGetLastError();
     const hipError_t f = hipFreeAsync(a.part, s);
     return e != hipSuccess ? e : f;
