@@ -591,11 +591,16 @@ __global__ __launch_bounds__(kPoseThreads) void k_adi(const ObjDesc* __restrict_
                                                       double* __restrict__ out,
                                                       const int32_t* __restrict__ order,
                                                       int nsplit, int64_t stride,
-                                                      double* __restrict__ best2) {
+                                                      double* __restrict__ best2, int nq) {
   __shared__ double s_e[3][kAdiTile];
   __shared__ double s_part[kPoseThreads / 64];
-  const int64_t u = SPLIT ? (int64_t)blockIdx.x / nsplit : (int64_t)blockIdx.x;
-  const int part = SPLIT ? (int)(blockIdx.x % (unsigned)nsplit) : 0;
+  // SPLIT: workgroup (tuple u, estimate-point range part, query chunk class qc);
+  // query chunks qc, qc + nq, ... (nq > 1 only for batches too small to fill
+  // the chip with point ranges alone)
+  const int64_t cell = SPLIT ? (int64_t)blockIdx.x / nq : (int64_t)blockIdx.x;
+  const int qc = SPLIT ? (int)((int64_t)blockIdx.x - cell * nq) : 0;
+  const int64_t u = SPLIT ? cell / nsplit : (int64_t)blockIdx.x;
+  const int part = SPLIT ? (int)(cell % nsplit) : 0;
   const int64_t b = order ? (int64_t)order[u] : u;
   const int tid = threadIdx.x;
   const ObjDesc o = objs[slots[b]];
@@ -626,7 +631,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_adi(const ObjDesc* __restrict_
   const double* __restrict__ py = o.pts + nv;
   const double* __restrict__ pz = o.pts + 2 * (int64_t)nv;
   double total = 0.0;
-  for (int q0 = 0; q0 < nv; q0 += kAdiChunk) {
+  for (int q0 = qc * kAdiChunk; q0 < nv; q0 += (SPLIT ? nq : 1) * kAdiChunk) {
     double qx[kAdiQ], qy[kAdiQ], qz[kAdiQ], best[kAdiQ];
 #pragma unroll
     for (int q = 0; q < kAdiQ; ++q) {
@@ -751,12 +756,24 @@ hipError_t launch_adi(const ObjDesc* objs, int max_nv, int64_t n, const int32_t*
                                     (max_nv + kAdiMinRange - 1) / kAdiMinRange);
   }
   nsplit = std::max(1, std::min(nsplit, std::max(max_nv, 1)));
+  // query-chunk classes per range (BOPX_ADI_QSPLIT forces): up to the query
+  // chunks of the largest object, until ~kAdiQWorkgroups workgroups
+  const char* qenv = getenv("BOPX_ADI_QSPLIT");
+  int nq = qenv ? atoi(qenv) : 0;
+  const int64_t chunks = std::max<int64_t>(1, (max_nv + kAdiChunk - 1) / kAdiChunk);
+  if (nq <= 0) {
+    constexpr int64_t kAdiQWorkgroups = 1024;
+    nq = (int)std::min<int64_t>(chunks, (kAdiQWorkgroups + n * nsplit - 1) / (n * nsplit));
+  }
+  nq = (int)std::max<int64_t>(1, std::min<int64_t>(nq, chunks));
   // the per-query scratch is n x max_nv doubles: only for small batches
   const int64_t stride = max_nv;
-  if (nsplit > 1 && (n * nsplit > 0x7FFFFFFF || n * stride > ((int64_t)1 << 26))) nsplit = 1;
-  if (nsplit == 1) {
+  if (nsplit * (int64_t)nq > 1 &&
+      (n * nsplit * nq > 0x7FFFFFFF || n * stride > ((int64_t)1 << 26)))
+    nsplit = nq = 1;
+  if (nsplit == 1 && nq == 1) {  // (a query split alone still takes the SPLIT path)
     hipLaunchKernelGGL(k_adi<false>, dim3((unsigned)n), dim3(kPoseThreads), 0, s, objs, slots,
-                       pe, pg, out, order, 1, (int64_t)0, (double*)nullptr);
+                       pe, pg, out, order, 1, (int64_t)0, (double*)nullptr, 1);
     return hipGetLastError();
   }
   double* best2 = nullptr;
@@ -764,14 +781,14 @@ hipError_t launch_adi(const ObjDesc* objs, int max_nv, int64_t n, const int32_t*
   if (e != hipSuccess) {  // no room for the scratch: one workgroup per tuple (same result)
     (void)hipGetLastError();
     hipLaunchKernelGGL(k_adi<false>, dim3((unsigned)n), dim3(kPoseThreads), 0, s, objs, slots,
-                       pe, pg, out, order, 1, (int64_t)0, (double*)nullptr);
+                       pe, pg, out, order, 1, (int64_t)0, (double*)nullptr, 1);
     return hipGetLastError();
   }
   // 0xFF bytes: above the bits of every non-negative double (the +inf start)
   e = hipMemsetAsync(best2, 0xFF, (size_t)(n * stride) * sizeof(double), s);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_adi<true>, dim3((unsigned)(n * nsplit)), dim3(kPoseThreads), 0, s, objs,
-                       slots, pe, pg, out, order, nsplit, stride, best2);
+    hipLaunchKernelGGL(k_adi<true>, dim3((unsigned)(n * nsplit * nq)), dim3(kPoseThreads), 0, s,
+                       objs, slots, pe, pg, out, order, nsplit, stride, best2, nq);
     hipLaunchKernelGGL(k_adi_finish, dim3((unsigned)n), dim3(kPoseThreads), 0, s, objs, slots,
                        stride, (const double*)best2, out);
     e = hipGetLastError();

@@ -802,16 +802,20 @@ def test_adi_split_bit_identical(monkeypatch):
   pe = np.concatenate([Re.reshape(n, 9), te], 1)
   pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
   outs = {}
-  for split in ("1", "2", "3", "7", "64", "100000", None):
-    if split is None:
-      monkeypatch.delenv("BOPX_ADI_SPLIT", raising=False)
-    else:
-      monkeypatch.setenv("BOPX_ADI_SPLIT", split)
-    outs[split] = _batch(c, "bopx_adi_batch", ids, pe, pg)
-  for split, o in outs.items():
-    assert np.array_equal(o.view(np.uint64), outs["1"].view(np.uint64)), split
+  # (point ranges, query-chunk classes) per tuple; ("1", "1") = one workgroup
+  for split, qsplit in (("1", "1"), ("2", "1"), ("3", "1"), ("7", "1"), ("64", "1"),
+                        ("100000", "1"), ("1", "2"), ("3", "5"), ("7", "1000"), ("1", None),
+                        (None, None)):
+    for var, v in (("BOPX_ADI_SPLIT", split), ("BOPX_ADI_QSPLIT", qsplit)):
+      if v is None:
+        monkeypatch.delenv(var, raising=False)
+      else:
+        monkeypatch.setenv(var, v)
+    outs[(split, qsplit)] = _batch(c, "bopx_adi_batch", ids, pe, pg)
+  for key, o in outs.items():
+    assert np.array_equal(o.view(np.uint64), outs[("1", "1")].view(np.uint64)), key
   want = np.array([oracle.adi(objs[int(ids[i])], pe[i], pg[i]) for i in range(n)])
-  assert np.max(np.abs(outs[None] - want) / np.maximum(1.0, np.abs(want))) < 1e-9
+  assert np.max(np.abs(outs[(None, None)] - want) / np.maximum(1.0, np.abs(want))) < 1e-9
 
 
 def test_auto_backface_cull_all_modes(oracle_mod, monkeypatch):
