@@ -768,12 +768,22 @@ static int point_batch(bopx_ctx* c, int kind, int64_t n, const int32_t* obj_ids,
   double* d_pe = cv.take<double>(12 * n);
   double* d_pg = cv.take<double>(12 * n);
   double* d_K = needK ? cv.take<double>(9 * n) : nullptr;
+  const size_t small = cv.off;
   double* d_out = cv.take<double>(n);
   hipStream_t s = c->stream;
-  HIPCHK(c, hipMemcpyAsync(d_s, slots.data(), 4 * n, hipMemcpyHostToDevice, s));
-  HIPCHK(c, hipMemcpyAsync(d_pe, pe, 96 * n, hipMemcpyHostToDevice, s));
-  HIPCHK(c, hipMemcpyAsync(d_pg, pg, 96 * n, hipMemcpyHostToDevice, s));
-  if (needK) HIPCHK(c, hipMemcpyAsync(d_K, K, 72 * n, hipMemcpyHostToDevice, s));
+  // small batches (per-call latency): inputs staged in one host block, one
+  // upload; large ones copy each array directly (no extra host pass)
+  std::vector<char> h(n <= 4096 ? small : 0);
+  const auto stage = [&](void* d, const void* src, size_t nb) -> hipError_t {
+    if (h.empty()) return hipMemcpyAsync(d, src, nb, hipMemcpyHostToDevice, s);
+    std::memcpy(h.data() + ((const char*)d - (const char*)c->ws.p), src, nb);
+    return hipSuccess;
+  };
+  HIPCHK(c, stage(d_s, slots.data(), 4 * n));
+  HIPCHK(c, stage(d_pe, pe, 96 * n));
+  HIPCHK(c, stage(d_pg, pg, 96 * n));
+  if (needK) HIPCHK(c, stage(d_K, K, 72 * n));
+  if (!h.empty()) HIPCHK(c, hipMemcpyAsync(c->ws.p, h.data(), small, hipMemcpyHostToDevice, s));
   LaunchOrder ord;
   const bopx::OrderCost sc = sym_order_cost(c);
   if (int r = make_order(c, n, d_s, s, ord, kind <= 1 ? &sc : nullptr)) return r;
