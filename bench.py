@@ -2,16 +2,17 @@
 """BOP19 pose-error throughput on MI355X: VSD (10 taus) + MSSD + MSPD tuples/s.
 
 One step = the full BOP19 error set of every (est, gt) tuple of a synthetic
-batch (BASELINE.json configs[3], per-GPU shard): 21 LM-O/YCB-V-like objects
-(5,002 verts / 10,000 faces, S in {1,2,4,8} + one continuous-symmetry object
-with S = 314), 640x480 test depth, YCB-V intrinsics, 6 objects per image,
-12,500 tuples per GPU by default (100k tuples over 8 GPUs = configs[3]).
-Inputs are resident in HBM before timing; each step runs k_vsd (both renders
-+ VSD fused), k_sym_error<MSSD> and k_sym_error<MSPD>, and for N > 1 an RCCL
-all-gather of the per-tuple error rows. Weak scaling: each rank owns a fixed
-shard of images (tuples are independent).
+job (BASELINE.json configs[3]): 21 LM-O/YCB-V-like objects (5,002 verts /
+10,000 faces, S in {1,2,4,8} + one continuous-symmetry object with S = 314),
+640x480 test depth, YCB-V intrinsics, 6 objects per image, 100,002 tuples
+(16,667 images) in total. Inputs are resident in HBM before timing; each step
+runs k_vsd (both renders + VSD fused), k_sym_error<MSSD> and
+k_sym_error<MSPD>, and for N > 1 one RCCL gather of the per-tuple error rows
+to rank 0. Strong scaling: the configuration's tuple count is fixed and its
+images are split over the ranks by LPT on the SURVEY.md §8d cost model
+(shard.lpt_shard; tuples are independent).
 
-    python bench.py [--gpus N --steps K --warmup W --tuples T]
+    python bench.py [--gpus N --steps K --warmup W --config C --tuples T]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -35,25 +36,26 @@ FP64_PEAK_TF = 78.6
 FP32_PEAK_TF = 157.3
 
 
-# BASELINE.json configs (index): per-GPU shard of the workload each names.
-# Default: configs[3], the metric's configuration (BOP19 set, 100k est / 8 GPUs).
+# BASELINE.json configs (index): the whole job each names (tuples in total,
+# split over the ranks). Default: configs[3], the metric's configuration
+# (BOP19 set, 100k est).
 CONFIGS = {
     0: {"objects": 1, "n_lat": 25, "n_lon": 40, "syms": [1], "continuous": False,
         "tuples": 100, "K": "LMO_K", "W": 640, "H": 480, "errors": ("add", "adi"),
         "what": "configs[0]: ADD/ADI, 1 LM-O-like obj ~1k verts, 100 est/gt pairs"},
     1: {"objects": 8, "n_lat": 50, "n_lon": 100, "syms": [1, 2, 4, 8], "continuous": False,
         "tuples": 10000, "K": "LMO_K", "W": 640, "H": 480, "errors": ("mssd", "mspd"),
-        "what": "configs[1]: MSSD+MSPD, 8 LM-O-like objs, S<=8, 10k est/GPU"},
+        "what": "configs[1]: MSSD+MSPD, 8 LM-O-like objs, S<=8, 10k est"},
     2: {"objects": 21, "n_lat": 50, "n_lon": 100, "syms": [1, 2, 4, 8], "continuous": True,
         "tuples": 50000, "K": "YCBV_K", "W": 640, "H": 480, "errors": ("vsd",),
-        "what": "configs[2]: VSD (10 taus) with HIP raster, 21 YCB-V-like objs, 50k est/GPU"},
+        "what": "configs[2]: VSD (10 taus) with HIP raster, 21 YCB-V-like objs, 50k est"},
     3: {"objects": 21, "n_lat": 50, "n_lon": 100, "syms": [1, 2, 4, 8], "continuous": True,
-        "tuples": 12500, "K": "YCBV_K", "W": 640, "H": 480, "errors": ("vsd", "mssd", "mspd"),
-        "what": "BASELINE configs[3] per-GPU shard: BOP19 error set (VSD 10 taus + MSSD + MSPD)"},
+        "tuples": 100000, "K": "YCBV_K", "W": 640, "H": 480, "errors": ("vsd", "mssd", "mspd"),
+        "what": "BASELINE configs[3]: BOP19 error set (VSD 10 taus + MSSD + MSPD), 100k est"},
     4: {"objects": 30, "n_lat": 100, "n_lon": 150, "syms": [1, 2, 4, 8, 16, 32, 64],
-        "continuous": False, "tuples": 25000, "K": "TLESS_K", "W": 720, "H": 540,
+        "continuous": False, "tuples": 200000, "K": "TLESS_K", "W": 720, "H": 540,
         "errors": ("vsd", "mssd", "mspd"),
-        "what": "configs[4] per-GPU shard: T-LESS-like BOP19 set, ~15k verts, S<=64"},
+        "what": "configs[4]: T-LESS-like BOP19 set, ~15k verts, S<=64, 200k est"},
 }
 
 
@@ -64,7 +66,8 @@ def parse():
   ap.add_argument("--warmup", type=int, default=2)
   ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS),
                   help="BASELINE.json configs index (3 = the metric's workload)")
-  ap.add_argument("--tuples", type=int, default=None, help="tuples per GPU")
+  ap.add_argument("--tuples", type=int, default=None,
+                  help="tuples of the whole job (split over the ranks)")
   ap.add_argument("--objects", type=int, default=None)
   ap.add_argument("--n-lat", type=int, default=None)
   ap.add_argument("--n-lon", type=int, default=None)
@@ -114,97 +117,78 @@ def build_objects(ev, args, torch):
   return objs
 
 
-def build_workload(ev, objs, args, rank, torch):
-  """Images with 6 objects each; test depth = composite GT render + background
-  plane + occluder + noise + 10 % holes, rounded to integer mm (uint16 PNG)."""
-  from bop_toolkit_amd import synth
-  rng = np.random.default_rng(args.seed + 1000 * (rank + 1))
+def build_workload(ev, objs, args, rank, world, torch):
+  """The whole job's images (6 objects each), identical for every N, and this
+  rank's LPT shard of them. Test depth = composite GT render + background
+  plane + occluder + noise + 10 % holes, rounded to integer mm (uint16 PNG),
+  synthesised on the GPU in chunks of images (bounded temporaries)."""
+  from bop_toolkit_amd import shard, synth
+  rng = np.random.default_rng(args.seed + 1000)
   per_img = min(6, len(objs))
-  n_img = (args.tuples + per_img - 1) // per_img
-  n = n_img * per_img
-  obj = np.stack([rng.choice(len(objs), per_img, replace=False) for _ in range(n_img)]).reshape(-1)
-  obj = obj.astype(np.int32)
-  Rg, tg = synth.gt_poses(rng, n)
+  n_img_all = (args.tuples + per_img - 1) // per_img
+  n_all = n_img_all * per_img
+  obj_all = np.stack([rng.choice(len(objs), per_img, replace=False)
+                      for _ in range(n_img_all)]).reshape(-1).astype(np.int32)
+  Rg, tg = synth.gt_poses(rng, n_all)
   Re, te = synth.perturb(rng, Rg, tg)
-  pe = np.concatenate([Re.reshape(n, 9), te], 1)
-  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
-  frame_idx = np.repeat(np.arange(n_img, dtype=np.int32), per_img)
+  pe_all = np.concatenate([Re.reshape(n_all, 9), te], 1)
+  pg_all = np.concatenate([Rg.reshape(n_all, 9), tg], 1)
   K = getattr(synth, args.cfg["K"])
+  if world > 1:
+    # LPT over images on the SURVEY §8d per-tuple cost (shard.tuple_cost)
+    roi = roi_pixels(objs, obj_all, [pe_all, pg_all], K)
+    nv = np.array([len(objs[o]["pts"]) for o in obj_all])
+    nf = np.array([len(objs[o]["faces"]) for o in obj_all])
+    ns = np.array([len(objs[o]["syms"]) for o in obj_all])
+    cost = shard.image_costs(np.repeat(np.arange(n_img_all), per_img),
+                             shard.tuple_cost(nv, nf, ns, roi), n_img_all)
+    parts = shard.lpt_shard(cost, world)
+  else:
+    parts = [np.arange(n_img_all)]
+  mine = parts[rank]
+  counts = [len(p) * per_img for p in parts]
+  gid = (mine[:, None] * per_img + np.arange(per_img)).reshape(-1)
+  n_img, n = len(mine), len(gid)
+  obj, pe, pg = obj_all[gid], pe_all[gid], pg_all[gid]
+  frame_idx = np.repeat(np.arange(n_img, dtype=np.int32), per_img)
   cam = np.tile([K[0, 0], K[1, 1], K[0, 2], K[1, 2]], (n_img, 1)).astype(np.float64)
   dev = ev.device
   t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
   d = {"slots": ev.slots(obj), "pose_est": t(pe, torch.float64), "pose_gt": t(pg, torch.float64),
        "frame_idx": t(frame_idx, torch.int32), "cam": t(cam, torch.float64),
        "K": t(np.tile(K.reshape(9), (n, 1)), torch.float64),
-       "diameters": t([objs[o]["diameter"] for o in obj], torch.float64)}
+       "diameters": t([objs[o]["diameter"] for o in obj], torch.float64),
+       "gid": t(gid, torch.int64), "counts": counts, "n_total": n_all}
   frames = ev.render(d["slots"], d["pose_gt"], d["frame_idx"], d["cam"], n_img, W, H)
   g = torch.Generator(device=dev)
   g.manual_seed(args.seed + rank)
-  frames = torch.where(frames > 0, frames, torch.full_like(frames, 1600.0))
-  # one occluder rectangle per image in front of the scene
   ys = torch.arange(H, device=dev).view(1, H, 1)
   xs = torch.arange(W, device=dev).view(1, 1, W)
-  x0 = torch.randint(0, W - 120, (n_img, 1, 1), device=dev, generator=g)
-  y0 = torch.randint(0, H - 120, (n_img, 1, 1), device=dev, generator=g)
-  sz = torch.randint(40, 120, (n_img, 1, 1), device=dev, generator=g)
-  occ = (xs >= x0) & (xs < x0 + sz) & (ys >= y0) & (ys < y0 + sz)
-  frames = torch.where(occ, torch.full_like(frames, 450.0), frames)
-  frames = frames + 2.0 * torch.randn(frames.shape, device=dev, generator=g)
-  frames = torch.round(frames).clamp_(0, 65535)
-  frames[torch.rand(frames.shape, device=dev, generator=g) < 0.1] = 0.0
-  d["frames"] = frames.contiguous()
+  for c0 in range(0, n_img, 2048):
+    f = frames[c0:c0 + 2048]
+    m = f.shape[0]
+    f[f <= 0] = 1600.0  # background plane
+    # one occluder rectangle per image in front of the scene
+    x0 = torch.randint(0, W - 120, (m, 1, 1), device=dev, generator=g)
+    y0 = torch.randint(0, H - 120, (m, 1, 1), device=dev, generator=g)
+    sz = torch.randint(40, 120, (m, 1, 1), device=dev, generator=g)
+    occ = (xs >= x0) & (xs < x0 + sz) & (ys >= y0) & (ys < y0 + sz)
+    f.masked_fill_(occ, 450.0)
+    f.add_(torch.randn(f.shape, device=dev, generator=g), alpha=2.0)
+    f.round_().clamp_(0, 65535)
+    f.masked_fill_(torch.rand(f.shape, device=dev, generator=g) < 0.1, 0.0)
+  d["frames"] = frames
   d["host"] = {"obj": obj, "pe": pe, "pg": pg, "frame_idx": frame_idx, "cam": cam}
-  perm = os.environ.get("BOPX_BENCH_PERM")  # launch-order experiments (DESIGN.md §5)
-  if perm:
-    cost = (np.array([objs[o]["diameter"] for o in obj]) / pg[:, 11]) ** 2
-    if perm == "lpt":
-      idx = np.argsort(-cost, kind="stable")
-    elif perm.startswith("lptobj"):
-      nb = int(perm[6:] or 4)
-      q = np.quantile(cost, np.linspace(0, 1, nb + 1)[1:-1])
-      bucket = nb - 1 - np.searchsorted(q, cost)
-      idx = np.lexsort((obj, bucket))
-    else:
-      idx = np.arange(n)
-    it = torch.as_tensor(idx, device=dev)
-    for k in ("slots", "pose_est", "pose_gt", "frame_idx", "K", "diameters"):
-      d[k] = d[k][it].contiguous()
-    d["host"] = {"obj": obj[idx], "pe": pe[idx], "pg": pg[idx], "frame_idx": frame_idx[idx],
-                 "cam": cam}
   torch.cuda.synchronize()
   return n, d
 
 
 def roi_pixels(objs, obj, poses, K):
-  """Survey §8d ROI: union over both poses of the clipped screen bbox of the
-  projected 8 model-bbox corners (whole image if a corner is behind the camera)."""
-  n = len(obj)
+  """Survey §8d ROI per tuple (shard.roi_pixels)."""
+  from bop_toolkit_amd import shard
   lo = np.stack([objs[o]["bbox"][0] for o in obj])
   hi = np.stack([objs[o]["bbox"][1] for o in obj])
-  corners = np.stack([np.where(np.array([(k >> a) & 1 for a in range(3)]) == 1, hi, lo)
-                      for k in range(8)], 1)  # n x 8 x 3
-  x0 = np.full(n, np.inf)
-  y0 = np.full(n, np.inf)
-  x1 = np.full(n, -np.inf)
-  y1 = np.full(n, -np.inf)
-  full = np.zeros(n, bool)
-  for p in poses:
-    R = p[:, :9].reshape(n, 3, 3)
-    t = p[:, 9:]
-    X = np.einsum("nij,nkj->nki", R, corners) + t[:, None, :]
-    full |= (X[..., 2] <= 0).any(1)
-    Z = np.where(X[..., 2] > 0, X[..., 2], 1.0)
-    u = K[0, 0] * X[..., 0] / Z + K[0, 2]
-    v = K[1, 1] * X[..., 1] / Z + K[1, 2]
-    x0 = np.minimum(x0, u.min(1))
-    x1 = np.maximum(x1, u.max(1))
-    y0 = np.minimum(y0, v.min(1))
-    y1 = np.maximum(y1, v.max(1))
-  w = np.clip(np.floor(x1), -1, W - 1) - np.clip(np.ceil(x0), 0, W) + 1
-  h = np.clip(np.floor(y1), -1, H - 1) - np.clip(np.ceil(y0), 0, H) + 1
-  area = np.maximum(w, 0) * np.maximum(h, 0)
-  area[full] = W * H
-  return area
+  return shard.roi_pixels(lo, hi, poses, K, W, H)
 
 
 def algorithmic_cost(objs, host, n, K):
@@ -232,17 +216,39 @@ def algorithmic_cost(objs, host, n, K):
           "mspd": (mspd_bytes, 0.0, mspd_f64), "roi_mean": float(roi.mean())}
 
 
-def load_traffic():
-  """HBM bytes per k_vsd launch from the committed rocprofv3 PMC summary
-  (profiles/*_pmc.json, written by tools/pmc_summary.py), or None."""
+def lib_digest():
+  """sha256 of the loaded libbopx.so: ties a PMC summary to the build it measured."""
+  import hashlib
+  from bop_toolkit_amd import _lib
+  with open(_lib.LIB_PATH, "rb") as f:
+    return hashlib.sha256(f.read()).hexdigest()
+
+
+def workload_key(args, n):
+  return "config=%d tuples=%d objects=%d n_lat=%d n_lon=%d axes_scale=%g seed=%d" % (
+      args.config, n, args.objects, args.n_lat, args.n_lon, args.axes_scale, args.seed)
+
+
+def load_traffic(dom, args, n):
+  """HBM bytes per launch of kernel `dom` from the committed rocprofv3 PMC
+  summaries (profiles/*_pmc.json, written by tools/pmc_summary.py), or None.
+  A summary counts only if it records this library build (`lib_sha256`) and
+  this launch's workload (`workload`): otherwise it measured something else."""
   import glob
+  name = {"vsd": "k_vsd", "mssd": "k_sym_error<MSSD>", "mspd": "k_sym_error<MSPD>"}.get(dom)
+  if name is None:
+    return None
+  digest, key = lib_digest(), workload_key(args, n)
   best = None
   for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json"))):
     try:
       with open(path) as f:
-        best = json.load(f).get("k_vsd", {}).get("hbm_bytes_per_launch")
+        j = json.load(f)
     except (OSError, ValueError):
-      pass
+      continue
+    meta = j.get("_meta", {})
+    if meta.get("lib_sha256") == digest and meta.get("workload") == key:
+      best = j.get(name, {}).get("hbm_bytes_per_launch", best)
   return best
 
 
@@ -313,13 +319,17 @@ def main():
   from bop_toolkit_amd.batch import BatchEvaluator
   ev = BatchEvaluator(local)
   objs = build_objects(ev, args, torch)
-  n, d = build_workload(ev, objs, args, rank, torch)
+  n, d = build_workload(ev, objs, args, rank, world, torch)
+  meta = os.environ.get("BOPX_BENCH_META")  # tools/pmc.sh: what the counters measured
+  if meta and rank == 0:
+    with open(meta, "w") as f:
+      json.dump({"lib_sha256": lib_digest(), "workload": workload_key(args, n)}, f)
 
   out_vsd = torch.empty((n, N_TAU), dtype=torch.float64, device=ev.device)
   out_mssd = torch.empty(n, dtype=torch.float64, device=ev.device)
   out_mspd = torch.empty(n, dtype=torch.float64, device=ev.device)
   rows = torch.empty((n, N_TAU + 2), dtype=torch.float64, device=ev.device)
-  gids = torch.arange(rank * n, (rank + 1) * n, dtype=torch.int64, device=ev.device)
+  gids = d["gid"]
   ktime = {k: 0.0 for k in args.cfg["errors"]}
   marks = []  # per timed step: HIP events bracketing each kernel on the launch stream
 
@@ -358,9 +368,9 @@ def main():
       rows[:, N_TAU + 1] = out_mspd
       # per-tuple error rows -> rank 0, ordered by global tuple id (RCCL)
       if backend == "nccl":
-        shard.gather_rows(rows, gids, world * n, counts=[n] * world)
+        shard.gather_rows(rows, gids, d["n_total"], counts=d["counts"])
       else:
-        shard.gather_rows(rows.cpu(), gids.cpu(), world * n, counts=[n] * world)
+        shard.gather_rows(rows.cpu(), gids.cpu(), d["n_total"], counts=d["counts"])
 
   for _ in range(args.warmup):
     step(False)
@@ -387,7 +397,7 @@ def main():
 
   if rank == 0:
     steps = args.steps
-    total = n * world * steps
+    total = d["n_total"] * steps
     from bop_toolkit_amd import synth
     cost = algorithmic_cost(objs, d["host"], n, getattr(synth, args.cfg["K"]))
     kt = {k: v / steps for k, v in ktime.items()}
@@ -408,9 +418,9 @@ def main():
       b, f32, f64 = cost[dom]
       ach = b / kt[dom] / 1e9
       t_valu = f64 / (FP64_PEAK_TF * 1e12) + f32 / (FP32_PEAK_TF * 1e12)
-      # PMC bytes were collected on the default configs[3] shard (tools/pmc.sh)
-      traffic = load_traffic() if (dom == "vsd" and args.config == 3 and
-                                   args.tuples == CONFIGS[3]["tuples"]) else None
+      # PMC bytes per launch, only from a summary of this library build on this
+      # launch's workload (tools/pmc.sh records both), else null
+      traffic = load_traffic(dom, args, n) if world == 1 else None
       roof = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
               "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": traffic,
               "kernel": {"vsd": "k_vsd", "mssd": "k_sym_error<MSSD>", "mspd": "k_sym_error<MSPD>",
@@ -429,14 +439,16 @@ def main():
             round(len(objs[0]["pts"]) / 1000)),
         "value": total / elapsed, "unit": "tuples/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": elapsed / steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64+f32", "data": "synthetic",
-        "config": {"workload": "%s, %d objs V=%d F=%d S in {%s}, %dx%d %s, %d tuples/GPU" % (
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64+f32", "data": "synthetic",
+        "config": {"workload": "%s, %d objs V=%d F=%d S in {%s}, %dx%d %s, %d tuples" % (
                                    args.cfg["what"], args.objects, len(objs[0]["pts"]),
                                    len(objs[0]["faces"]),
                                    ",".join(map(str, sorted(set(
                                        len(o["syms"]) for o in objs)))), W, H,
-                                   args.cfg["K"].split("_")[0], n),
-                   "global_batch": n * world, "parallelism": "image-sharded x%d" % world,
+                                   args.cfg["K"].split("_")[0], d["n_total"]),
+                   "global_batch": d["n_total"],
+                   "parallelism": "image-sharded x%d (LPT)" % world,
+                   "tuples_rank0": n,
                    "roi_mean_px": round(cost["roi_mean"], 1),
                    **({"axes_scale": args.axes_scale} if args.axes_scale != 1.0 else {})},
         "roofline": roof, "kernels": kernels, "cpu_baseline": cpu}

@@ -17,6 +17,7 @@ OK, E_INVALID, E_NOT_FOUND, E_HIP, E_OOM, E_UNSUPPORTED = 0, 1, 2, 3, 4, 5
 COST_STEP, COST_TLINEAR = 0, 1
 VISIB_BOP18, VISIB_BOP19 = 0, 1
 DELTA_F64 = 1
+VSD_UNIONS = 2  # BOPX_VSD_UNIONS: union pixel counts appended to the VSD output
 MAX_TAUS = 16
 
 _d = ctypes.POINTER(ctypes.c_double)

@@ -50,10 +50,12 @@ class BatchEvaluator:
     if syms is not None:
       s12 = syms if isinstance(syms, np.ndarray) else symmetries_to_array(syms)
       self.ctx.set_symmetries(obj_id, s12)
+    pts = np.asarray(pts, np.float64)
     self.objects[obj_id] = {
         "slot": self.ctx.slot(obj_id), "nv": len(pts),
         "nf": 0 if faces is None else len(faces),
-        "ns": 0 if syms is None else len(syms), "diameter": diameter}
+        "ns": 0 if syms is None else len(syms), "diameter": diameter,
+        "bbox": (pts.min(0), pts.max(0)) if len(pts) else (np.zeros(3), np.zeros(3))}
 
   def slots(self, obj_ids):
     """int32 device tensor of slots for a sequence of obj_ids."""

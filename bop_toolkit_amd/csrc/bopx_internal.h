@@ -105,6 +105,7 @@ struct VsdArgs {
   int split;
   int64_t split_from;
   double* part;
+  double* unions;  // optional (BOPX_VSD_UNIONS): per tuple visibility-union pixel count
   double taus[kMaxTaus];
 };
 constexpr int kVsdPartCols = 2 + 2 * kMaxTaus;  // union, inter, cnt[kMaxTaus], lin[kMaxTaus]

@@ -716,10 +716,11 @@ hipError_t launch_sym_error(int mode, const ObjDesc* objs, int max_ns, int64_t n
   hipLaunchKernelGGL(k_sym_init, gfix, bfix, 0, s, out, n);
   dim3 grid((unsigned)(n * nch)), block(kPoseThreads);
   // BOPX_SYM_PRUNE: units with at least this many symmetries take the pruned
-  // path (0 = never; identical results either way)
+  // path (<= 0: never, every set sweeps exhaustively chunk by chunk, including
+  // the whole-set units of up to kPruneSpan; identical results either way)
   const char* pe_env = getenv("BOPX_SYM_PRUNE");  // read per call (tests compare both paths)
   const int prune_env = pe_env ? atoi(pe_env) : BOPX_SYM_PRUNE_MIN;
-  const int prune_min = prune_env > 0 ? prune_env : kSymChunk + 1;
+  const int prune_min = prune_env > 0 ? prune_env : 0x7FFFFFFF;
   if (mode == 0)
     hipLaunchKernelGGL(k_sym_error<0>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch,
                        order, prune_min);

@@ -1476,6 +1476,7 @@ void k_vsd(VsdArgs a) {
       return;
     }
     double* out = a.out + b * (int64_t)a.n_tau;
+    if (a.unions) a.unions[b] = (double)un;
     for (int k = 0; k < a.n_tau; ++k) {
       if (un == 0) {
         out[k] = 1.0;
@@ -1512,7 +1513,7 @@ constexpr int kBopTaus = 10;  // eval_calc_errors.py:47, np.arange(0.05, 0.51, 0
 constexpr int kCombineThreads = 256;
 __global__ __launch_bounds__(kCombineThreads) void k_vsd_combine(
     int S, int n_tau, int cost_type, const double* __restrict__ part, double* __restrict__ out,
-    const int32_t* __restrict__ order, int64_t n0) {
+    const int32_t* __restrict__ order, int64_t n0, double* __restrict__ unions) {
   __shared__ double s_row[kVsdMaxSplit * kVsdPartCols];
   const int64_t j = blockIdx.x, kb = n0 + j;  // split tuple j of the launch order
   const int64_t b = order ? (int64_t)order[kb] : kb;
@@ -1542,6 +1543,7 @@ __global__ __launch_bounds__(kCombineThreads) void k_vsd_combine(
     acc += s_row[s * kVsdPartCols + col];
   }
   out[b * n_tau + k] = un == 0.0 ? 1.0 : (acc + (un - in)) / un;
+  if (unions && k == 0) unions[b] = un;
 }
 
 // Workgroups per tuple: batches of fewer than kVsdSplitBelow tuples split each
@@ -1631,12 +1633,14 @@ hipError_t launch_vsd(const VsdArgs& a_in, int cost_type, hipStream_t s) {
   else
     launch_vsd_rpt<0>(a, cost_type, s);  // rectangles recomputed per tile (any size)
   if (a.split > 1) {
+    // the scratch is freed on every path (a failed launch skips the combine)
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_vsd_combine, dim3((unsigned)(a.n - a.split_from)), dim3(kCombineThreads),
-                       0, s, a.split, a.n_tau, cost_type, (const double*)a.part, a.out, a.order,
-                       a.split_from);
-    e = hipGetLastError();
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(k_vsd_combine, dim3((unsigned)(a.n - a.split_from)),
+                         dim3(kCombineThreads), 0, s, a.split, a.n_tau, cost_type,
+                         (const double*)a.part, a.out, a.order, a.split_from, a.unions);
+      e = hipGetLastError();
+    }
     const hipError_t f = hipFreeAsync(a.part, s);
     return e != hipSuccess ? e : f;
   }

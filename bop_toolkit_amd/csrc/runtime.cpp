@@ -791,8 +791,14 @@ static int point_batch(bopx_ctx* c, int kind, int64_t n, const int32_t* obj_ids,
   if (kind <= 1)
     e = bopx::launch_sym_error(kind, c->d_desc, c->max_ns, n, d_s, d_pe, d_pg, d_K, d_out, ord.p,
                                s);
-  else if (kind == 3)
-    e = bopx::launch_adi(c->d_desc, c->max_nv, n, d_s, d_pe, d_pg, d_out, ord.p, s);
+  else if (kind == 3) {
+    // ADI scratch stride: the largest object of THIS batch (the host knows the
+    // slots), not of the context, so small-object calls do not pay for a large
+    // resident model
+    int batch_nv = 1;
+    for (int32_t sl : slots) batch_nv = std::max(batch_nv, (int)c->objs[sl].nv);
+    e = bopx::launch_adi(c->d_desc, batch_nv, n, d_s, d_pe, d_pg, d_out, ord.p, s);
+  }
   else
     e = bopx::launch_mean_error(kind == 2 ? 0 : 1, c->d_desc, n, d_s, d_pe, d_pg, d_K, d_out,
                                 ord.p, s);
@@ -976,6 +982,7 @@ int bopx_vsd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doubl
   a.cam = cam;
   a.diameters = diameters;
   a.out = out;
+  a.unions = (flags & BOPX_VSD_UNIONS) ? out + n * n_tau : nullptr;
   a.n = n;
   {
     const hipStream_t so = pick_stream(c, stream);
@@ -1012,9 +1019,10 @@ int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double*
   std::vector<int32_t> slots;
   if (int r = map_slots(c, n, obj_ids, slots, false, true)) return r;
   const size_t fbytes = (size_t)n_frames * width * height * sizeof(float);
+  const size_t n_out = (size_t)n * n_tau + ((flags & BOPX_VSD_UNIONS) ? (size_t)n : 0);
   const size_t bytes = carve_size({4 * (size_t)n, 96 * (size_t)n, 96 * (size_t)n,
                                    4 * (size_t)n, 32 * (size_t)n_frames, 8 * (size_t)n,
-                                   fbytes, 8 * (size_t)n * n_tau});
+                                   fbytes, 8 * n_out});
   if (int r = ws_reserve(c, bytes)) return r;
   // The per-tuple arrays are carved first and staged in one host block with the
   // same offsets: one small upload instead of six (per-call latency), then the
@@ -1028,7 +1036,7 @@ int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double*
   double* d_dia = cv.take<double>(n);
   const size_t small = cv.off;
   float* d_fr = cv.take<float>((size_t)n_frames * width * height);
-  double* d_out = cv.take<double>((size_t)n * n_tau);
+  double* d_out = cv.take<double>(n_out);
   std::vector<char> h(small);
   const auto stage = [&](const void* d, const void* src, size_t nb) {
     std::memcpy(h.data() + ((const char*)d - (const char*)c->ws.p), src, nb);
@@ -1052,6 +1060,7 @@ int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double*
   a.cam = d_cam;
   a.diameters = d_dia;
   a.out = d_out;
+  a.unions = (flags & BOPX_VSD_UNIONS) ? d_out + (size_t)n * n_tau : nullptr;
   a.n = n;
   {
     const hipStream_t so = s;
@@ -1061,7 +1070,7 @@ int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double*
     a.order = ord.p;
     HIPCHK(c, bopx::launch_vsd(a, cost_type, so));
   }
-  HIPCHK(c, hipMemcpyAsync(out, d_out, 8 * (size_t)n * n_tau, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipMemcpyAsync(out, d_out, 8 * n_out, hipMemcpyDeviceToHost, s));
   HIPCHK(c, hipStreamSynchronize(s));
   return BOPX_OK;
 }
@@ -1342,6 +1351,7 @@ int bopx_vsd_from_depths(bopx_ctx* c, int width, int height, const float* depth_
   for (int b = 0; b < nb; ++b)
     for (int k = 0; k < stride; ++k) tot[k] += part[(size_t)b * stride + k];
   const double un = tot[0], comp = tot[0] - tot[1];
+  if (flags & BOPX_VSD_UNIONS) out[n_tau] = un;
   if (un == 0.0) {
     for (int k = 0; k < n_tau; ++k) out[k] = 1.0;
     return BOPX_OK;

@@ -318,9 +318,37 @@ def _dist():
   return 0, 1
 
 
+def todo_costs(objects, p, recs, todo, scene_camera, im_size):
+  """Estimated cost of every todo tuple for the LPT image shard (SURVEY.md §8d
+  flop model, shard.error_cost): mesh size, symmetry count and, for VSD / CUS,
+  the tuple's ROI (bbox corners of the model in both poses, projected with the
+  image's K). objects: BatchEvaluator.objects (nv, nf, ns, bbox per obj_id).
+  None when the object table is not available (uniform weights)."""
+  from . import shard
+  if not todo or not objects:
+    return None
+  et = p["error_type"]
+  obj = [recs[ri]["obj_id"] for ri, _, _, _ in todo]
+  o = [objects[i] for i in obj]
+  nv = np.array([x["nv"] for x in o], np.float64)
+  nf = np.array([x["nf"] for x in o], np.float64)
+  ns = np.array([max(1, x["ns"]) for x in o], np.float64)
+  roi = np.zeros(len(todo))
+  if et in ("vsd", "cus") and scene_camera is not None:
+    lo = np.stack([x["bbox"][0] for x in o])
+    hi = np.stack([x["bbox"][1] for x in o])
+    pe = np.stack([_pose12(recs[ri]["R"], recs[ri]["t"]) for ri, _, _, _ in todo])
+    pg = np.stack([_pose12(R_g, t_g) for _, _, R_g, t_g in todo])
+    K = np.stack([np.asarray(scene_camera[recs[ri]["im_id"]]["cam_K"], np.float64).reshape(3, 3)
+                  for ri, _, _, _ in todo])
+    roi = shard.roi_pixels(lo, hi, [pe, pg], K, im_size[0], im_size[1])
+  return shard.error_cost(et, nv, nf, ns, roi)
+
+
 def shard_todo(recs, todo, world, costs=None):
-  """Images of the scene over ranks (LPT on the number of tuples per image, or
-  on `costs` per todo entry); returns one index array into todo per rank."""
+  """Images of the scene over ranks (LPT on the summed `costs` of each image's
+  todo entries, or on its tuple count); returns one index array into todo per
+  rank (possibly empty: fewer images than ranks)."""
   from . import shard
   ims = sorted({recs[ri]["im_id"] for ri, _, _, _ in todo})
   col = {im: k for k, im in enumerate(ims)}
@@ -330,27 +358,42 @@ def shard_todo(recs, todo, world, costs=None):
   return [np.nonzero(np.isin(frame, part))[0] for part in parts]
 
 
+def plan_rank(p, recs, models_info, objects, scene_camera, im_size, rank, world):
+  """plan() plus this rank's LPT share of the todo tuples (all of them for one
+  rank): (errs, todo, mine)."""
+  errs, todo = plan(p, recs, models_info)
+  if world == 1 or not todo:
+    return errs, todo, np.arange(len(todo))
+  costs = todo_costs(objects, p, recs, todo, scene_camera, im_size)
+  return errs, todo, shard_todo(recs, todo, world, costs)[rank]
+
+
 def evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, models_info,
              symmetric_ids, batch_fn=None, planned=None):
   """errors dict per record. The gated-in tuples of the scene are evaluated as
   one GPU batch; under torch.distributed (world > 1) the scene's images are
-  split over the ranks (LPT) and the rows gathered to rank 0 (RCCL), which
-  alone returns the errors (None elsewhere). planned: (errs, todo, depths)
-  prepared ahead by run() (single process), else computed here."""
+  split over the ranks (LPT on the estimated tuple costs) and the rows gathered
+  to rank 0 (RCCL), which alone returns the errors (None elsewhere). planned:
+  (errs, todo, mine, depths) prepared ahead by run() (depths: the frames of
+  this rank's images, or None), else computed here."""
   et = p["error_type"]
-  errs, todo, depths = planned if planned is not None else plan(p, recs, models_info) + (None,)
   rank, world = _dist()
+  if planned is None:
+    objects = getattr(ev, "objects", None)
+    planned = plan_rank(p, recs, models_info, objects, scene_camera, dp_split["im_size"], rank,
+                        world) + (None,)
+  errs, todo, mine, depths = planned
   if todo:
     batch_fn = batch_fn or evaluate_batch
+    kw = {"depths": depths} if depths is not None else {}
     if world == 1:
-      kw = {"depths": depths} if depths is not None else {}
       rows = batch_fn(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
                       models_info, symmetric_ids, todo, **kw)
     else:
       from . import shard
-      mine = shard_todo(recs, todo, world)[rank]
       local = batch_fn(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
-                       models_info, symmetric_ids, [todo[i] for i in mine]) if len(mine) else None
+                       models_info, symmetric_ids, [todo[i] for i in mine],
+                       **kw) if len(mine) else None
       width = len(p["vsd_taus"]) if et == "vsd" else (10 if et == "cus" else 1)
       dev = ev.device if ev is not None else torch.device("cpu")
       if local is None:
@@ -405,24 +448,26 @@ def run(p, device=0):
     targets_org, ests_org = organize(targets, ests)
     sym_ids = set(dp_model["symmetric_obj_ids"] or [])
     ests_counter = 0
-    single = _dist()[1] == 1
+    rank, world = _dist()
 
     def prepare(scene_id, scene_targets):
-      # host side of one scene: annotations, records, gates and (VSD) the
-      # test-depth PNGs, decoded while the previous scene runs and is saved
+      # host side of one scene: annotations, records, gates, this rank's share
+      # of the tuples and (VSD) its test-depth PNGs, decoded while the previous
+      # scene runs and is saved
       scene_camera = cached_load(inout.load_scene_camera,
                                  dp_split["scene_camera_tpath"].format(scene_id=scene_id))
       scene_gt = cached_load(inout.load_scene_gt,
                              dp_split["scene_gt_tpath"].format(scene_id=scene_id))
       recs, n_ests = scene_records(p, scene_id, scene_targets, ests_org, scene_gt)
       planned = None
-      if single and recs:
-        errs, todo = plan(p, recs, models_info)
+      if recs:
+        errs, todo, mine = plan_rank(p, recs, models_info, ev.objects if ev else None,
+                                     scene_camera, dp_split["im_size"], rank, world)
         depths = None
-        if et == "vsd" and todo:
-          depths = load_scene_depths(dp_split, scene_camera, scene_id, todo_images(recs, todo),
-                                     torch)
-        planned = (errs, todo, depths)
+        if et == "vsd" and len(mine):
+          depths = load_scene_depths(dp_split, scene_camera, scene_id,
+                                     todo_images(recs, [todo[i] for i in mine]), torch)
+        planned = (errs, todo, mine, depths)
       return scene_camera, recs, n_ests, planned
 
     from concurrent.futures import ThreadPoolExecutor

@@ -57,23 +57,27 @@ def vsd(R_est, t_est, R_gt, t_gt, depth_test, K, delta, taus, normalized_by_diam
   masks and the per-tau costs run in one fused kernel (k_vsd). With any other
   duck-typed renderer (renderer.render_object(...)['depth']), its depth maps
   are evaluated on the GPU (k_vsd_depths).
-  Returns a list of len(taus) floats; [1.0] * len(taus) for an empty union.
+  Returns a list of len(taus) numpy.float64 errors (pose_error.py:90-91), or
+  the Python floats [1.0] * len(taus) for an empty visibility union
+  (pose_error.py:75-76); the kernels report the union count for that choice.
   """
   taus = [float(t) for t in taus]
   ctx = runtime.context()
   fx, fy, cx, cy = float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2])
   depth_test = np.ascontiguousarray(depth_test, np.float32)
   H, W = depth_test.shape
-  flags = runtime.delta_flags(delta)
+  flags = runtime.delta_flags(delta) | _lib.VSD_UNIONS
   tau_arr = np.asarray(taus, np.float64)
-  out = np.empty(len(taus), np.float64)
+  out = np.empty(len(taus) + 1, np.float64)  # errors, then the union count
   code = _cost_code(cost_type)
   if isinstance(renderer, RendererHIP) and renderer.ctx is ctx and code is not None and taus:
     oid = int(obj_id)
     p_ids = _const(("id", oid), lambda: np.array([oid], np.int32), _i32)
-    # pose_est | pose_gt | cam | diameter | results in one float64 block
+    # pose_est | pose_gt | cam | diameter | results | union in one float64 block
+    # (a tau chunk writes its union count after its results: into the next
+    # chunk's first slot, which that chunk then overwrites, or the last slot)
     nt = len(taus)
-    blk = np.empty(29 + nt, np.float64)
+    blk = np.empty(30 + nt, np.float64)
     blk[0:9] = np.asarray(R_est, np.float64).reshape(9)
     blk[9:12] = np.asarray(t_est, np.float64).reshape(3)
     blk[12:21] = np.asarray(R_gt, np.float64).reshape(9)
@@ -91,7 +95,7 @@ def vsd(R_est, t_est, R_gt, t_gt, depth_test, K, delta, taus, normalized_by_diam
       ctx.call("bopx_vsd_batch", 1, p_ids, p_pe, p_pg, _ZERO_I32_P, p_dep, 1, W, H, p_cam,
                float(delta), flags, p_tau, k1 - k0, int(bool(normalized_by_diameter)), p_dia,
                code, _lib.cast_ptr(base + (29 + k0) * step, _d))
-    return blk[29:].tolist()
+    return _vsd_result(blk[29:29 + nt], blk[29 + nt])
   depth_est = renderer.render_object(obj_id, R_est, t_est, fx, fy, cx, cy)["depth"]
   depth_gt = renderer.render_object(obj_id, R_gt, t_gt, fx, fy, cx, cy)["depth"]
   de = np.ascontiguousarray(depth_est, np.float32)
@@ -99,13 +103,23 @@ def vsd(R_est, t_est, R_gt, t_gt, depth_test, K, delta, taus, normalized_by_diam
   if not taus:
     return []
   for k0, k1 in _tau_chunks(len(taus)):
-    part, o = np.ascontiguousarray(tau_arr[k0:k1]), np.empty(k1 - k0, np.float64)
+    part, o = np.ascontiguousarray(tau_arr[k0:k1]), np.empty(k1 - k0 + 1, np.float64)
     ctx.call("bopx_vsd_from_depths", W, H, ptr(depth_test, _f), ptr(de, _f), ptr(dg, _f), fx,
              fy, cx, cy, float(delta), flags, ptr(part, _d), k1 - k0,
              int(bool(normalized_by_diameter)), float(diameter),
              code if code is not None else 99, ptr(o, _d))
-    out[k0:k1] = o
-  return [float(e) for e in out]
+    out[k0:k1] = o[:-1]
+    out[-1] = o[-1]
+  return _vsd_result(out[:-1], out[-1])
+
+
+def _vsd_result(errors, union):
+  """The reference's return value: numpy.float64 elements (pose_error.py:90-91,
+  `(np.sum(costs) + comp) / float(union)`), Python floats for an empty union
+  (:75-76)."""
+  if union == 0:
+    return [1.0] * len(errors)
+  return list(np.array(errors, np.float64))
 
 
 def _point_error(name, R_est, t_est, R_gt, t_gt, pts, syms=None, K=None):

@@ -2,8 +2,15 @@
 
 The factory adds renderer_type='hip' (RendererHIP, the gfx950 rasteriser).
 The reference's OpenGL back-ends ('vispy', 'python') and the external C++
-'cpp' renderer are not part of this package.
+'cpp' renderer are not part of this package. For an import-only drop-in
+(scripts/eval_calc_errors.py:57 defaults renderer_type='vispy' and calls
+create_renderer(W, H, p['renderer_type'], mode='depth') at :188-189), the
+environment variable BOPX_RENDERER_ALIAS names reference back-ends (comma
+separated, e.g. "vispy" or "vispy,cpp,python") that the factory maps to
+RendererHIP. It is opt-in: without it those names raise as before, so nobody
+gets a different rasteriser than the one they asked for by accident.
 """
+import os
 
 
 class Renderer(object):
@@ -38,7 +45,8 @@ class Renderer(object):
 def create_renderer(width, height, renderer_type="hip", mode="depth", shading="phong",
                     bg_color=(0.0, 0.0, 0.0, 0.0)):
   """Renderer factory (renderer.py:77-104) with the 'hip' back-end."""
-  if renderer_type == "hip":
+  alias = {a.strip() for a in os.environ.get("BOPX_RENDERER_ALIAS", "").split(",") if a.strip()}
+  if renderer_type == "hip" or renderer_type in alias:
     from .renderer_hip import RendererHIP
     return RendererHIP(width, height, mode, shading, bg_color)
   if renderer_type in ("vispy", "python", "cpp"):

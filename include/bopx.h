@@ -59,6 +59,13 @@ extern "C" {
  * under NumPy >= 2 and the comparison happens in float32 (the default here).
  * A numpy.float64 delta promotes the comparison to float64: set this flag. */
 #define BOPX_DELTA_F64 1
+/* Flag for the VSD entry points: also report each tuple's visibility-union
+ * pixel count (pose_error.py:64), appended after the n x n_tau errors (out
+ * then holds n x n_tau + n doubles). A union of 0 is the reference's
+ * `[1.0] * len(taus)` branch (pose_error.py:75-76), whose elements are Python
+ * floats rather than numpy.float64: the drop-in needs it to return the same
+ * element types. */
+#define BOPX_VSD_UNIONS 2
 
 /* Maximum number of VSD misalignment tolerances per call (the Python layer,
  * bop_toolkit_amd.pose_error.vsd / batch.vsd, splits longer tau lists into

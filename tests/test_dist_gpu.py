@@ -78,10 +78,28 @@ print("RCCL_GATHER_OK")
 
 def test_rccl_gather_rows_one_rank():
   """shard.gather_rows over the real RCCL backend (the collective bench.py and
-  the sharded callers use at N > 1: one all_gather_into_tensor of device rows,
-  scattered by tuple id on rank 0), world size 1 on this one-GPU box."""
+  the sharded callers use at N > 1: one gather of device rows to rank 0,
+  scattered by tuple id there), world size 1 on this one-GPU box."""
   env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
              WORLD_SIZE="1", LOCAL_RANK="0", PYTHONPATH=REPO)
   r = subprocess.run([sys.executable, "-c", _RCCL_GATHER], env=env, cwd=REPO,
                      capture_output=True, text=True, timeout=180)
   assert r.returncode == 0 and "RCCL_GATHER_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def test_bench_two_ranks_strong_scaling():
+  """bench.py under torchrun, 2 ranks on the one GPU (gloo host collectives):
+  the job's 1,002 tuples (167 images) are split by LPT into two uneven shards,
+  rows gathered to rank 0 every step; the line reports the whole job."""
+  import json
+  env = dict(os.environ, BOPX_DIST_BACKEND="gloo")
+  cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+         "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(),
+         os.path.join(REPO, "bench.py"), "--gpus", "2", "--tuples", "1000", "--steps", "2",
+         "--warmup", "1", "--no-cpu-baseline"]
+  r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=300)
+  assert r.returncode == 0, r.stderr[-3000:]
+  line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+  assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 1002
+  assert line["scaling"] == "strong" and 0 < line["config"]["tuples_rank0"] < 1002
+  assert line["value"] > 0

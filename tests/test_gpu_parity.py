@@ -860,3 +860,44 @@ def test_auto_backface_cull_all_modes(oracle_mod, monkeypatch):
     de = oracle_mod.render_depth(pts, faces, Re[i], te_[i], fx, fy, cx, cy, W, H)
     assert np.array_equal(cov[i], _cover_ref(de, dgs[i])), i
     assert np.array_equal(masks[i, 0] > 0, dgs[i] > 0), i
+
+
+def test_drop_in_vsd_return_types(oracle_mod, monkeypatch):
+  """pose_error.vsd returns what the reference returns: a list of numpy.float64
+  (pose_error.py:90-91) when the visibility union is non-empty, and the Python
+  floats [1.0] * len(taus) for an empty union (:75-76), with the HIP renderer
+  and with a foreign one. BOPX_RENDERER_ALIAS=vispy makes the reference's
+  default create_renderer(W, H, 'vispy', mode='depth') (eval_calc_errors.py:57,
+  188-189) a RendererHIP, so the drop-in is import-only."""
+  from bop_toolkit_amd import pose_error as pe
+  from bop_toolkit_amd.renderer import create_renderer
+  from bop_toolkit_amd.renderer_hip import RendererHIP
+  rng, pts, faces, Rg, tg, Re, te_, K = _scene(37, 2)
+  monkeypatch.setenv("BOPX_RENDERER_ALIAS", "vispy")
+  ren = create_renderer(640, 480, "vispy", mode="depth")
+  assert isinstance(ren, RendererHIP)
+  ren.add_object_arrays(31, pts, faces)
+  fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+
+  class Foreign:
+    def render_object(self, obj_id, R, t, fx, fy, cx, cy):
+      return {"depth": oracle_mod.render_depth(pts, faces, R, t, fx, fy, cx, cy, 640, 480)}
+
+  taus = list(np.arange(0.05, 0.51, 0.05))
+  many = list(np.linspace(0.02, 0.6, 20))  # two tau chunks
+  dg = oracle_mod.render_depth(pts, faces, Rg[0], tg[0], fx, fy, cx, cy, 640, 480)
+  dt = np.where(dg > 0, dg + 1.0, 0.0).astype(np.float32)
+  behind = np.array([[0.0], [0.0], [-300.0]])
+  for r in (ren, Foreign()):
+    for tl in (taus, many):
+      e = pe.vsd(Re[0], te_[0].reshape(3, 1), Rg[0], tg[0].reshape(3, 1), dt, K, 15.0, tl, True,
+                 150.0, r, 31, "step")
+      assert len(e) == len(tl) and all(type(x) is np.float64 for x in e), (type(e[0]), r)
+      de = oracle_mod.render_depth(pts, faces, Re[0], te_[0], fx, fy, cx, cy, 640, 480)
+      assert e == oracle_mod.vsd_depths(dt, de, dg, fx, fy, cx, cy, 15.0, tl, True, 150.0)
+      # both poses behind the camera: empty union, plain floats
+      e = pe.vsd(Rg[0], behind, Rg[0], behind, dt, K, 15.0, tl, True, 150.0, r, 31, "step")
+      assert e == [1.0] * len(tl) and all(type(x) is float for x in e)
+  monkeypatch.delenv("BOPX_RENDERER_ALIAS")
+  with pytest.raises(NotImplementedError):
+    create_renderer(640, 480, "vispy", mode="depth")

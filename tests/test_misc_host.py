@@ -54,3 +54,37 @@ def test_delta_flags_follow_legacy_numpy_casting():
   # 15.3 rounds to 15.300000190734863 in float32, so d_diff = that value passes
   d = np.float32(15.3)
   assert d <= np.float32(np.float64(15.3)) and not float(d) <= 15.3
+
+
+def test_renderer_alias_is_opt_in(monkeypatch):
+  """create_renderer(W, H, 'vispy') (the reference caller's default,
+  eval_calc_errors.py:57,188-189) raises unless BOPX_RENDERER_ALIAS names it;
+  then it builds the HIP renderer (stubbed here: no GPU on this host)."""
+  from bop_toolkit_amd import renderer, renderer_hip
+
+  class Fake:
+    def __init__(self, *a):
+      self.args = a
+
+  monkeypatch.setattr(renderer_hip, "RendererHIP", Fake)
+  monkeypatch.delenv("BOPX_RENDERER_ALIAS", raising=False)
+  with pytest.raises(NotImplementedError):
+    renderer.create_renderer(640, 480, "vispy", mode="depth")
+  with pytest.raises(ValueError):
+    renderer.create_renderer(640, 480, "opengl", mode="depth")
+  monkeypatch.setenv("BOPX_RENDERER_ALIAS", "cpp, vispy")
+  r = renderer.create_renderer(640, 480, "vispy", mode="depth")
+  assert isinstance(r, Fake) and r.args[:3] == (640, 480, "depth")
+  assert isinstance(renderer.create_renderer(640, 480, "cpp"), Fake)
+  with pytest.raises(NotImplementedError):
+    renderer.create_renderer(640, 480, "python")
+
+
+def test_vsd_result_types():
+  """The drop-in VSD's return value (pose_error.py:75-91): numpy.float64
+  elements for a non-empty union, Python floats [1.0] * n for an empty one."""
+  from bop_toolkit_amd.pose_error import _vsd_result
+  e = _vsd_result(np.array([0.25, 1.0]), 40.0)
+  assert e == [0.25, 1.0] and all(type(x) is np.float64 for x in e)
+  e = _vsd_result(np.array([1.0, 1.0, 1.0]), 0.0)
+  assert e == [1.0] * 3 and all(type(x) is float for x in e)

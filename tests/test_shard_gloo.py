@@ -1,5 +1,6 @@
-"""Multi-process sharding / gather on CPU (gloo, world_size 2): the gathered
-table is bitwise identical to the single-process table."""
+"""Multi-process sharding / gather on CPU (gloo, world sizes 2, 4 and 8): the
+gathered table is bitwise identical to the single-process table (SURVEY.md
+§8e), also when ranks get no images at all (4 test images over 8 ranks)."""
 import os
 import socket
 
@@ -76,15 +77,30 @@ def test_gather_bitwise_equals_single(tmp_path, world):
 def _stub_rows(ev, torch_, p, dataset, dp_split, scene_camera, scene_id, recs, models_info,
                sym_ids, todo):
   """Stand-in for the GPU batch: a deterministic function of (record, gt)."""
-  width = len(p["vsd_taus"])
+  width = len(p["vsd_taus"]) if p["error_type"] == "vsd" else 1
   return torch.tensor([[ri * 1000.0 + gt_id + 0.1 * k for k in range(width)]
                        for ri, gt_id, _, _ in todo], dtype=torch.float64)
 
 
-def _caller_errs(world_rank=None):
+class _FakeEv:
+  """The object table the caller's LPT cost model reads (BatchEvaluator.objects)
+  without a GPU: sizes per object, bbox from models_info.json."""
+
+  def __init__(self, info):
+    import torch as _t
+    self.device = _t.device("cpu")
+    self.objects = {}
+    for k, (obj_id, m) in enumerate(sorted(info.items())):
+      lo = np.array([m["min_x"], m["min_y"], m["min_z"]])
+      hi = lo + np.array([m["size_x"], m["size_y"], m["size_z"]])
+      self.objects[obj_id] = {"nv": 1000 + 700 * k, "nf": 2000 + 1400 * k, "ns": 1 + k,
+                              "bbox": (lo, hi)}
+
+
+def _caller_errs(error_type="vsd", with_costs=False):
   from bop_toolkit_amd import dataset_params, eval_calc_errors as ece, inout
   e2e = os.path.join(os.path.dirname(__file__), "golden", "e2e")
-  p = ece.parse_args(["--error_type", "vsd", "--n_top", "-1", "--result_filenames",
+  p = ece.parse_args(["--error_type", error_type, "--n_top", "-1", "--result_filenames",
                       "synth_lmo-test.csv", "--results_path", os.path.join(e2e, "results"),
                       "--datasets_path", os.path.join(e2e, "datasets")])
   dp_split = dataset_params.get_split_params(p["datasets_path"], "lmo", "test")
@@ -94,16 +110,18 @@ def _caller_errs(world_rank=None):
   t_org, e_org = ece.organize(targets, ests)
   info = inout.load_json(dp_model["models_info_path"], keys_to_int=True)
   scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=2))
+  scene_camera = inout.load_scene_camera(dp_split["scene_camera_tpath"].format(scene_id=2))
   recs, _ = ece.scene_records(p, 2, t_org[2], e_org, scene_gt)
-  return ece.evaluate(None, torch, p, "lmo", dp_split, None, 2, recs, info, set(),
+  ev = _FakeEv(info) if with_costs else None
+  return ece.evaluate(ev, torch, p, "lmo", dp_split, scene_camera, 2, recs, info, set(),
                       batch_fn=_stub_rows)
 
 
-def _caller_worker(rank, world, port, out_path):
+def _caller_worker(rank, world, port, out_path, error_type, with_costs):
   os.environ["MASTER_ADDR"] = "127.0.0.1"
   os.environ["MASTER_PORT"] = str(port)
   dist.init_process_group("gloo", rank=rank, world_size=world)
-  errs = _caller_errs()
+  errs = _caller_errs(error_type, with_costs)
   if rank == 0:
     import json
     with open(out_path, "w") as f:
@@ -114,12 +132,48 @@ def _caller_worker(rank, world, port, out_path):
   dist.destroy_process_group()
 
 
-def test_caller_sharded_equals_single(tmp_path):
-  """eval_calc_errors.evaluate under gloo world 2 (images of the scene split
-  by LPT, rows gathered to rank 0) == the single-process result."""
+@pytest.mark.parametrize("world,error_type,with_costs", [
+    (2, "vsd", False), (2, "vsd", True), (4, "mssd", True), (8, "vsd", True),
+    (8, "mssd", True)])
+def test_caller_sharded_equals_single(tmp_path, world, error_type, with_costs):
+  """eval_calc_errors.evaluate under gloo (images of the scene split by LPT on
+  the SURVEY §8d tuple costs, rows gathered to rank 0) == the single-process
+  result. World 8 > the 4 test images: some ranks evaluate nothing and still
+  join the gather with zero rows."""
   import json
   out = str(tmp_path / "errs.json")
-  mp.spawn(_caller_worker, args=(2, _free_port(), out), nprocs=2, join=True)
-  single = [{str(k): v for k, v in e.items()} for e in _caller_errs()]
+  mp.spawn(_caller_worker, args=(world, _free_port(), out, error_type, with_costs),
+           nprocs=world, join=True)
+  single = [{str(k): v for k, v in e.items()} for e in _caller_errs(error_type, with_costs)]
   assert json.load(open(out)) == single
   assert sum(v[0] != 1.0 and v[0] < 1e6 for e in single for v in e.values()) > 10
+
+
+def test_caller_cost_model_shapes_the_shard():
+  """todo_costs: VSD costs grow with the projected ROI, MSSD costs with V * S,
+  and the LPT shard built from them covers every tuple exactly once."""
+  from bop_toolkit_amd import dataset_params, eval_calc_errors as ece, inout
+  e2e = os.path.join(os.path.dirname(__file__), "golden", "e2e")
+  for et in ("vsd", "mssd"):
+    p = ece.parse_args(["--error_type", et, "--n_top", "-1", "--datasets_path",
+                        os.path.join(e2e, "datasets")])
+    dp_split = dataset_params.get_split_params(p["datasets_path"], "lmo", "test")
+    dp_model = dataset_params.get_model_params(p["datasets_path"], "lmo", "eval")
+    targets = inout.load_json(os.path.join(dp_split["base_path"], p["targets_filename"]))
+    ests = inout.load_bop_results(os.path.join(e2e, "results", "synth_lmo-test.csv"))
+    t_org, e_org = ece.organize(targets, ests)
+    info = inout.load_json(dp_model["models_info_path"], keys_to_int=True)
+    scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=2))
+    cams = inout.load_scene_camera(dp_split["scene_camera_tpath"].format(scene_id=2))
+    recs, _ = ece.scene_records(p, 2, t_org[2], e_org, scene_gt)
+    ev = _FakeEv(info)
+    errs, todo = ece.plan(p, recs, info)
+    c = ece.todo_costs(ev.objects, p, recs, todo, cams, dp_split["im_size"])
+    assert c.shape == (len(todo),) and (c > 0).all()
+    if et == "mssd":
+      o = [ev.objects[recs[ri]["obj_id"]] for ri, _, _, _ in todo]
+      assert np.allclose(c, [x["nv"] * (18 + 28 * x["ns"]) for x in o])
+    else:
+      assert np.ptp(c) > 0
+    parts = ece.shard_todo(recs, todo, 3, c)
+    assert np.array_equal(np.sort(np.concatenate(parts)), np.arange(len(todo)))

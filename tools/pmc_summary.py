@@ -2,6 +2,10 @@
 
     python tools/pmc_summary.py OUT.json DIR [DIR ...]
 
+If a DIR holds meta.json (bench.py with BOPX_BENCH_META: the libbopx.so sha256
+and the workload), it is recorded as `_meta`; bench.py uses a summary's
+traffic only when both match the run it reports.
+
 Per kernel: mean value per dispatch of every counter collected (each DIR is one
 rocprofv3 pass). HBM traffic per launch follows MI355X_MICROARCH.md §HBM:
 FETCH_SIZE and WRITE_SIZE are in KiB (TCC_EA0_RDREQ/_WRREQ based); on gfx950
@@ -44,6 +48,15 @@ def main(out, dirs):
       r["hbm_bytes_raw_per_launch"] = (r["FETCH_SIZE"] + r["WRITE_SIZE"]) * 1024.0
       r["hbm_bytes_per_launch"] = (2.0 * r["FETCH_SIZE"] + r["WRITE_SIZE"]) * 1024.0
     res[k] = r
+  metas = []
+  for d in dirs:
+    try:
+      with open(os.path.join(d, "meta.json")) as f:
+        metas.append(json.load(f))
+    except (OSError, ValueError):
+      pass
+  if metas and all(m == metas[0] for m in metas):
+    res["_meta"] = metas[0]
   with open(out, "w") as f:
     json.dump(res, f, indent=1, sort_keys=True)
   for k, r in res.items():
