@@ -470,6 +470,12 @@ constexpr int kCullAutoDensity = 12;  // ... and at least this many meshlets per
 #ifndef BOPX_VSD_EARLY_RESET
 #define BOPX_VSD_EARLY_RESET 0
 #endif
+#ifndef BOPX_VSD_XLAT
+#define BOPX_VSD_XLAT 0
+#endif
+#ifndef BOPX_VSD_LDSPAD
+#define BOPX_VSD_LDSPAD 0  // experiment: extra LDS bytes per workgroup (occupancy)
+#endif
 #ifndef BOPX_VSD_PRECLAIM
 #define BOPX_VSD_PRECLAIM 1
 #endif
@@ -520,6 +526,10 @@ void k_vsd(VsdArgs a) {
   __shared__ float s_qhi[2];
   __shared__ float s_zr[2][2];  // per pose: depth range of the meshlet corners (min, max)
   __shared__ int s_next;
+#if BOPX_VSD_LDSPAD
+  __shared__ uint8_t s_pad[BOPX_VSD_LDSPAD];
+  if (threadIdx.x == 0) asm volatile("" ::"v"(s_pad + blockIdx.x % 7));
+#endif
   __shared__ __attribute__((aligned(16))) float s_pose[2][12];
   __shared__ int s_roi[4];
   __shared__ int s_nlist;
@@ -906,6 +916,16 @@ void k_vsd(VsdArgs a) {
                                     make_region(word[g], tx1 - tx0 + 1, ty1 - ty0 + 1), 0, lane);
           }
         }
+#if BOPX_VSD_XLAT
+        // experiment: one extra dependent (L1/L2-hit) load per vertex block, to
+        // measure the kernel's sensitivity to the vertex-load latency
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g) {
+          uint32_t z;
+          asm volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"(__float_as_uint(v[g].x)));
+          v[g] = ld_off(g_mvtx3 + mlt[g] * kMeshletVerts, (uint32_t)lane * 16u + z);
+        }
+#endif
         if (VSD_DIAG(8)) {  // diagnostics: time the vertex-block loads alone
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           VSD_STAMP(13);

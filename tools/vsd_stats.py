@@ -31,7 +31,7 @@ def main():
   args = bench.parse()
   ev = BatchEvaluator(0)
   objs = bench.build_objects(ev, args, torch)
-  n, d = bench.build_workload(ev, objs, args, 0, torch)
+  n, d = bench.build_workload(ev, objs, args, 0, 1, torch)
   fn = ev.ctx.lib.bopx_debug_vsd_stats
   fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
   st = (ctypes.c_ulonglong * 32)()
