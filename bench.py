@@ -56,6 +56,17 @@ CONFIGS = {
         "continuous": False, "tuples": 200000, "K": "TLESS_K", "W": 720, "H": 540,
         "errors": ("vsd", "mssd", "mspd"),
         "what": "configs[4]: T-LESS-like BOP19 set, ~15k verts, S<=64, 200k est"},
+    # Multi-instance variant of configs[4] (T-LESS / IC-BIN / ITODD images hold
+    # several instances of an object; n_top = -1 pairs every estimate with every
+    # GT instance, eval_calc_errors.py:281-290): 3 objects per image with k in
+    # [3, 6] instances and k estimates each, k^2 tuples per (image, object). VSD
+    # runs on shared renders (each distinct pose rasterised once, k_vsd_pair per
+    # tuple); the fused per-tuple k_vsd on the same tuples is timed beside it.
+    5: {"objects": 30, "n_lat": 100, "n_lon": 150, "syms": [1, 2, 4, 8, 16, 32, 64],
+        "continuous": False, "tuples": 100000, "K": "TLESS_K", "W": 720, "H": 540,
+        "errors": ("vsd", "mssd", "mspd"), "multi": (3, 3, 6),
+        "what": "configs[4] multi-instance variant: 3 objs/image x k in [3,6] instances, "
+                "k^2 tuples each (n_top -1), shared renders"},
 }
 
 
@@ -174,6 +185,78 @@ def build_workload(ev, objs, args, rank, world, torch):
     sz = torch.randint(40, 120, (m, 1, 1), device=dev, generator=g)
     occ = (xs >= x0) & (xs < x0 + sz) & (ys >= y0) & (ys < y0 + sz)
     f.masked_fill_(occ, 450.0)
+    f.add_(torch.randn(f.shape, device=dev, generator=g), alpha=2.0)
+    f.round_().clamp_(0, 65535)
+    f.masked_fill_(torch.rand(f.shape, device=dev, generator=g) < 0.1, 0.0)
+  d["frames"] = frames
+  d["host"] = {"obj": obj, "pe": pe, "pg": pg, "frame_idx": frame_idx, "cam": cam}
+  torch.cuda.synchronize()
+  return n, d
+
+
+def build_workload_multi(ev, objs, args, rank, world, torch):
+  """configs[5]: images with m objects, k instances of each (k uniform in
+  [kmin, kmax]) and k estimates per (image, object); tuples = every estimate x
+  every GT instance of its object. Test depth as in build_workload, composited
+  from every GT instance. This rank's images: a contiguous share."""
+  from bop_toolkit_amd import synth
+  from bop_toolkit_amd.batch import unique_renders
+  m, kmin, kmax = args.cfg["multi"]
+  rng = np.random.default_rng(args.seed + 2000)
+  per_img_mean = m * np.mean([k * k for k in range(kmin, kmax + 1)])
+  n_img_all = int(np.ceil(args.tuples / per_img_mean))
+  lo = rank * n_img_all // world
+  hi = (rank + 1) * n_img_all // world
+  K = getattr(synth, args.cfg["K"])
+  inst_obj, inst_f, inst_pose = [], [], []
+  t_obj, t_f, t_pe, t_pg, t_gid = [], [], [], [], []
+  gid = 0
+  for f in range(n_img_all):
+    for o in rng.choice(len(objs), m, replace=False):
+      k = int(rng.integers(kmin, kmax + 1))
+      Rg, tg = synth.gt_poses(rng, k)
+      Re, te = synth.perturb(rng, Rg, tg)
+      pg = np.concatenate([Rg.reshape(k, 9), tg], 1)
+      pe = np.concatenate([Re.reshape(k, 9), te], 1)
+      mine = lo <= f < hi
+      if mine:
+        inst_obj += [o] * k
+        inst_f += [f - lo] * k
+        inst_pose.append(pg)
+      for i in range(k):
+        for j in range(k):
+          if mine:
+            t_obj.append(o)
+            t_f.append(f - lo)
+            t_pe.append(pe[i])
+            t_pg.append(pg[j])
+            t_gid.append(gid)
+          gid += 1
+  n_all, n_img = gid, hi - lo
+  obj = np.array(t_obj, np.int32)
+  frame_idx = np.array(t_f, np.int32)
+  pe, pg = np.stack(t_pe), np.stack(t_pg)
+  n = len(obj)
+  cam = np.tile([K[0, 0], K[1, 1], K[0, 2], K[1, 2]], (n_img, 1)).astype(np.float64)
+  dev = ev.device
+  t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+  ro, rp, rf, er, gr = unique_renders(obj, pe, pg, frame_idx)
+  d = {"slots": ev.slots(obj), "pose_est": t(pe, torch.float64), "pose_gt": t(pg, torch.float64),
+       "frame_idx": t(frame_idx, torch.int32), "cam": t(cam, torch.float64),
+       "K": t(np.tile(K.reshape(9), (n, 1)), torch.float64),
+       "diameters": t([objs[o]["diameter"] for o in obj], torch.float64),
+       "gid": t(t_gid, torch.int64), "n_total": n_all,
+       "counts": [None] * world,
+       "renders": {"slots": ev.slots(ro), "pose": t(rp, torch.float64),
+                   "frame_idx": t(rf, torch.int32), "est": t(er, torch.int32),
+                   "gt": t(gr, torch.int32), "n": len(ro)}}
+  frames = ev.render(ev.slots(inst_obj), t(np.concatenate(inst_pose), torch.float64),
+                     t(inst_f, torch.int32), d["cam"], n_img, W, H)
+  g = torch.Generator(device=dev)
+  g.manual_seed(args.seed + rank)
+  for c0 in range(0, n_img, 1024):
+    f = frames[c0:c0 + 1024]
+    f[f <= 0] = 1600.0
     f.add_(torch.randn(f.shape, device=dev, generator=g), alpha=2.0)
     f.round_().clamp_(0, 65535)
     f.masked_fill_(torch.rand(f.shape, device=dev, generator=g) < 0.1, 0.0)
@@ -319,7 +402,13 @@ def main():
   from bop_toolkit_amd.batch import BatchEvaluator
   ev = BatchEvaluator(local)
   objs = build_objects(ev, args, torch)
-  n, d = build_workload(ev, objs, args, rank, world, torch)
+  multi = "multi" in args.cfg
+  n, d = (build_workload_multi if multi else build_workload)(ev, objs, args, rank, world, torch)
+  if multi and world > 1:  # the shares are uneven: exchange the counts once
+    dv = ev.device if backend == "nccl" else torch.device("cpu")
+    cl = [torch.zeros(1, dtype=torch.int64, device=dv) for _ in range(world)]
+    dist.all_gather(cl, torch.tensor([n], dtype=torch.int64, device=dv))
+    d["counts"] = [int(c.item()) for c in cl]
   meta = os.environ.get("BOPX_BENCH_META")  # tools/pmc.sh: what the counters measured
   if meta and rank == 0:
     with open(meta, "w") as f:
@@ -344,9 +433,13 @@ def main():
 
   def step(timed):
     e = pool[len(marks)] if timed else None
+    rd = d.get("renders")
     run = {
-        "vsd": lambda: ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"],
-                              d["frames"], d["cam"], DELTA, TAUS, d["diameters"], out=out_vsd),
+        "vsd": (lambda: ev.vsd_shared(rd["slots"], rd["pose"], rd["frame_idx"], rd["est"],
+                                      rd["gt"], d["frames"], d["cam"], DELTA, TAUS,
+                                      d["diameters"], out=out_vsd)) if rd else
+               (lambda: ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"],
+                               d["frames"], d["cam"], DELTA, TAUS, d["diameters"], out=out_vsd)),
         "mssd": lambda: ev.mssd(d["slots"], d["pose_est"], d["pose_gt"], out=out_mssd),
         "mspd": lambda: ev.mspd(d["slots"], d["pose_est"], d["pose_gt"], d["K"], out=out_mspd),
         "add": lambda: ev.add(d["slots"], d["pose_est"], d["pose_gt"], out=out_mssd),
@@ -395,6 +488,21 @@ def main():
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = float(tt.item())
 
+  fused_ms = None
+  if multi:  # the same tuples through the fused per-tuple k_vsd, for comparison
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ref = ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"], d["frames"], d["cam"],
+                 DELTA, TAUS, d["diameters"])
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(max(1, args.steps // 2)):
+      ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"], d["frames"], d["cam"],
+             DELTA, TAUS, d["diameters"], out=ref)
+    e1.record()
+    torch.cuda.synchronize()
+    fused_ms = e0.elapsed_time(e1) / max(1, args.steps // 2)
+    if not torch.equal(ref, out_vsd):
+      raise RuntimeError("shared-render VSD differs from the fused kernel")
   if rank == 0:
     steps = args.steps
     total = d["n_total"] * steps
@@ -452,6 +560,15 @@ def main():
                    "roi_mean_px": round(cost["roi_mean"], 1),
                    **({"axes_scale": args.axes_scale} if args.axes_scale != 1.0 else {})},
         "roofline": roof, "kernels": kernels, "cpu_baseline": cpu}
+    if multi:
+      rd = d["renders"]
+      if roof is not None and roof["kernel"] == "k_vsd":
+        roof["kernel"] = "k_vsd (render mode) + k_vsd_pair"
+        roof["note"] = "algorithmic bytes / flops of the per-tuple model (two renders each)"
+      line["config"]["renders"] = rd["n"]
+      line["kernels"]["vsd_fused_per_tuple"] = {"ms": fused_ms,
+                                                "renders": 2 * n,
+                                                "note": "same tuples, two renders each (k_vsd)"}
     print(json.dumps(line), flush=True)
   if world > 1:
     dist.barrier()

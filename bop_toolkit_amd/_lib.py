@@ -51,6 +51,10 @@ SIGNATURES = {
     "bopx_proj_batch": (_I, [_CTX, _I64, _i32, _d, _d, _d, _d]),
     "bopx_vsd_batch": (_I, [_CTX, _I64, _i32, _d, _d, _i32, _f, _I64, _I, _I, _d, _D, _I, _d,
                             _I, _I, _d, _I, _d]),
+    "bopx_vsd_shared_batch": (_I, [_CTX, _I64, _i32, _d, _i32, _I64, _i32, _i32, _f, _I64, _I,
+                                   _I, _d, _D, _I, _d, _I, _I, _d, _I, _d]),
+    "bopx_vsd_shared_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _I64, _P, _P, _P, _I, _I, _P, _D,
+                                       _I, _d, _I, _I, _P, _I, _P, _P]),
     "bopx_vsd_from_depths": (_I, [_CTX, _I, _I, _f, _f, _f, _D, _D, _D, _D, _D, _I, _d, _I, _I,
                                   _D, _I, _d]),
     "bopx_cover_batch": (_I, [_CTX, _I64, _i32, _d, _d, _i32, _I64, _I, _I, _d, _d]),

@@ -126,6 +126,35 @@ class BatchEvaluator:
                   _p(diameters), code, _p(out), _stream(self.device))
     return out
 
+  def vsd_shared(self, render_slots, render_poses, render_frame_idx, est_render, gt_render,
+                 frames, cam, delta, taus, diameters, normalized_by_diameter=True,
+                 cost_type="step", out=None, delta_flags=0):
+    """VSD of n (est, gt) tuples over distinct renders (multi-instance images,
+    see unique_renders): each render rasterised once into an HBM depth buffer,
+    then the VSD pixel pass per tuple (k_vsd_pair). Same results as vsd() on
+    the expanded tuples (step cost bit for bit). Synchronises the stream once."""
+    n = est_render.numel()
+    taus = np.ascontiguousarray(taus, np.float64)
+    code = {"step": _lib.COST_STEP, "tlinear": _lib.COST_TLINEAR}.get(cost_type)
+    if code is None:
+      raise ValueError("Unknown pixel matching cost.")
+    out = self._out(n, len(taus)) if out is None else out
+    if len(taus) > _lib.MAX_TAUS:
+      for k0 in range(0, len(taus), _lib.MAX_TAUS):
+        k1 = min(k0 + _lib.MAX_TAUS, len(taus))
+        out[:, k0:k1] = self.vsd_shared(render_slots, render_poses, render_frame_idx,
+                                        est_render, gt_render, frames, cam, delta, taus[k0:k1],
+                                        diameters, normalized_by_diameter, cost_type,
+                                        delta_flags=delta_flags)
+      return out
+    H, W = int(frames.shape[-2]), int(frames.shape[-1])
+    self.ctx.call("bopx_vsd_shared_batch_dev", render_slots.numel(), _p(render_slots),
+                  _p(render_poses), _p(render_frame_idx), n, _p(est_render), _p(gt_render),
+                  _p(frames), W, H, _p(cam), float(delta), int(delta_flags),
+                  taus.ctypes.data_as(_lib._d), len(taus), int(bool(normalized_by_diameter)),
+                  _p(diameters), code, _p(out), _stream(self.device))
+    return out
+
   def cover(self, slots, pose_est, pose_gt, frame_idx, cam, width, height, out=None):
     """Silhouette overlap per tuple for cus / cou_bb_proj: float64 [n, 10] =
     union, inter, est bbox (x0, y0, x1, y1), gt bbox (empty: x1 = y1 = -1)."""
@@ -173,3 +202,21 @@ class BatchEvaluator:
     m = self.mssd(slots, pose_est, pose_gt, out=out_mssd)
     p = self.mspd(slots, pose_est, pose_gt, K, out=out_mspd)
     return {"vsd": v, "mssd": m, "mspd": p}
+
+
+def unique_renders(obj, pose_est, pose_gt, frame_idx):
+  """Distinct renders of a batch of VSD tuples (host arrays): every (object,
+  pose, frame) once, estimates and GT poses alike (bit-identical float64 poses
+  are one render). Returns (render_obj, render_pose n_r x 12, render_frame,
+  est_render, gt_render) for BatchEvaluator.vsd_shared."""
+  obj = np.ascontiguousarray(obj, np.int64)
+  fi = np.ascontiguousarray(frame_idx, np.int64)
+  poses = np.ascontiguousarray(np.concatenate([pose_est, pose_gt]), np.float64)
+  keys = np.concatenate([np.stack([np.concatenate([obj, obj]), np.concatenate([fi, fi])], 1),
+                         poses.view(np.int64)], 1)
+  _, first, inv = np.unique(keys, axis=0, return_index=True, return_inverse=True)
+  inv = inv.reshape(-1)
+  n = len(obj)
+  o2, f2 = np.concatenate([obj, obj]), np.concatenate([fi, fi])
+  return (o2[first].astype(np.int32), poses[first], f2[first].astype(np.int32),
+          inv[:n].astype(np.int32), inv[n:].astype(np.int32))

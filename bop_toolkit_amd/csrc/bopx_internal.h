@@ -43,6 +43,9 @@ constexpr int kCostCover = 2;  // k_vsd mode: silhouette union/inter + bboxes (c
 constexpr int kCoverCols = 10;  // union, inter, est bbox x0 y0 x1 y1, gt bbox x0 y0 x1 y1
 constexpr int kCostGtInfo = 3;  // k_vsd mode: one (gt) pose, silhouette + visibility stats
 constexpr int kGtInfoCols = 11;  // all, visib, obj bbox x0 y0 x1 y1, visib bbox, valid
+// k_vsd mode: one pose rendered into an HBM q buffer over its ROI (VsdArgs::rois,
+// qoff, qbuf), shared by every VSD tuple that uses the pose (k_vsd_pair)
+constexpr int kCostRender = 4;
 constexpr int kTileW = BOPX_TILE_W;  // VSD screen tile (LDS-resident q pair)
 constexpr int kTileH = BOPX_TILE_H;
 #ifndef BOPX_TILE_STRIDE
@@ -106,6 +109,11 @@ struct VsdArgs {
   int64_t split_from;
   double* part;
   double* unions;  // optional (BOPX_VSD_UNIONS): per tuple visibility-union pixel count
+  // render mode (kCostRender): per render its ROI (x0, y0, x1, y1, from
+  // launch_pose_roi) and the offset of its row-major q buffer in qbuf
+  const int4* rois;
+  const int64_t* qoff;
+  uint32_t* qbuf;
   double taus[kMaxTaus];
 };
 constexpr int kVsdPartCols = 2 + 2 * kMaxTaus;  // union, inter, cnt[kMaxTaus], lin[kMaxTaus]
@@ -138,6 +146,35 @@ struct OrderCost {  // VSD inputs of the cost classes (pe == nullptr: order by s
 hipError_t launch_order_by_slot(const int32_t* slots, int64_t n, int ns, int32_t* order,
                                 int32_t* keys, hipStream_t s, const OrderCost* cost = nullptr);
 hipError_t launch_vsd(const VsdArgs& a, int cost_type, hipStream_t s);  // or kCostCover
+
+// Shared renders (GT-side / estimate reuse, multi-instance images): each
+// distinct (object, pose, frame) is rasterised once (k_vsd, kCostRender) into an
+// HBM q buffer over its ROI; every (est, gt) tuple then runs the VSD pixel pass
+// on the two cached buffers (k_vsd_pair).
+// ROI of each render: the union of its meshlet rectangles (k_vsd's own rule).
+hipError_t launch_pose_roi(const ObjDesc* objs, int64_t n, const int32_t* slots,
+                           const double* pose, const int32_t* frame_idx, const double* cam, int W,
+                           int H, int4* rois, hipStream_t s);
+struct PairArgs {
+  const int4* rois;        // per render
+  const int64_t* qoff;     // per render: offset of its q buffer in qbuf (dwords)
+  const uint32_t* qbuf;    // q = 1/Z bits, 0 = background
+  const int32_t* rframe;   // per render: frame index
+  const int32_t* est_r;    // per tuple: render of the estimate
+  const int32_t* gt_r;     // per tuple: render of the GT
+  int64_t n_renders;       // render indices outside [0, n_renders) give NaN errors
+  const float* frames;     // n_frames x H x W test depth
+  const double* cam;       // per frame fx fy cx cy
+  const double* diameters; // per tuple
+  double* out;             // n x n_tau
+  double* unions;          // optional: per tuple visibility-union count
+  int64_t n;
+  int width, height;
+  float dthr;
+  int n_tau, normalized;
+  double taus[kMaxTaus];
+};
+hipError_t launch_vsd_pair(const PairArgs& a, int cost_type, hipStream_t s);
 hipError_t launch_cover_depths(int W, int H, const float* de, const float* dg,
                                long long* acc /* kCoverCols, device */, hipStream_t s);
 hipError_t read_vsd_stats(unsigned long long* out, int reset);  // diagnostics

@@ -635,7 +635,7 @@ void k_vsd(VsdArgs a) {
     rect[j] = make_short4(1, 1, 0, 0);
     zmin[j] = -INFINITY;
     qbv[j] = 0.0f;
-    if (i < 2 * nm && !(COST == kCostGtInfo && i < nm)) {  // GT-info: gt pose only
+    if (i < 2 * nm && !((COST == kCostGtInfo || COST == kCostRender) && i < nm)) {  // GT-info: gt pose only
       const int r = i >= nm, m = i - r * nm;
       bool bk = false;
       rect[j] = meshlet_rect(g_mlet + kMletFloats * (int64_t)m, s_pose[r], c32, W, H, zmin[j],
@@ -702,7 +702,14 @@ void k_vsd(VsdArgs a) {
   // tiles are clean for the next tile without a separate clearing pass.
   for (int i = tid; i < 2 * kTileStride * kTileH; i += kVsdThreads) (&s_dep[0][0])[i] = 0u;
   __syncthreads();
-  const int rx0 = s_roi[0], ry0 = s_roi[1], rx1 = s_roi[2], ry1 = s_roi[3];
+  // render mode: the ROI its q buffer was sized for (launch_pose_roi, the same
+  // rule), so every write lands inside the buffer
+  int4 rroi = make_int4(0, 0, -1, -1);
+  if constexpr (COST == kCostRender) rroi = a.rois[b];
+  const int rx0 = COST == kCostRender ? rroi.x : s_roi[0];
+  const int ry0 = COST == kCostRender ? rroi.y : s_roi[1];
+  const int rx1 = COST == kCostRender ? rroi.z : s_roi[2];
+  const int ry1 = COST == kCostRender ? rroi.w : s_roi[3];
   // automatic mode also asks for meshlets dense on screen: >= kCullAutoDensity
   // per ROI tile (a 30k-triangle object drawn large, 10 per tile, loses 1 %)
   const int roi_tiles = rx0 <= rx1 && ry0 <= ry1
@@ -783,7 +790,7 @@ void k_vsd(VsdArgs a) {
         if constexpr (kStream) {  // recomputed (round e0, entry e0 + tid + 512 j)
           const int i = e0 + tid + j * kVsdThreads;
           rc = make_short4(1, 1, 0, 0);
-          if (i < 2 * nm && !(COST == kCostGtInfo && i < nm)) {
+          if (i < 2 * nm && !((COST == kCostGtInfo || COST == kCostRender) && i < nm)) {
             const int r = i >= nm, m = i - r * nm;
             float zm, qq;
             bool bk;
@@ -1320,7 +1327,8 @@ void k_vsd(VsdArgs a) {
           }
         }
       };
-      if constexpr (COST == kCostCover || COST == kCostGtInfo || !BOPX_VSD_PIXPIPE) {
+      if constexpr (COST == kCostCover || COST == kCostGtInfo || COST == kCostRender ||
+                    !BOPX_VSD_PIXPIPE) {
       for (int i = lane; i < npix; i += 64) {
         const int p = pix[i];
         const int row = ty0 + p / kTileW, col = tx0 + p % kTileW;
@@ -1329,6 +1337,10 @@ void k_vsd(VsdArgs a) {
         s_dep[0][ps] = 0u;  // clean for the next tile (rows are wave-private here)
         s_dep[1][ps] = 0u;
         if VSD_DIAG(4) atomicAdd(&g_vsd_stats[6], 1ull);
+        if constexpr (COST == kCostRender) {  // the pose's q into its ROI buffer
+          a.qbuf[a.qoff[b] + (int64_t)(row - ry0) * (rx1 - rx0 + 1) + (col - rx0)] = qg;
+          continue;
+        }
         if constexpr (COST == kCostCover) {  // silhouettes only (cus, cou_bb_proj)
           ++c_union;
           c_inter += (qe != 0u && qg != 0u);
@@ -1411,6 +1423,7 @@ void k_vsd(VsdArgs a) {
     }
   }
 
+  if constexpr (COST == kCostRender) return;  // the q buffer is the output
   // 4. workgroup reduction (fixed order) and the error formula (pose_error.py:75-91).
   __syncthreads();  // s_cnt / s_lin alias the depth tiles
   c_union = wave_sum_u32(c_union);
@@ -1622,8 +1635,23 @@ static void launch_vsd_rpt(const VsdArgs& a, int cost_type, hipStream_t s) {
     hipLaunchKernelGGL((k_vsd<1, RPT, kMaxTaus>), grid, block, 0, s, a);
   else if (cost_type == kCostCover)
     hipLaunchKernelGGL((k_vsd<kCostCover, RPT, kMaxTaus>), grid, block, 0, s, a);
+  else if (cost_type == kCostRender)
+    hipLaunchKernelGGL((k_vsd<kCostRender, RPT, kMaxTaus>), grid, block, 0, s, a);
   else
     hipLaunchKernelGGL((k_vsd<kCostGtInfo, RPT, kMaxTaus>), grid, block, 0, s, a);
+}
+
+// rectangle registers per thread (RPT) for the largest registered object
+static void launch_vsd_rpt_any(const VsdArgs& a, int cost_type, hipStream_t s) {
+  const int need = 2 * a.max_nm;
+  if (need <= kVsdThreads)
+    launch_vsd_rpt<1>(a, cost_type, s);
+  else if (need <= 2 * kVsdThreads)
+    launch_vsd_rpt<2>(a, cost_type, s);
+  else if (need <= kRectsPerThread * kVsdThreads)
+    launch_vsd_rpt<kRectsPerThread>(a, cost_type, s);
+  else
+    launch_vsd_rpt<0>(a, cost_type, s);  // rectangles recomputed per tile (any size)
 }
 
 hipError_t launch_vsd(const VsdArgs& a_in, int cost_type, hipStream_t s) {
@@ -1631,6 +1659,11 @@ hipError_t launch_vsd(const VsdArgs& a_in, int cost_type, hipStream_t s) {
   VsdArgs a = a_in;
   a.split = vsd_split(a.n, cost_type, a.split_from);
   a.part = nullptr;
+  // render mode: the splits write disjoint tiles of the q buffer, nothing to combine
+  if (a.split > 1 && cost_type == kCostRender) {
+    launch_vsd_rpt_any(a, cost_type, s);
+    return hipGetLastError();
+  }
   if (a.split > 1) {
     // stream-ordered scratch, freed behind the combine pass; without it the
     // launch keeps one workgroup per tuple
@@ -1643,15 +1676,7 @@ hipError_t launch_vsd(const VsdArgs& a_in, int cost_type, hipStream_t s) {
       a.split_from = 0;
     }
   }
-  const int need = 2 * a.max_nm;
-  if (need <= kVsdThreads)
-    launch_vsd_rpt<1>(a, cost_type, s);
-  else if (need <= 2 * kVsdThreads)
-    launch_vsd_rpt<2>(a, cost_type, s);
-  else if (need <= kRectsPerThread * kVsdThreads)
-    launch_vsd_rpt<kRectsPerThread>(a, cost_type, s);
-  else
-    launch_vsd_rpt<0>(a, cost_type, s);  // rectangles recomputed per tile (any size)
+  launch_vsd_rpt_any(a, cost_type, s);
   if (a.split > 1) {
     // the scratch is freed on every path (a failed launch skips the combine)
     hipError_t e = hipGetLastError();
@@ -1664,6 +1689,263 @@ hipError_t launch_vsd(const VsdArgs& a_in, int cost_type, hipStream_t s) {
     const hipError_t f = hipFreeAsync(a.part, s);
     return e != hipSuccess ? e : f;
   }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Shared renders (multi-instance images: an image with k instances of an object
+// and k estimates has k^2 (est, gt) tuples; the reference renders both poses
+// for every one of them, pose_error.py:42-45 under eval_calc_errors.py:281-290).
+// Each distinct pose is rasterised once (k_vsd<kCostRender>) into an HBM q
+// buffer over its ROI, then k_vsd_pair runs the VSD pixel pass of every tuple
+// on the two cached buffers: 2k renders instead of 2k^2. Same raster, same
+// per-pixel arithmetic and integer counts as the fused k_vsd: step-cost results
+// are bit-identical to it (tlinear sums change order, ~1e-13).
+
+// ROI of each render: the union of its pose's meshlet rectangles, clipped to
+// the image (exactly k_vsd's per-tuple ROI restricted to one pose).
+__global__ __launch_bounds__(256) void k_pose_roi(const ObjDesc* __restrict__ objs,
+                                                  const int32_t* __restrict__ slots,
+                                                  const double* __restrict__ pose,
+                                                  const int32_t* __restrict__ frame_idx,
+                                                  const double* __restrict__ cam, int W, int H,
+                                                  int4* __restrict__ rois) {
+  __shared__ float s_rf[12];
+  __shared__ int s_r[4];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const ObjDesc o = objs[slots[b]];
+  const int64_t fi = frame_idx[b];
+  Cam32 c32;
+  c32.fx = (float)cam[4 * fi + 0];
+  c32.fy = (float)cam[4 * fi + 1];
+  c32.cx = (float)(cam[4 * fi + 2] + 0.0);  // k_vsd: cx + ox, ox = 0 here
+  c32.cy = (float)(cam[4 * fi + 3] + 0.0);
+  if (tid < 12) s_rf[tid] = (float)pose[12 * b + tid];
+  if (tid == 0) {
+    s_r[0] = s_r[1] = 0x7FFFFFFF;
+    s_r[2] = s_r[3] = -1;
+  }
+  __syncthreads();
+  float rf[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) rf[k] = s_rf[k];
+  int r[4] = {INT32_MAX, INT32_MAX, -1, -1};
+  const gptr<const float> mlet = (gptr<const float>)o.mlet;
+  for (int m = tid; m < o.nm; m += 256) {
+    float zm, qb;
+    bool bk;
+    const short4 rc = meshlet_rect(mlet + kMletFloats * (int64_t)m, rf, c32, W, H, zm, qb, bk);
+    if (rc.x <= rc.z && rc.y <= rc.w) {
+      r[0] = min(r[0], (int)rc.x);
+      r[1] = min(r[1], (int)rc.y);
+      r[2] = max(r[2], (int)rc.z);
+      r[3] = max(r[3], (int)rc.w);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    r[0] = min(r[0], __shfl_xor(r[0], off, 64));
+    r[1] = min(r[1], __shfl_xor(r[1], off, 64));
+    r[2] = max(r[2], __shfl_xor(r[2], off, 64));
+    r[3] = max(r[3], __shfl_xor(r[3], off, 64));
+  }
+  if (lane == 0 && r[2] >= 0) {
+    atomicMin(&s_r[0], r[0]);
+    atomicMin(&s_r[1], r[1]);
+    atomicMax(&s_r[2], r[2]);
+    atomicMax(&s_r[3], r[3]);
+  }
+  __syncthreads();
+  if (tid == 0) rois[b] = s_r[2] >= 0 ? make_int4(s_r[0], s_r[1], s_r[2], s_r[3])
+                                      : make_int4(0, 0, -1, -1);  // empty
+}
+
+hipError_t launch_pose_roi(const ObjDesc* objs, int64_t n, const int32_t* slots,
+                           const double* pose, const int32_t* frame_idx, const double* cam, int W,
+                           int H, int4* rois, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pose_roi, dim3((unsigned)n), dim3(256), 0, s, objs, slots, pose, frame_idx,
+                     cam, W, H, rois);
+  return hipGetLastError();
+}
+
+// The VSD pixel pass of one (est, gt) tuple on two cached q buffers: one
+// 256-thread workgroup per tuple sweeps the union of the two ROIs, wave w
+// taking rows w, w + 4, ... and lanes the columns (a fixed pixel -> lane map:
+// deterministic float64 sums), with the fused kernel's per-pixel arithmetic.
+constexpr int kPairThreads = 256;
+constexpr int kPairWaves = kPairThreads / 64;
+constexpr int kPairCols = 2048;  // column coefficients staged in LDS per block of columns
+
+template <int COST, int NT>
+__global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {
+  __shared__ double s_pX[kPairCols];
+  __shared__ double s_thr[kMaxTaus];
+  __shared__ uint32_t s_cnt[kPairWaves][2 + kMaxTaus];
+  __shared__ double s_lin[kPairWaves][kMaxTaus];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int re = a.est_r[b], rg = a.gt_r[b];
+  if ((uint64_t)re >= (uint64_t)a.n_renders || (uint64_t)rg >= (uint64_t)a.n_renders) {
+    // bad render index (the _dev entry cannot check on the host): NaN errors
+    if (tid < a.n_tau) a.out[b * (int64_t)a.n_tau + tid] = __builtin_nan("");
+    if (tid == 0 && a.unions) a.unions[b] = __builtin_nan("");
+    return;
+  }
+  const int4 Re = a.rois[re], Rg = a.rois[rg];
+  const int64_t oe = a.qoff[re], og = a.qoff[rg];
+  const int we = Re.z - Re.x + 1, wg = Rg.z - Rg.x + 1;
+  const int64_t fidx = a.rframe[rg];
+  const int W = a.width, H = a.height;
+  const gptr<const float> frame = (gptr<const float>)(a.frames + fidx * (int64_t)W * H);
+  const gptr<const uint32_t> qbuf = (gptr<const uint32_t>)a.qbuf;
+  const double fx = a.cam[4 * fidx + 0], fy = a.cam[4 * fidx + 1];
+  const double cx = a.cam[4 * fidx + 2], cy = a.cam[4 * fidx + 3];
+  const double diam = COST == 0 && a.normalized ? a.diameters[b] : 1.0;
+  bool divide = false;
+  if constexpr (COST == 0) {  // step thresholds as in k_vsd
+    bool fast = a.normalized && diam > 0.0 && diam <= DBL_MAX;
+    for (int k = 0; k < a.n_tau; ++k) fast = fast && a.taus[k] == a.taus[k];
+    divide = a.normalized && !fast;
+    if (tid < NT) {
+      double T = INFINITY;
+      if (tid < a.n_tau) T = fast ? step_threshold(a.taus[tid], diam) : a.taus[tid];
+      s_thr[tid] = T;
+    }
+  }
+  // union of the two ROIs (an empty ROI has x0 > x1)
+  const bool ee = Re.x > Re.z, ge = Rg.x > Rg.z;
+  const int ux0 = ee ? Rg.x : (ge ? Re.x : min(Re.x, Rg.x));
+  const int uy0 = ee ? Rg.y : (ge ? Re.y : min(Re.y, Rg.y));
+  const int ux1 = ee ? Rg.z : (ge ? Re.z : max(Re.z, Rg.z));
+  const int uy1 = ee ? Rg.w : (ge ? Re.w : max(Re.w, Rg.w));
+  __syncthreads();
+  double thr[NT];
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    const double v = COST == 0 ? s_thr[k] : 0.0;
+    thr[k] = __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                              __builtin_amdgcn_readfirstlane(__double2loint(v)));
+  }
+  uint32_t c_union = 0, c_inter = 0;
+  uint32_t c_tau[(NT + 1) / 2];
+  double lin[kMaxTaus];
+#pragma unroll
+  for (int k = 0; k < kMaxTaus; ++k) {
+    if (k < (NT + 1) / 2) c_tau[k] = 0;
+    lin[k] = 0.0;
+  }
+  for (int cb = ux0; cb <= ux1; cb += kPairCols) {  // blocks of columns (wide images)
+    const int cb1 = min(cb + kPairCols - 1, ux1);
+    __syncthreads();  // the previous block's coefficients are consumed
+    for (int i = tid; i <= cb1 - cb; i += kPairThreads) s_pX[i] = ((double)(cb + i) - cx) / fx;
+    __syncthreads();
+    for (int row = uy0 + wave; row <= uy1; row += kPairWaves) {
+      const double pY = ((double)row - cy) / fy;  // misc.py:137-138, as k_vsd's w_pY
+      const bool rin_e = row >= Re.y && row <= Re.w, rin_g = row >= Rg.y && row <= Rg.w;
+      for (int col = cb + lane; col <= cb1; col += 64) {
+        const uint32_t qe = rin_e && col >= Re.x && col <= Re.z
+                                ? qbuf[oe + (int64_t)(row - Re.y) * we + (col - Re.x)]
+                                : 0u;
+        const uint32_t qg = rin_g && col >= Rg.x && col <= Rg.z
+                                ? qbuf[og + (int64_t)(row - Rg.y) * wg + (col - Rg.x)]
+                                : 0u;
+        if ((qe | qg) == 0u) continue;
+        const float dtest = frame[(int64_t)row * W + col];
+        const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
+        const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
+        const double pX = s_pX[col - cb];
+        const double dist_t = dist_of(pX, pY, dtest);
+        const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
+        const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
+        const bool vg = visib19t(dist_t, dist_g, a.dthr);
+        bool ve = visib19t(dist_t, dist_e, a.dthr);
+        ve = ve || (vg && dist_e > 0.0);  // visibility.py:74
+        c_union += (vg || ve);
+        if (vg && ve) {
+          ++c_inter;
+          double dd = fabs(dist_g - dist_e);
+          if constexpr (COST == 0) {
+            if (divide) {
+              dd /= diam;
+              asm volatile("" : "+v"(dd));
+            }
+#pragma unroll
+            for (int k = 0; k < NT; ++k) c_tau[k >> 1] += (uint32_t)(dd >= thr[k]) << (16 * (k & 1));
+          } else {
+            if (a.normalized) dd /= a.diameters[b];
+#pragma unroll
+            for (int k = 0; k < kMaxTaus; ++k) {
+              if (k < a.n_tau) {
+                const double cst = dd / a.taus[k];
+                lin[k] += cst > 1.0 ? 1.0 : cst;
+              }
+            }
+          }
+        }
+      }
+      // 16-bit per-lane tau counters: a lane sees at most (w/64 + 1)(h/4 + 1)
+      // pixels of a w x h union, < 42k for any image within the fused kernel's
+      // kVsdMaxTiles (w h <= 2048 x 4096, w, h <= 32767; fill_vsd_args checks it)
+    }
+  }
+  c_union = wave_sum_u32(c_union);
+  c_inter = wave_sum_u32(c_inter);
+  uint32_t tau_sum[kMaxTaus];
+#pragma unroll
+  for (int k = 0; k < kMaxTaus; ++k) {
+    tau_sum[k] = 0;
+    if (COST == 0) {
+      if (k < NT) tau_sum[k] = wave_sum_u32((c_tau[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+    } else {
+      lin[k] = wave_sum_f64(lin[k]);
+    }
+  }
+  if (lane == 0) {
+    s_cnt[wave][0] = c_union;
+    s_cnt[wave][1] = c_inter;
+#pragma unroll
+    for (int k = 0; k < kMaxTaus; ++k) {
+      s_cnt[wave][2 + k] = tau_sum[k];
+      s_lin[wave][k] = lin[k];
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t un = 0, in = 0;
+    for (int w = 0; w < kPairWaves; ++w) {
+      un += s_cnt[w][0];
+      in += s_cnt[w][1];
+    }
+    if (a.unions) a.unions[b] = (double)un;
+    double* out = a.out + b * (int64_t)a.n_tau;
+    for (int k = 0; k < a.n_tau; ++k) {
+      if (un == 0) {
+        out[k] = 1.0;
+      } else if (COST == 0) {
+        uint64_t cnt = 0;
+        for (int w = 0; w < kPairWaves; ++w) cnt += s_cnt[w][2 + k];
+        out[k] = (double)(cnt + (un - in)) / (double)un;
+      } else {
+        double sum = 0.0;
+        for (int w = 0; w < kPairWaves; ++w) sum += s_lin[w][k];
+        out[k] = (sum + (double)(un - in)) / (double)un;
+      }
+    }
+  }
+}
+
+hipError_t launch_vsd_pair(const PairArgs& a, int cost_type, hipStream_t s) {
+  if (a.n <= 0) return hipSuccess;
+  const dim3 grid((unsigned)a.n), block(kPairThreads);
+  if (cost_type == 0 && a.n_tau <= kBopTaus)
+    hipLaunchKernelGGL((k_vsd_pair<0, kBopTaus>), grid, block, 0, s, a);
+  else if (cost_type == 0)
+    hipLaunchKernelGGL((k_vsd_pair<0, kMaxTaus>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((k_vsd_pair<1, kMaxTaus>), grid, block, 0, s, a);
   return hipGetLastError();
 }
 

@@ -1075,6 +1075,179 @@ int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double*
   return BOPX_OK;
 }
 
+// -------------------------------------------------------------- shared renders
+// VSD of many (est, gt) tuples over a set of distinct renders (multi-instance
+// images: k estimates x k GT instances of an object share 2k renders instead of
+// 2k^2). Device pointers, stream s; one host synchronisation (the ROI sizes
+// decide the q buffer layout).
+static int vsd_shared_core(bopx_ctx* c, int64_t nr, const int32_t* rslots, const double* rpose,
+                           const int32_t* rframe, int64_t n, const int32_t* est_r,
+                           const int32_t* gt_r, const float* frames, int width, int height,
+                           const double* cam, double delta, int flags, const double* taus,
+                           int n_tau, int normalized, const double* dia, int cost_type,
+                           double* out, hipStream_t s) {
+  bopx::VsdArgs a{};
+  a.cull = vsd_cull_enabled();
+  a.qorder = vsd_queue_order();
+  if (int r = fill_vsd_args(c, a, width, height, delta, flags, taus, n_tau, normalized,
+                            cost_type))
+    return r;
+  if (n <= 0 || nr <= 0) return BOPX_OK;
+  int4* d_roi = nullptr;
+  int64_t* d_off = nullptr;
+  uint32_t* d_q = nullptr;
+  HIPCHK(c, hipMallocAsync((void**)&d_roi, (size_t)nr * (sizeof(int4) + sizeof(int64_t)), s));
+  d_off = reinterpret_cast<int64_t*>(d_roi + nr);
+  int rc = BOPX_OK;
+  std::vector<int4> roi((size_t)nr);
+  std::vector<int64_t> off((size_t)nr);
+  int64_t total = 0;
+  hipError_t e = bopx::launch_pose_roi(c->d_desc, nr, rslots, rpose, rframe, cam, width, height,
+                                       d_roi, s);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(roi.data(), d_roi, (size_t)nr * sizeof(int4), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) {
+    for (int64_t i = 0; i < nr; ++i) {
+      off[i] = total;
+      const int4 r = roi[i];
+      if (r.x <= r.z && r.y <= r.w) total += (int64_t)(r.z - r.x + 1) * (r.w - r.y + 1);
+    }
+    e = hipMemcpyAsync(d_off, off.data(), (size_t)nr * sizeof(int64_t), hipMemcpyHostToDevice, s);
+  }
+  if (e == hipSuccess) e = hipMallocAsync((void**)&d_q, (size_t)std::max<int64_t>(total, 1) * 4, s);
+  if (e == hipSuccess) e = hipMemsetAsync(d_q, 0, (size_t)std::max<int64_t>(total, 1) * 4, s);
+  if (e == hipSuccess) {
+    a.objs = c->d_desc;
+    a.max_nm = c->max_nm;
+    a.slots = rslots;
+    a.pose_est = rpose;
+    a.pose_gt = rpose;
+    a.frame_idx = rframe;
+    a.frames = frames;
+    a.cam = cam;
+    a.rois = d_roi;
+    a.qoff = d_off;
+    a.qbuf = d_q;
+    a.n = nr;
+    LaunchOrder ord;
+    rc = make_order(c, nr, rslots, s, ord);
+    if (rc == BOPX_OK) {
+      a.order = ord.p;
+      e = bopx::launch_vsd(a, bopx::kCostRender, s);
+    }
+  }
+  if (rc == BOPX_OK && e == hipSuccess) {
+    bopx::PairArgs p{};
+    p.rois = d_roi;
+    p.qoff = d_off;
+    p.qbuf = d_q;
+    p.rframe = rframe;
+    p.est_r = est_r;
+    p.gt_r = gt_r;
+    p.n_renders = nr;
+    p.frames = frames;
+    p.cam = cam;
+    p.diameters = dia;
+    p.out = out;
+    p.unions = (flags & BOPX_VSD_UNIONS) ? out + n * n_tau : nullptr;
+    p.n = n;
+    p.width = width;
+    p.height = height;
+    p.dthr = a.dthr;
+    p.n_tau = n_tau;
+    p.normalized = a.normalized;
+    for (int k = 0; k < bopx::kMaxTaus; ++k) p.taus[k] = a.taus[k];
+    e = bopx::launch_vsd_pair(p, cost_type, s);
+  }
+  // scratch freed on every path, behind the launches that read it
+  const hipError_t f1 = d_q ? hipFreeAsync(d_q, s) : hipSuccess;
+  const hipError_t f2 = hipFreeAsync(d_roi, s);
+  if (rc != BOPX_OK) return rc;
+  HIPCHK(c, e);
+  HIPCHK(c, f1);
+  HIPCHK(c, f2);
+  return BOPX_OK;
+}
+
+int bopx_vsd_shared_batch_dev(bopx_ctx* c, int64_t n_renders, const int32_t* render_slots,
+                              const double* render_poses, const int32_t* render_frame_idx,
+                              int64_t n, const int32_t* est_render, const int32_t* gt_render,
+                              const float* frames, int width, int height, const double* cam,
+                              double delta, int flags, const double* taus, int n_tau,
+                              int normalized, const double* diameters, int cost_type,
+                              double* out, void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (n < 0 || n_renders < 0) return fail(c, BOPX_E_INVALID, "negative size");
+  if (int r = set_dev(c)) return r;
+  return vsd_shared_core(c, n_renders, render_slots, render_poses, render_frame_idx, n,
+                         est_render, gt_render, frames, width, height, cam, delta, flags, taus,
+                         n_tau, normalized, diameters, cost_type, out, pick_stream(c, stream));
+}
+
+int bopx_vsd_shared_batch(bopx_ctx* c, int64_t n_renders, const int32_t* render_obj_ids,
+                          const double* render_poses, const int32_t* render_frame_idx, int64_t n,
+                          const int32_t* est_render, const int32_t* gt_render,
+                          const float* frames, int64_t n_frames, int width, int height,
+                          const double* cam, double delta, int flags, const double* taus,
+                          int n_tau, int normalized, const double* diameters, int cost_type,
+                          double* out) {
+  if (!c) return BOPX_E_INVALID;
+  if (n < 0 || n_renders < 0 || n_frames < 0) return fail(c, BOPX_E_INVALID, "negative size");
+  if (n == 0) return BOPX_OK;
+  if (!render_obj_ids || !render_poses || !render_frame_idx || !est_render || !gt_render ||
+      !frames || !cam || !diameters || !out)
+    return fail(c, BOPX_E_INVALID, "NULL buffer");
+  for (int64_t i = 0; i < n_renders; ++i)
+    if (render_frame_idx[i] < 0 || render_frame_idx[i] >= n_frames)
+      return fail(c, BOPX_E_INVALID, "render_frame_idx[%lld] = %d out of range", (long long)i,
+                  render_frame_idx[i]);
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t e = est_render[i], g = gt_render[i];
+    if (e < 0 || e >= n_renders || g < 0 || g >= n_renders)
+      return fail(c, BOPX_E_INVALID, "tuple %lld: render index out of range", (long long)i);
+    if (render_frame_idx[e] != render_frame_idx[g])
+      return fail(c, BOPX_E_INVALID, "tuple %lld: est and gt renders of different frames",
+                  (long long)i);
+  }
+  if (int r = set_dev(c)) return r;
+  std::vector<int32_t> slots;
+  if (int r = map_slots(c, n_renders, render_obj_ids, slots, false, true)) return r;
+  const size_t fbytes = (size_t)n_frames * width * height * sizeof(float);
+  const size_t n_out = (size_t)n * n_tau + ((flags & BOPX_VSD_UNIONS) ? (size_t)n : 0);
+  const size_t nr = (size_t)n_renders;
+  if (int r = ws_reserve(c, carve_size({4 * nr, 96 * nr, 4 * nr, 4 * (size_t)n, 4 * (size_t)n,
+                                        32 * (size_t)n_frames, 8 * (size_t)n, fbytes,
+                                        8 * n_out})))
+    return r;
+  Carve cv{(char*)c->ws.p};
+  int32_t* d_rs = cv.take<int32_t>(nr);
+  double* d_rp = cv.take<double>(12 * nr);
+  int32_t* d_rf = cv.take<int32_t>(nr);
+  int32_t* d_e = cv.take<int32_t>(n);
+  int32_t* d_g = cv.take<int32_t>(n);
+  double* d_cam = cv.take<double>(4 * n_frames);
+  double* d_dia = cv.take<double>(n);
+  float* d_fr = cv.take<float>((size_t)n_frames * width * height);
+  double* d_out = cv.take<double>(n_out);
+  hipStream_t s = c->stream;
+  HIPCHK(c, hipMemcpyAsync(d_rs, slots.data(), 4 * nr, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_rp, render_poses, 96 * nr, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_rf, render_frame_idx, 4 * nr, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_e, est_render, 4 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_g, gt_render, 4 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_cam, cam, 32 * n_frames, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_dia, diameters, 8 * n, hipMemcpyHostToDevice, s));
+  HIPCHK(c, hipMemcpyAsync(d_fr, frames, fbytes, hipMemcpyHostToDevice, s));
+  if (int r = vsd_shared_core(c, n_renders, d_rs, d_rp, d_rf, n, d_e, d_g, d_fr, width, height,
+                              d_cam, delta, flags, taus, n_tau, normalized, d_dia, cost_type,
+                              d_out, s))
+    return r;
+  HIPCHK(c, hipMemcpyAsync(out, d_out, 8 * n_out, hipMemcpyDeviceToHost, s));
+  HIPCHK(c, hipStreamSynchronize(s));
+  return BOPX_OK;
+}
+
 // ----------------------------------------------------------- silhouette cover
 static int cover_args(bopx_ctx* c, bopx::VsdArgs& a, int width, int height) {
   if (width <= 0 || height <= 0 || width > 32767 || height > 32767)

@@ -52,6 +52,10 @@ DEFAULTS = {
 }
 
 POINT_ERRORS = ("ad", "add", "adi", "mssd", "mspd", "proj")
+# VSD batches whose distinct renders number at most this times the tuples take
+# the shared-render path (batch.BatchEvaluator.vsd_shared); one instance per
+# object (2 renders per tuple) keeps the fused per-tuple kernel
+SHARED_RENDER_RATIO = float(os.environ.get("BOPX_SHARED_RENDER_RATIO", "1.5"))
 ERROR_TYPES = ("vsd", "mssd", "mspd", "ad", "add", "adi", "cus", "proj", "rete", "re", "te")
 
 
@@ -276,8 +280,8 @@ def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs
     frame_of = {im: k for k, im in enumerate(ims)}
     cam = np.array([[K[0, 0], K[1, 1], K[0, 2], K[1, 2]]
                     for K in (scene_camera[im]["cam_K"] for im in ims)], np.float64)
-    fidx = T(np.array([frame_of[recs[ri]["im_id"]] for ri, _, _, _ in todo], np.int32),
-             torch.int32)
+    fidx_h = np.array([frame_of[recs[ri]["im_id"]] for ri, _, _, _ in todo], np.int32)
+    fidx = T(fidx_h, torch.int32)
     if et == "cus":
       W, H = dp_split["im_size"]
       return ev.cover(slots, d_pe, d_pg, fidx, T(cam, torch.float64), W, H)
@@ -289,6 +293,16 @@ def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs
     dia = np.array([models_info[o]["diameter"] for o in obj], np.float64)
     delta = p["vsd_deltas"][dataset]
     from . import runtime
+    from .batch import unique_renders
+    # multi-instance images (every estimate x every GT instance of its object,
+    # :281-290): each distinct pose rendered once when that saves renders
+    ro, rp, rf, er, gr = unique_renders(obj, pe, pg, fidx_h)
+    if len(ro) <= SHARED_RENDER_RATIO * n:
+      return ev.vsd_shared(ev.slots(ro), T(rp, torch.float64), T(rf, torch.int32),
+                           T(er, torch.int32), T(gr, torch.int32), d_frames,
+                           T(cam, torch.float64), delta, p["vsd_taus"], T(dia, torch.float64),
+                           normalized_by_diameter=p["vsd_normalized_by_diameter"],
+                           cost_type="step", delta_flags=runtime.delta_flags(delta))
     return ev.vsd(slots, d_pe, d_pg, fidx, d_frames,
                   T(cam, torch.float64), delta, p["vsd_taus"], T(dia, torch.float64),
                   normalized_by_diameter=p["vsd_normalized_by_diameter"], cost_type="step",

@@ -129,6 +129,25 @@ int bopx_vsd_batch(bopx_ctx* ctx, int64_t n, const int32_t* obj_ids,
                    const double* taus, int n_tau, int normalized_by_diameter,
                    const double* diameters, int cost_type, double* out);
 
+/* vsd with shared renders: pose_error.py:17-93 for n (est, gt) tuples whose
+ * poses come from a list of distinct renders (obj_id, pose 12, frame). The
+ * reference renders both poses of every tuple (pose_error.py:42-45), and
+ * eval_calc_errors.py:281-290 pairs every estimate with every GT instance of
+ * its object, so an image with k instances and k estimates costs 2k^2 renders
+ * there; here each render is rasterised once (2k) into an HBM depth buffer over
+ * its ROI and every tuple runs the VSD pixel pass on its two buffers.
+ * est_render / gt_render: n indices into the render list (both renders of a
+ * tuple must use the same frame); everything else as bopx_vsd_batch. Step-cost
+ * results are bit-identical to bopx_vsd_batch on the same tuples (tlinear:
+ * float64 sums in another order, ~1e-13). */
+int bopx_vsd_shared_batch(bopx_ctx* ctx, int64_t n_renders, const int32_t* render_obj_ids,
+                          const double* render_poses, const int32_t* render_frame_idx,
+                          int64_t n, const int32_t* est_render, const int32_t* gt_render,
+                          const float* frames, int64_t n_frames, int width, int height,
+                          const double* cam, double delta, int flags, const double* taus,
+                          int n_tau, int normalized_by_diameter, const double* diameters,
+                          int cost_type, double* out);
+
 /* vsd given already-rendered depth maps (for foreign renderers, e.g. a
  * reference vispy/cpp renderer passed to pose_error.vsd). All maps h x w f32. */
 int bopx_vsd_from_depths(bopx_ctx* ctx, int width, int height, const float* depth_test,
@@ -209,6 +228,17 @@ int bopx_vsd_batch_dev(bopx_ctx* ctx, int64_t n, const int32_t* slots,
                        const double* taus, int n_tau, int normalized_by_diameter,
                        const double* diameters, int cost_type, double* out,
                        void* stream);
+/* bopx_vsd_shared_batch on device pointers (render_slots: object slots). It
+ * synchronises `stream` once (the renders' ROI sizes lay out the depth
+ * buffers, stream-ordered scratch); render indices outside [0, n_renders) give
+ * NaN errors for that tuple. */
+int bopx_vsd_shared_batch_dev(bopx_ctx* ctx, int64_t n_renders, const int32_t* render_slots,
+                              const double* render_poses, const int32_t* render_frame_idx,
+                              int64_t n, const int32_t* est_render, const int32_t* gt_render,
+                              const float* frames, int width, int height, const double* cam,
+                              double delta, int flags, const double* taus, int n_tau,
+                              int normalized_by_diameter, const double* diameters,
+                              int cost_type, double* out, void* stream);
 int bopx_cover_batch_dev(bopx_ctx* ctx, int64_t n, const int32_t* slots,
                          const double* pose_est, const double* pose_gt,
                          const int32_t* frame_idx, int width, int height, const double* cam,

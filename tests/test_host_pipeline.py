@@ -96,3 +96,32 @@ def test_save_json_per_value_bytes(tmp_path):
   inout.save_json_per_value([str(tmp_path / "e.json")], [], 1)
   inout.save_json(str(tmp_path / "re.json"), [])
   assert open(tmp_path / "e.json").read() == open(tmp_path / "re.json").read()
+
+
+def test_unique_renders_dedupes_bitwise():
+  """batch.unique_renders: one render per distinct (object, frame, float64 pose
+  bits); estimates equal to a GT share its render."""
+  from bop_toolkit_amd.batch import unique_renders
+  rng = np.random.default_rng(3)
+  g = rng.normal(size=(3, 12))
+  e = rng.normal(size=(3, 12))
+  e[0] = g[1]
+  pe = np.repeat(e, 3, 0)  # every estimate x every GT
+  pg = np.tile(g, (3, 1))
+  obj = np.zeros(9, np.int32)
+  fi = np.zeros(9, np.int32)
+  ro, rp, rf, er, gr = unique_renders(obj, pe, pg, fi)
+  assert len(ro) == 5  # 3 GT + 2 new estimates
+  assert np.array_equal(rp[er], pe) and np.array_equal(rp[gr], pg)
+  # another frame or object: separate renders
+  fi2 = fi.copy()
+  fi2[:3] = 1
+  ro2, rp2, rf2, er2, gr2 = unique_renders(obj, pe, pg, fi2)
+  assert len(ro2) > len(ro) and np.array_equal(rf2[er2], fi2) and np.array_equal(rf2[gr2], fi2)
+  # -0.0 and 0.0 are different bits: kept apart (the raster sees float32 values
+  # that are equal, but a render is keyed by what the caller passed)
+  pz = pg.copy()
+  pz[0, 9] = 0.0
+  pz2 = pz.copy()
+  pz2[0, 9] = -0.0
+  assert len(unique_renders(obj[:1], pz[:1], pz2[:1], fi[:1])[0]) == 2
