@@ -114,6 +114,10 @@ struct VsdArgs {
   const int4* rois;
   const int64_t* qoff;
   uint32_t* qbuf;
+  // ... and per ROI row the covered column span [smin, smax] (empty: INT_MAX, -1)
+  const int64_t* rowoff;
+  int32_t* smin;
+  int32_t* smax;
   double taus[kMaxTaus];
 };
 constexpr int kVsdPartCols = 2 + 2 * kMaxTaus;  // union, inter, cnt[kMaxTaus], lin[kMaxTaus]
@@ -159,6 +163,9 @@ struct PairArgs {
   const int4* rois;        // per render
   const int64_t* qoff;     // per render: offset of its q buffer in qbuf (dwords)
   const uint32_t* qbuf;    // q = 1/Z bits, 0 = background
+  const int64_t* rowoff;   // per render: offset of its row spans in smin / smax
+  const int32_t* smin;     // per ROI row: first / last covered column (INT_MAX / -1: none)
+  const int32_t* smax;
   const int32_t* rframe;   // per render: frame index
   const int32_t* est_r;    // per tuple: render of the estimate
   const int32_t* gt_r;     // per tuple: render of the GT

@@ -1096,12 +1096,13 @@ static int vsd_shared_core(bopx_ctx* c, int64_t nr, const int32_t* rslots, const
   int4* d_roi = nullptr;
   int64_t* d_off = nullptr;
   uint32_t* d_q = nullptr;
-  HIPCHK(c, hipMallocAsync((void**)&d_roi, (size_t)nr * (sizeof(int4) + sizeof(int64_t)), s));
+  HIPCHK(c, hipMallocAsync((void**)&d_roi, (size_t)nr * (sizeof(int4) + 2 * sizeof(int64_t)), s));
   d_off = reinterpret_cast<int64_t*>(d_roi + nr);
+  int64_t* d_roff = d_off + nr;
   int rc = BOPX_OK;
   std::vector<int4> roi((size_t)nr);
-  std::vector<int64_t> off((size_t)nr);
-  int64_t total = 0;
+  std::vector<int64_t> off(2 * (size_t)nr);  // q offsets, then row-span offsets
+  int64_t total = 0, rows = 0;
   hipError_t e = bopx::launch_pose_roi(c->d_desc, nr, rslots, rpose, rframe, cam, width, height,
                                        d_roi, s);
   if (e == hipSuccess)
@@ -1110,13 +1111,24 @@ static int vsd_shared_core(bopx_ctx* c, int64_t nr, const int32_t* rslots, const
   if (e == hipSuccess) {
     for (int64_t i = 0; i < nr; ++i) {
       off[i] = total;
+      off[nr + i] = rows;
       const int4 r = roi[i];
-      if (r.x <= r.z && r.y <= r.w) total += (int64_t)(r.z - r.x + 1) * (r.w - r.y + 1);
+      if (r.x <= r.z && r.y <= r.w) {
+        total += (int64_t)(r.z - r.x + 1) * (r.w - r.y + 1);
+        rows += r.w - r.y + 1;
+      }
     }
-    e = hipMemcpyAsync(d_off, off.data(), (size_t)nr * sizeof(int64_t), hipMemcpyHostToDevice, s);
+    e = hipMemcpyAsync(d_off, off.data(), 2 * (size_t)nr * sizeof(int64_t),
+                       hipMemcpyHostToDevice, s);
   }
-  if (e == hipSuccess) e = hipMallocAsync((void**)&d_q, (size_t)std::max<int64_t>(total, 1) * 4, s);
-  if (e == hipSuccess) e = hipMemsetAsync(d_q, 0, (size_t)std::max<int64_t>(total, 1) * 4, s);
+  // q buffers (0 = background), then the row spans: min 0x7F7F7F7F, max -1
+  const size_t qn = (size_t)std::max<int64_t>(total, 1), sn = (size_t)std::max<int64_t>(rows, 1);
+  if (e == hipSuccess) e = hipMallocAsync((void**)&d_q, 4 * (qn + 2 * sn), s);
+  if (e == hipSuccess) e = hipMemsetAsync(d_q, 0, 4 * qn, s);
+  int32_t* d_smin = reinterpret_cast<int32_t*>(d_q + qn);
+  int32_t* d_smax = d_smin + sn;
+  if (e == hipSuccess) e = hipMemsetAsync(d_smin, 0x7F, 4 * sn, s);
+  if (e == hipSuccess) e = hipMemsetAsync(d_smax, 0xFF, 4 * sn, s);
   if (e == hipSuccess) {
     a.objs = c->d_desc;
     a.max_nm = c->max_nm;
@@ -1129,6 +1141,9 @@ static int vsd_shared_core(bopx_ctx* c, int64_t nr, const int32_t* rslots, const
     a.rois = d_roi;
     a.qoff = d_off;
     a.qbuf = d_q;
+    a.rowoff = d_roff;
+    a.smin = d_smin;
+    a.smax = d_smax;
     a.n = nr;
     LaunchOrder ord;
     rc = make_order(c, nr, rslots, s, ord);
@@ -1142,6 +1157,9 @@ static int vsd_shared_core(bopx_ctx* c, int64_t nr, const int32_t* rslots, const
     p.rois = d_roi;
     p.qoff = d_off;
     p.qbuf = d_q;
+    p.rowoff = d_roff;
+    p.smin = d_smin;
+    p.smax = d_smax;
     p.rframe = rframe;
     p.est_r = est_r;
     p.gt_r = gt_r;
