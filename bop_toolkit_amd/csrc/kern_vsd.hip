@@ -470,6 +470,9 @@ constexpr int kCullAutoDensity = 12;  // ... and at least this many meshlets per
 #ifndef BOPX_VSD_EARLY_RESET
 #define BOPX_VSD_EARLY_RESET 0
 #endif
+#ifndef BOPX_VSD_LIST_AHEAD
+#define BOPX_VSD_LIST_AHEAD 1
+#endif
 #ifndef BOPX_VSD_XLAT
 #define BOPX_VSD_XLAT 0
 #endif
@@ -519,21 +522,25 @@ void k_vsd(VsdArgs a) {
   constexpr bool kCull = RPT >= 1 && RPT <= 2;
   constexpr int kListLen = kR * kVsdThreads;  // >= 2 * nm (launch_vsd) unless kStream
   using ListT = typename std::conditional<kCull, uint32_t, uint16_t>::type;
-  __shared__ __attribute__((aligned(4))) ListT s_list[kListLen];
+  // list-ahead (BOPX_VSD_LIST_AHEAD, objects of <= 256 meshlets): two queues,
+  // the next tile's listed by each wave in the current tile's raster tail
+  constexpr bool kAhead = BOPX_VSD_LIST_AHEAD && !kStream && RPT == 1;
+  constexpr int kQueues = kAhead ? 2 : 1;
+  __shared__ __attribute__((aligned(4))) ListT s_lists[kQueues][kListLen];
   // Back-face occlusion test (cull 3): per entry, its fragment bound qb as an
   // 8-bit code below the pose's largest bound: qb <= s_qhi[pose] 2^(-code/64).
   __shared__ uint8_t s_qb[kCull ? kListLen : 4];
   __shared__ float s_qhi[2];
   __shared__ float s_zr[2][2];  // per pose: depth range of the meshlet corners (min, max)
-  __shared__ int s_next;
+  __shared__ int s_nexts[kQueues];
 #if BOPX_VSD_LDSPAD
   __shared__ uint8_t s_pad[BOPX_VSD_LDSPAD];
   if (threadIdx.x == 0) asm volatile("" ::"v"(s_pad + blockIdx.x % 7));
 #endif
   __shared__ __attribute__((aligned(16))) float s_pose[2][12];
   __shared__ int s_roi[4];
-  __shared__ int s_nlist;
-  __shared__ int s_nsmall;
+  __shared__ int s_nlists[kQueues];
+  __shared__ int s_nsmalls[kQueues];
   __shared__ double s_thr[kMaxTaus];  // step-cost thresholds (T_k, +inf past n_tau)
   // Final per-wave partial counters reuse the depth tiles (after the tile loop).
   uint32_t(*s_cnt)[2 + kMaxTaus] = reinterpret_cast<uint32_t(*)[2 + kMaxTaus]>(&s_dep[0][0]);
@@ -598,9 +605,11 @@ void k_vsd(VsdArgs a) {
     }
   }
   if (tid == 0) {
-    s_nlist = 0;  // tile queue counters (reset again behind each raster-end barrier)
-    s_nsmall = 0;
-    s_next = kVsdFirstClaim;
+    for (int q = 0; q < kQueues; ++q) {  // tile queue counters (reset again per tile)
+      s_nlists[q] = 0;
+      s_nsmalls[q] = 0;
+      s_nexts[q] = kVsdFirstClaim;
+    }
     s_roi[0] = s_roi[1] = 0x7FFFFFFF;
     s_roi[2] = s_roi[3] = -1;
     s_zr[0][0] = s_zr[1][0] = INFINITY;
@@ -765,25 +774,12 @@ void k_vsd(VsdArgs a) {
     const int ntx = (rx1 - rx0 + kTileW) / kTileW, nty = (ry1 - ry0 + kTileH) / kTileH;
     if (VSD_DIAG(4) && tid == 0) atomicAdd(&g_vsd_stats[0], (unsigned long long)(ntx * nty));
     VSD_STAMP(6);
-    for (int t = sp; t < ntx * nty; t += S) {
-      const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
-      const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
-      // 2a. list the (pose, meshlet) entries touching the tile (the q tiles are
-      // already zero, see the pixel pass). The queue counters were reset behind
-      // the previous tile's raster-end barrier (or before the loop), so no
-      // barrier is needed here: the previous tile's pixel-end barrier orders it.
-      // kStream: one round per kListLen entries (a single round otherwise)
-      for (int e0 = 0; e0 < (kStream ? 2 * nm : 1); e0 += kListLen) {
-      if (kStream && e0 > 0) __syncthreads();  // every wave is done with the last round's queue
-      if (!BOPX_VSD_EARLY_RESET || kStream) {
-        if (tid == 0) {
-          s_nlist = 0;
-          s_nsmall = 0;
-          s_next = kVsdFirstClaim;
-        }
-        __syncthreads();
-      }
-      VSD_STAMP(0);
+    // 2a. list the (pose, meshlet) entries touching tile tt into queue qb (the
+    // q tiles are already zero, see the pixel pass): each thread its kR
+    // rectangles (kStream: round e0, recomputed)
+    auto list_tile = [&](int tt, int qb, int e0) {
+      const int lx0 = rx0 + (tt % ntx) * kTileW, ly0 = ry0 + (tt / ntx) * kTileH;
+      const int lx1 = min(lx0 + kTileW - 1, rx1), ly1 = min(ly0 + kTileH - 1, ry1);
 #pragma unroll
       for (int j = 0; j < kR; ++j) {
         short4 rc;
@@ -799,44 +795,71 @@ void k_vsd(VsdArgs a) {
         } else {
           rc = rect[j];
         }
-        if (rc.x <= tx1 && rc.z >= tx0 && rc.y <= ty1 && rc.w >= ty0 && rc.x <= rc.z &&
+        if (rc.x <= lx1 && rc.z >= lx0 && rc.y <= ly1 && rc.w >= ly0 && rc.x <= rc.z &&
             rc.y <= rc.w) {
           const uint32_t far = (far_bits >> j) & 1u;
           ListT word = (ListT)(tid + j * kVsdThreads);
           if constexpr (kCull) {
-            const uint32_t x0 = (uint32_t)(max((int)rc.x, tx0) - tx0) >> 1;
-            const uint32_t x1 = (uint32_t)(min((int)rc.z, tx1) - tx0) >> 1;
-            const uint32_t y0 = (uint32_t)(max((int)rc.y, ty0) - ty0) >> 1;
-            const uint32_t y1 = (uint32_t)(min((int)rc.w, ty1) - ty0) >> 1;
+            const uint32_t x0 = (uint32_t)(max((int)rc.x, lx0) - lx0) >> 1;
+            const uint32_t x1 = (uint32_t)(min((int)rc.z, lx1) - lx0) >> 1;
+            const uint32_t y0 = (uint32_t)(max((int)rc.y, ly0) - ly0) >> 1;
+            const uint32_t y1 = (uint32_t)(min((int)rc.w, ly1) - ly0) >> 1;
             word |= (far << 11) | (x0 << 12) | (x1 << 17) | (y0 << 22) | (y1 << 27);
           }
           bool front = !far;
           if (a.qorder && !cull_back) {
-            const int ow = min((int)rc.z, tx1) - max((int)rc.x, tx0) + 1;
-            const int oh = min((int)rc.w, ty1) - max((int)rc.y, ty0) + 1;
+            const int ow = min((int)rc.z, lx1) - max((int)rc.x, lx0) + 1;
+            const int oh = min((int)rc.w, ly1) - max((int)rc.y, ly0) + 1;
             front = ow * oh >= kLptOverlap;
           }
           if (front)
-            s_list[atomicAdd(&s_nlist, 1)] = word;
+            s_lists[qb][atomicAdd(&s_nlists[qb], 1)] = word;
           else
-            s_list[kListLen - 1 - atomicAdd(&s_nsmall, 1)] = word;
+            s_lists[qb][kListLen - 1 - atomicAdd(&s_nsmalls[qb], 1)] = word;
         }
       }
-      __syncthreads();
+    };
+    for (int t = sp, it = 0; t < ntx * nty; t += S, ++it) {
+      const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
+      const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
+      const int qb = kAhead ? (it & 1) : 0;  // this tile's queue
+      ListT* const s_list = s_lists[qb];
+      int* const p_nlist = &s_nlists[qb];
+      int* const p_nsmall = &s_nsmalls[qb];
+      int* const p_next = &s_nexts[qb];
+      // The queue counters were reset behind the previous tile's raster-end
+      // barrier (or before the loop). list-ahead: this tile was listed in the
+      // previous tile's raster tail (the first one here), no barrier of its own.
+      // kStream: one round per kListLen entries (a single round otherwise)
+      for (int e0 = 0; e0 < (kStream ? 2 * nm : 1); e0 += kListLen) {
+      if (kStream && e0 > 0) __syncthreads();  // every wave is done with the last round's queue
+      if ((!BOPX_VSD_EARLY_RESET && !kAhead) || kStream) {
+        if (tid == 0) {
+          *p_nlist = 0;
+          *p_nsmall = 0;
+          *p_next = kVsdFirstClaim;
+        }
+        __syncthreads();
+      }
+      VSD_STAMP(0);
+      if (!kAhead || it == 0) {
+        list_tile(t, qb, e0);
+        __syncthreads();
+      }
       VSD_STAMP(1);
       // 2b. rasterise. Waves pull groups of kGroup (pose, meshlet) entries from a
       // shared counter (dynamic balance). Per group: the wave transforms the
       // three fixed-stride vertex blocks once (lane = vertex) into LDS, tests
       // every triangle's bbox against the tile, compacts the hits (ballot rank)
       // and only then sets up and rasterises them, one triangle per lane.
-      const int nnear = __builtin_amdgcn_readfirstlane(s_nlist);
-      const int nl = __builtin_amdgcn_readfirstlane(VSD_DIAG(1) ? 0 : s_nlist + s_nsmall);
+      const int nnear = __builtin_amdgcn_readfirstlane(*p_nlist);
+      const int nl = __builtin_amdgcn_readfirstlane(VSD_DIAG(1) ? 0 : *p_nlist + *p_nsmall);
       // each wave's first group is pre-assigned (wave-th group of the queue),
       // the rest are claimed from s_next, which starts past them
       for (int claimed = 0;; claimed = 1) {
         int base = BOPX_VSD_PRECLAIM ? wave * kGroup : 0;
         if (!BOPX_VSD_PRECLAIM || claimed) {
-          if (lane == 0) base = atomicAdd(&s_next, kGroup);
+          if (lane == 0) base = atomicAdd(p_next, kGroup);
           base = __builtin_amdgcn_readfirstlane(base);
         }
         VSD_STAMP(12);
@@ -1209,6 +1232,11 @@ void k_vsd(VsdArgs a) {
         wave_lds_sync();  // the staging area is rewritten by the next group
       }
       }  // rounds (kStream)
+      // list-ahead: this wave's share of the next tile's queue, while the other
+      // waves finish rasterising (the raster-end barrier below publishes it)
+      if constexpr (kAhead) {
+        if (t + S < ntx * nty) list_tile(t + S, qb ^ 1, 0);
+      }
       // Touch the test-depth lines of this wave's pixel rows (w, w + 8, ...)
       // while it waits for the other waves at the raster-end barrier: the
       // pixel pass then reads them from L2 instead of HBM. The empty asm below
@@ -1237,10 +1265,10 @@ void k_vsd(VsdArgs a) {
       // every wave has read the queue counters (after the list barrier) and is
       // done with s_next: reset them for the next tile (ordered by the
       // pixel-end barrier)
-      if (BOPX_VSD_EARLY_RESET && tid == 0) {
-        s_nlist = 0;
-        s_nsmall = 0;
-        s_next = kVsdFirstClaim;
+      if ((BOPX_VSD_EARLY_RESET || kAhead) && tid == 0) {
+        *p_nlist = 0;
+        *p_nsmall = 0;
+        *p_next = kVsdFirstClaim;
       }
       asm volatile("" ::"v"(touch));
       VSD_STAMP(3);
