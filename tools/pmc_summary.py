@@ -60,6 +60,9 @@ def main(out, dirs):
   with open(out, "w") as f:
     json.dump(res, f, indent=1, sort_keys=True)
   for k, r in res.items():
+    if k == "_meta":
+      print("_meta", r)
+      continue
     print(k)
     for c, v in sorted(r.items()):
       print("   %-30s %16.6g" % (c, v))
