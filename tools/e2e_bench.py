@@ -34,7 +34,7 @@ PER_IMG = 6
 SCENES = list(range(48, 60))
 
 
-def make_dataset(root, n_im, seed, torch):
+def make_dataset(root, n_im, seed, torch, inst=1):
   from PIL import Image
   from concurrent.futures import ThreadPoolExecutor
   from bop_toolkit_amd import inout, misc, synth
@@ -57,7 +57,11 @@ def make_dataset(root, n_im, seed, torch):
     json.dump(info, f)
   shutil.copytree(mdir, os.path.join(ds, "models"))
 
-  obj = np.stack([rng.choice(np.arange(1, 22), PER_IMG, replace=False)
+  # inst > 1 (T-LESS / IC-BIN-like): PER_IMG // 2 objects per image with `inst`
+  # instances each and `inst` estimates of each (n_top = -1 pairs all of them)
+  per_obj = PER_IMG if inst == 1 else max(1, PER_IMG // 2)
+  per_img = per_obj * inst
+  obj = np.stack([np.repeat(rng.choice(np.arange(1, 22), per_obj, replace=False), inst)
                   for _ in range(n_im)]).reshape(-1).astype(np.int32)
   n = len(obj)
   Rg, tg = synth.gt_poses(rng, n)
@@ -65,7 +69,7 @@ def make_dataset(root, n_im, seed, torch):
   K = synth.YCBV_K
   dev = ev.device
   T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
-  fidx = np.repeat(np.arange(n_im, dtype=np.int32), PER_IMG)
+  fidx = np.repeat(np.arange(n_im, dtype=np.int32), per_img)
   cam = np.tile([K[0, 0], K[1, 1], K[0, 2], K[1, 2]], (n_im, 1)).astype(np.float64)
   frames = ev.render(ev.slots(obj), T(np.concatenate([Rg.reshape(n, 9), tg], 1), torch.float64),
                      T(fidx, torch.int32), T(cam, torch.float64), n_im, W, H)
@@ -94,12 +98,13 @@ def make_dataset(root, n_im, seed, torch):
     for im in np.nonzero(scene_of == s)[0]:
       jobs.append((os.path.join(sdir, "depth", "%06d.png" % im), im))
       cams[str(im)] = {"cam_K": K.reshape(-1).tolist(), "depth_scale": DEPTH_SCALE}
-      rows = range(im * PER_IMG, (im + 1) * PER_IMG)
+      rows = range(im * per_img, (im + 1) * per_img)
       gts[str(im)] = [{"cam_R_m2c": Rg[j].reshape(-1).tolist(), "cam_t_m2c": tg[j].tolist(),
                        "obj_id": int(obj[j])} for j in rows]
       for j in rows:
-        targets.append({"im_id": int(im), "inst_count": 1, "obj_id": int(obj[j]),
-                        "scene_id": s})
+        if j % inst == 0:
+          targets.append({"im_id": int(im), "inst_count": inst, "obj_id": int(obj[j]),
+                          "scene_id": s})
         lines.append("%d,%d,%d,%r,%s,%s,0.5" % (
             s, im, obj[j], float(rng.random()), " ".join(repr(float(x)) for x in Re[j].ravel()),
             " ".join(repr(float(x)) for x in te[j])))
@@ -116,7 +121,7 @@ def make_dataset(root, n_im, seed, torch):
   with open(os.path.join(root, "results", result), "w") as f:
     f.write("\n".join(lines) + "\n")
   del ev
-  return n, result, sorted(set(scene_of.tolist()))
+  return n * inst, result, sorted(set(scene_of.tolist()))  # tuples: inst^2 per object
 
 
 def main():
@@ -125,12 +130,14 @@ def main():
   ap.add_argument("--root", default="/tmp/bopx_e2e")
   ap.add_argument("--seed", type=int, default=7)
   ap.add_argument("--profile", action="store_true")
+  ap.add_argument("--instances", type=int, default=1,
+                  help="instances (and estimates) per object and image; > 1: multi-instance")
   a = ap.parse_args()
   import torch
   if os.path.exists(a.root):
     shutil.rmtree(a.root)
   t0 = time.perf_counter()
-  n, result, scenes = make_dataset(a.root, a.images, a.seed, torch)
+  n, result, scenes = make_dataset(a.root, a.images, a.seed, torch, a.instances)
   t_gen = time.perf_counter() - t0
   datasets = os.path.join(a.root, "datasets")
   os.environ["BOP_PATH"] = datasets
@@ -191,7 +198,8 @@ def main():
   print(json.dumps({
       "what": "end-to-end BOP19 evaluation (calc_gt_info + eval_bop19_pose), synthetic YCB-V "
               "layout, 21 objs V=5002, 640x480 PNG depth, 1 GPU",
-      "images": a.images, "tuples": n, "gen_s": round(t_gen, 2),
+      "images": a.images, "instances": a.instances, "tuples": n, "gen_s": round(t_gen, 2),
+      "shared_render_ratio": ece.SHARED_RENDER_RATIO,
       "calc_gt_info_s": round(phases["calc_gt_info"], 2),
       "errors_s": {k: round(v, 2) for k, v in err_t.items()},
       "scores_s": round(phases.get("scores", 0.0), 2), "eval_bop19_s": round(t_eval, 2),
