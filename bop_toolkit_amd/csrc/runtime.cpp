@@ -1123,7 +1123,13 @@ static int vsd_shared_core(bopx_ctx* c, int64_t nr, const int32_t* rslots, const
   }
   // q buffers (0 = background), then the row spans: min 0x7F7F7F7F, max -1
   const size_t qn = (size_t)std::max<int64_t>(total, 1), sn = (size_t)std::max<int64_t>(rows, 1);
-  if (e == hipSuccess) e = hipMallocAsync((void**)&d_q, 4 * (qn + 2 * sn), s);
+  if (e == hipSuccess && hipMallocAsync((void**)&d_q, 4 * (qn + 2 * sn), s) != hipSuccess) {
+    (void)hipGetLastError();
+    d_q = nullptr;
+    (void)hipFreeAsync(d_roi, s);
+    return fail(c, BOPX_E_OOM, "shared-render depth buffers of %zu bytes do not fit; split the "
+                "batch or use bopx_vsd_batch", 4 * (qn + 2 * sn));
+  }
   if (e == hipSuccess) e = hipMemsetAsync(d_q, 0, 4 * qn, s);
   int32_t* d_smin = reinterpret_cast<int32_t*>(d_q + qn);
   int32_t* d_smax = d_smin + sn;
