@@ -106,13 +106,20 @@ def _errors_and_scores(p, result_filename, result_name, dataset, device, calc_er
       signs = [misc.get_error_signature(error["type"], error["n_top"])]
     for sign in dict.fromkeys(signs):
       error_dir_path = os.path.join(result_name, sign)
-      sps = [ecs.parse_args([
+      # the reference's command line (eval_bop19_pose.py:196-213), parsed once
+      # per folder; the threshold settings differ only in correct_th[type],
+      # which argparse would give as the floats of the same strings
+      base = None if not error["correct_th"] else ecs.parse_args([
           "--error_dir_paths={}".format(error_dir_path),
           "--eval_path={}".format(p["eval_path"]),
           "--targets_filename={}".format(p["targets_filename"]),
           "--visib_gt_min={}".format(p["visib_gt_min"]),
-          "--correct_th_{}={}".format(error["type"], ",".join(map(str, th)))])
-          for th in error["correct_th"]]
+          "--correct_th_{}={}".format(error["type"], ",".join(map(str, error["correct_th"][0])))])
+      sps = []
+      for th in error["correct_th"]:
+        sp = copy.deepcopy(base)
+        sp["correct_th"][error["type"]] = [float(x) for x in ",".join(map(str, th)).split(",")]
+        sps.append(sp)
       jobs.append((error_dir_path, sps))
       owner.append(error["type"])
     scorer.submit(jobs)

@@ -122,9 +122,26 @@ def cached_load(loader, path, **kw):
 
 
 # ----------------------------------------------------------------- enumeration
+_ORG_CACHE = {}
+
+
 def organize(targets, ests):
   """targets_org[scene][im][obj] = target; ests_org[scene][im][obj] = [est]
-  (insertion order, eval_calc_errors.py:207-228)."""
+  (insertion order, eval_calc_errors.py:207-228). The parsed files come from
+  cached_load (the same objects for every error type of a BOP19 run), so the
+  organised view is cached on their identity too; callers treat it as read-only."""
+  key = (id(targets), id(ests))
+  hit = _ORG_CACHE.get(key)
+  if hit is not None and hit[0] is targets and hit[1] is ests:
+    return hit[2]
+  out = _organize(targets, ests)
+  if len(_ORG_CACHE) > 8:
+    _ORG_CACHE.clear()
+  _ORG_CACHE[key] = (targets, ests, out)
+  return out
+
+
+def _organize(targets, ests):
   targets_org, ests_org = {}, {}
   for t in targets:
     targets_org.setdefault(t["scene_id"], {}).setdefault(t["im_id"], {})[t["obj_id"]] = t
