@@ -1812,6 +1812,7 @@ hipError_t launch_pose_roi(const ObjDesc* objs, int64_t n, const int32_t* slots,
 constexpr int kPairThreads = 256;
 constexpr int kPairWaves = kPairThreads / 64;
 constexpr int kPairCols = 2048;  // column coefficients staged in LDS per block of columns
+constexpr int kPairU = 4;  // pixels per lane and step (loads in flight together)
 
 template <int COST, int NT>
 __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {
@@ -1895,15 +1896,10 @@ __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {
       R = __builtin_amdgcn_readfirstlane(min(R, cb1));
       if (L > R) continue;
       const double pY = ((double)row - cy) / fy;  // misc.py:137-138, as k_vsd's w_pY
-      for (int col = L + lane; col <= R; col += 64) {
-        const uint32_t qe = rin_e && col >= Re.x && col <= Re.z
-                                ? qbuf[oe + (int64_t)(row - Re.y) * we + (col - Re.x)]
-                                : 0u;
-        const uint32_t qg = rin_g && col >= Rg.x && col <= Rg.z
-                                ? qbuf[og + (int64_t)(row - Rg.y) * wg + (col - Rg.x)]
-                                : 0u;
-        if ((qe | qg) == 0u) continue;
-        const float dtest = frame[(int64_t)row * W + col];
+      // kPairU pixels per lane and step: every load of the step in flight
+      // before the first use (the loop is latency-bound on the q / test-depth
+      // reads otherwise); lane -> pixel map fixed (col = L + lane + 64 i)
+      auto vsd_pixel = [&](uint32_t qe, uint32_t qg, float dtest, int col) {
         const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
         const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
         const double pX = s_pX[col - cb];
@@ -1935,6 +1931,24 @@ __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {
             }
           }
         }
+      };
+      const int64_t re_row = oe + (int64_t)(row - Re.y) * we - Re.x;
+      const int64_t rg_row = og + (int64_t)(row - Rg.y) * wg - Rg.x;
+      const int64_t f_row = (int64_t)row * W;
+      for (int c0 = L + lane; c0 <= R; c0 += 64 * kPairU) {
+        uint32_t qe[kPairU], qg[kPairU];
+        float dt[kPairU];
+#pragma unroll
+        for (int u = 0; u < kPairU; ++u) {
+          const int col = c0 + 64 * u;
+          const bool in = col <= R;
+          qe[u] = in && rin_e && col >= Re.x && col <= Re.z ? qbuf[re_row + col] : 0u;
+          qg[u] = in && rin_g && col >= Rg.x && col <= Rg.z ? qbuf[rg_row + col] : 0u;
+          dt[u] = in ? frame[f_row + col] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kPairU; ++u)
+          if ((qe[u] | qg[u]) != 0u) vsd_pixel(qe[u], qg[u], dt[u], c0 + 64 * u);
       }
       // 16-bit per-lane tau counters: a lane sees at most (w/64 + 1)(h/4 + 1)
       // pixels of a w x h union, < 42k for any image within the fused kernel's
