@@ -626,6 +626,11 @@ void k_vsd(VsdArgs a) {
   // (tools/gpu_cull_density.sh: 30k triangles at 1.5x size -1.4 %, 2x +1 %;
   // 10k triangles at 0.5x / 0.7x size still +1.8 % / +1.2 %)
   const bool cull_maybe = kCull && (a.cull == 3 || (a.cull < 0 && nm > kCullAutoMeshlets));
+  // GT-info and render modes list only the second pose's entries (nm .. 2 nm - 1):
+  // the rectangle registers and queue words hold them from 0 (entry = ebase + local
+  // index), so an object needs nm rectangle slots instead of 2 nm (launch_vsd_rpt_any)
+  constexpr bool kOnePose = (COST == kCostGtInfo || COST == kCostRender) && !kStream;
+  const int ebase = kOnePose ? nm : 0;
 
   // 1. per-pose meshlet rectangles (kept in registers: entry tid + 512 j) + ROI,
   // and each entry's nearest corner depth (queue order, see BOPX_VSD_PRIO above).
@@ -640,7 +645,7 @@ void k_vsd(VsdArgs a) {
   for (int i0 = 0; i0 < (kStream ? 2 * nm : 1); i0 += kListLen)
 #pragma unroll
   for (int j = 0; j < kR; ++j) {
-    const int i = (kStream ? i0 : 0) + tid + j * kVsdThreads;
+    const int i = (kStream ? i0 : ebase) + tid + j * kVsdThreads;
     rect[j] = make_short4(1, 1, 0, 0);
     zmin[j] = -INFINITY;
     qbv[j] = 0.0f;
@@ -729,7 +734,7 @@ void k_vsd(VsdArgs a) {
   uint32_t far_bits = 0;
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
-    const int i = tid + j * kVsdThreads;
+    const int i = ebase + tid + j * kVsdThreads;
     const int r = i >= nm;
     const float zmid = 0.5f * (s_zr[r][0] + s_zr[r][1]);
     far_bits |= (uint32_t)(zmin[j] > zmid) << j;
@@ -743,7 +748,7 @@ void k_vsd(VsdArgs a) {
     for (int j = 0; j < RPT; ++j) {
       const int i = tid + j * kVsdThreads;
       if ((back_bits >> j) & 1u) {
-        const float qhi = s_qhi[i >= nm];
+        const float qhi = s_qhi[ebase + i >= nm];
         const float cf = floorf(64.0f * (__log2f(qhi) - __log2f(qbv[j])) - 0.05f);
         s_qb[i] = (uint8_t)fminf(fmaxf(cf, 0.0f), 255.0f);
       }
@@ -891,10 +896,10 @@ void k_vsd(VsdArgs a) {
         int mlt[kGroup];
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
-          const int e = (kStream ? e0 : 0) + (int)(word[g] & 0x7FFu);
+          ent[g] = (kStream ? e0 : 0) + (int)(word[g] & 0x7FFu);  // queue index (s_qb)
+          const int e = ebase + ent[g];
           pose[g] = e >= nm ? 1 : 0;  // uniform (SGPR): e came through readfirstlane
           mlt[g] = e - pose[g] * nm;
-          ent[g] = e;
         }
         // Back-face occlusion test (cull 3), before any of the entry's data is
         // fetched: skipped when every pixel of its rectangle in the tile already
@@ -1678,7 +1683,8 @@ static void launch_vsd_rpt(const VsdArgs& a, int cost_type, hipStream_t s) {
 
 // rectangle registers per thread (RPT) for the largest registered object
 static void launch_vsd_rpt_any(const VsdArgs& a, int cost_type, hipStream_t s) {
-  const int need = 2 * a.max_nm;
+  // GT-info / render modes hold only the second pose's rectangles (kOnePose)
+  const int need = (cost_type == kCostGtInfo || cost_type == kCostRender ? 1 : 2) * a.max_nm;
   if (need <= kVsdThreads)
     launch_vsd_rpt<1>(a, cost_type, s);
   else if (need <= 2 * kVsdThreads)
@@ -1812,7 +1818,10 @@ hipError_t launch_pose_roi(const ObjDesc* objs, int64_t n, const int32_t* slots,
 constexpr int kPairThreads = 256;
 constexpr int kPairWaves = kPairThreads / 64;
 constexpr int kPairCols = 2048;  // column coefficients staged in LDS per block of columns
-constexpr int kPairU = 4;  // pixels per lane and step (loads in flight together)
+#ifndef BOPX_PAIR_U
+#define BOPX_PAIR_U 2
+#endif
+constexpr int kPairU = BOPX_PAIR_U;  // pixels per lane and step (loads in flight together)
 
 template <int COST, int NT>
 __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {

@@ -13,14 +13,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _workload(seed, n_img=6, ks=(1, 3, 5), W=640, H=480):
+def _workload(seed, n_img=6, ks=(1, 3, 5), W=640, H=480, meshes=((30, 60), (50, 100))):
   import torch
   from bop_toolkit_amd import synth
   from bop_toolkit_amd.batch import BatchEvaluator
   rng = np.random.default_rng(seed)
   ev = BatchEvaluator(0)
   objs = []
-  for o, (nl, nn) in enumerate([(30, 60), (50, 100)]):
+  for o, (nl, nn) in enumerate(meshes):
     pts, faces = synth.superellipsoid(nl, nn, tuple(rng.uniform(35.0, 70.0, 3)), 0.7)
     ev.add_object(o, pts, faces)
     objs.append((pts, faces))
@@ -107,6 +107,38 @@ def test_shared_renders_equal_fused(oracle_mod, cost, taus):
       np.testing.assert_allclose(shared[i], ref, rtol=0, atol=1e-12)
 
 
+@pytest.mark.parametrize("big", [(90, 140), (130, 150)])
+def test_shared_renders_large_meshes(oracle_mod, big):
+  """Largest object of the context with >= 394 / >= 610 meshlets (25.2k / 39k
+  triangles): the render mode holds one pose's meshlet rectangles (1 / 2 per
+  thread) where the fused kernel holds both poses' (2 / 4 per thread); the
+  results are the same bits."""
+  import torch
+  from bop_toolkit_amd.batch import unique_renders
+  ev, objs, obj, fi, pe, pg, fr, cam, dia, t = _workload(55, n_img=3, ks=(2, 3),
+                                                        meshes=(big, (30, 60)))
+  nf = len(objs[0][1])
+  assert (256 < nf / 64 <= 512) if big == (90, 140) else (512 < nf / 64 <= 1024)
+  n = len(obj)
+  ro, rp, rf, er, gr = unique_renders(obj, pe, pg, fi)
+  taus = np.arange(0.05, 0.51, 0.05)
+  fused = ev.vsd(ev.slots(obj), t(pe, torch.float64), t(pg, torch.float64), t(fi, torch.int32),
+                 t(fr, torch.float32), t(cam, torch.float64), 15.0, taus,
+                 t(dia, torch.float64)).cpu().numpy()
+  shared = ev.vsd_shared(ev.slots(ro), t(rp, torch.float64), t(rf, torch.int32),
+                         t(er, torch.int32), t(gr, torch.int32), t(fr, torch.float32),
+                         t(cam, torch.float64), 15.0, taus, t(dia, torch.float64)).cpu().numpy()
+  assert np.ptp(fused) > 0.1
+  assert np.array_equal(shared, fused)
+  K = cam[0]
+  for i in range(0, n, 5):
+    pts, faces = objs[obj[i]]
+    de = oracle_mod.render_depth(pts, faces, pe[i, :9].reshape(3, 3), pe[i, 9:], *K, 640, 480)
+    dg = oracle_mod.render_depth(pts, faces, pg[i, :9].reshape(3, 3), pg[i, 9:], *K, 640, 480)
+    assert list(shared[i]) == oracle_mod.vsd_depths(fr[fi[i]], de, dg, *K, 15.0, taus, True,
+                                                    dia[i], "step"), i
+
+
 def test_shared_host_entry_unions_and_checks(oracle_mod):
   """bopx_vsd_shared_batch (host buffers) with BOPX_VSD_UNIONS and a float64
   delta: the same errors and union counts as bopx_vsd_batch; bad render
@@ -158,3 +190,60 @@ def test_shared_dev_bad_index_gives_nan():
                       t(cam, torch.float64), 15.0, np.arange(0.05, 0.51, 0.05),
                       t(dia, torch.float64)).cpu().numpy()
   assert np.isnan(out[1]).all() and np.isfinite(out[0]).all()
+
+
+def test_shared_wide_image_column_blocks(oracle_mod):
+  """Unions wider than k_vsd_pair's 2,048-column LDS block (4,096 x 512
+  image, estimates shifted right by up to ~3,700 px, one partly off the right
+  edge): equal to the fused kernel bit for bit and to the oracle."""
+  import torch
+  from bop_toolkit_amd import synth
+  from bop_toolkit_amd.batch import BatchEvaluator, unique_renders
+  rng = np.random.default_rng(54)
+  W, H = 4096, 512
+  ev = BatchEvaluator(0)
+  pts, faces = synth.superellipsoid(30, 60, (60.0, 45.0, 50.0), 0.7)
+  ev.add_object(0, pts, faces)
+  K = np.array([[1075.0, 0.0, 400.0], [0.0, 1075.0, 256.0], [0.0, 0.0, 1.0]])
+  Rg, tg = synth.gt_poses(rng, 2, z_range=(650.0, 750.0), xy=(60.0, 40.0))
+  gts = [np.concatenate([Rg[i].reshape(9), tg[i]]) for i in range(2)]
+  ests = []
+  for dx in (0.0, 800.0, 1600.0, 2600.0, None):
+    Re, te = synth.perturb(rng, Rg[:1], tg[:1], outlier_frac=0.0)
+    te = te.copy()
+    if dx is None:  # centre 20 px left of the right edge: the render is cut by it
+      dx = (W - 20 - K[0, 2]) * te[0, 2] / K[0, 0] - te[0, 0]
+    te[0, 0] += dx
+    ests.append(np.concatenate([Re[0].reshape(9), te[0]]))
+  pe = np.stack([e for e in ests for _ in gts])
+  pg = np.stack([g for _ in ests for g in gts])
+  n = len(pe)
+  obj = np.zeros(n, np.int32)
+  fi = np.zeros(n, np.int32)
+  cam = np.array([[K[0, 0], K[1, 1], K[0, 2], K[1, 2]]])
+  dev = ev.device
+  t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+  frames = ev.render(ev.slots([0, 0]), t(np.stack(gts), torch.float64), t([0, 0], torch.int32),
+                     t(cam, torch.float64), 1, W, H)
+  fr = frames.cpu().numpy()
+  fr = np.where(fr > 0, fr, 1500.0)
+  fr = np.round(fr + rng.normal(0.0, 3.0, fr.shape)).astype(np.float32)
+  fr[rng.random(fr.shape) < 0.1] = 0.0
+  dia = np.full(n, 150.0)
+  taus = np.arange(0.05, 0.51, 0.05)
+  ro, rp, rf, er, gr = unique_renders(obj, pe, pg, fi)
+  fused = ev.vsd(ev.slots(obj), t(pe, torch.float64), t(pg, torch.float64), t(fi, torch.int32),
+                 t(fr, torch.float32), t(cam, torch.float64), 15.0, taus,
+                 t(dia, torch.float64)).cpu().numpy()
+  shared = ev.vsd_shared(ev.slots(ro), t(rp, torch.float64), t(rf, torch.int32),
+                         t(er, torch.int32), t(gr, torch.int32), t(fr, torch.float32),
+                         t(cam, torch.float64), 15.0, taus, t(dia, torch.float64)).cpu().numpy()
+  assert np.array_equal(shared, fused)
+  assert (fused[-4:] == 1.0).all() and (fused[:2] < 1.0).any()  # shifted estimates miss
+  for i in range(n):
+    de = oracle_mod.render_depth(pts, faces, pe[i, :9].reshape(3, 3), pe[i, 9:], *cam[0], W, H)
+    dg = oracle_mod.render_depth(pts, faces, pg[i, :9].reshape(3, 3), pg[i, 9:], *cam[0], W, H)
+    if i == n - 1:
+      assert (de[:, W - 1] > 0).any() and (de[:, 0] == 0).all()  # cut by the right edge
+    assert list(shared[i]) == oracle_mod.vsd_depths(fr[0], de, dg, *cam[0], 15.0, taus, True,
+                                                    dia[i], "step"), i
