@@ -10,3 +10,6 @@ TAG=${TAG:-r03} bash tools/pmc.sh "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_W
 cp gpurun_out/${TAG:-r03}_pmc.json profiles/${TAG:-r03}_pmc.json
 timeout -k 10 600 python bench.py > gpurun_out/bench_${TAG:-r03}_traffic.json 2> gpurun_out/bench_${TAG:-r03}_traffic.err || { tail -20 gpurun_out/bench_${TAG:-r03}_traffic.err; exit 1; }
 cat gpurun_out/bench_${TAG:-r03}_traffic.json
+# multi-instance variant (shared renders): bench line + kernel stats
+timeout -k 10 300 python bench.py --config 5 --tuples 20000 --no-cpu-baseline > gpurun_out/bench_${TAG:-r03}_config5.json 2> gpurun_out/bench_${TAG:-r03}_config5.err || { tail -20 gpurun_out/bench_${TAG:-r03}_config5.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG:-r03}_config5 -o run --output-format csv -- python3 bench.py --config 5 --tuples 20000 --no-cpu-baseline --steps 5 > gpurun_out/prof_${TAG:-r03}_config5.log 2>&1 || { tail -20 gpurun_out/prof_${TAG:-r03}_config5.log; exit 1; }
