@@ -196,15 +196,27 @@ class FolderScorer:
       import multiprocessing as mp
       self.pool = mp.get_context("spawn").Pool(self.workers)
     if self.pool is None:
-      self.pending.append([_score_job(a) for a in args])
-    else:
-      self.pending.append(self.pool.map_async(_score_job, args, chunksize=1))
+      self.pending.append([[_score_job(a)] for a in args])  # one finished chunk per folder
+      return
+    # A group of fewer folders than workers (MSSD, MSPD: one folder of ten
+    # thresholds each) spreads each folder's settings over the idle workers in
+    # contiguous chunks; a chunk re-reads the folder's errors, the scores are
+    # the same (BOPX_SCORE_SPLIT=0: one task per folder)
+    split = os.environ.get("BOPX_SCORE_SPLIT", "1") != "0"
+    group = []
+    for path, sps, do_print in args:
+      k = max(1, min(len(sps), self.workers // max(1, len(args)))) if split else 1
+      cut = [len(sps) * i // k for i in range(k + 1)]
+      group.append([self.pool.apply_async(_score_job, ((path, sps[cut[i]:cut[i + 1]], do_print),))
+                    for i in range(k)])
+    self.pending.append(group)
 
   def results(self):
     try:
       out = []
-      for r in self.pending:
-        out.extend(r if isinstance(r, list) else r.get())
+      for group in self.pending:  # per folder: its chunks' scores in setting order
+        for chunks in group:
+          out.append([s for c in chunks for s in (c if isinstance(c, list) else c.get())])
       return out
     finally:
       self.close()
