@@ -57,6 +57,16 @@ class BatchEvaluator:
         "ns": 0 if syms is None else len(syms), "diameter": diameter,
         "bbox": (pts.min(0), pts.max(0)) if len(pts) else (np.zeros(3), np.zeros(3))}
 
+  def remove_object(self, obj_id):
+    self.ctx.remove_object(obj_id)
+    self.objects.pop(obj_id, None)
+
+  def set_symmetries(self, obj_id, syms):
+    """Replace a registered object's symmetry set (list of {'R','t'} or S x 12)."""
+    s12 = syms if isinstance(syms, np.ndarray) else symmetries_to_array(syms)
+    self.ctx.set_symmetries(obj_id, s12)
+    self.objects[obj_id]["ns"] = len(s12)
+
   def slots(self, obj_ids):
     """int32 device tensor of slots for a sequence of obj_ids."""
     table = {k: v["slot"] for k, v in self.objects.items()}

@@ -179,6 +179,25 @@ def scene_records(p, scene_id, scene_targets, ests_org, scene_gt):
   return recs, n_ests
 
 
+_REC_CACHE = {}
+
+
+def scene_records_cached(p, scene_id, scene_targets, ests_org, scene_gt):
+  """scene_records, shared by the error types of one BOP19 run: the inputs are
+  the cached parses (the same objects for every error type), so the records
+  are keyed on their identity and the n_top / skip_missing settings; callers
+  treat them as read-only."""
+  key = (scene_id, id(scene_targets), id(ests_org), id(scene_gt), p["n_top"], p["skip_missing"])
+  hit = _REC_CACHE.get(key)
+  if hit is not None and hit[0] is scene_targets and hit[1] is ests_org and hit[2] is scene_gt:
+    return hit[3]
+  out = scene_records(p, scene_id, scene_targets, ests_org, scene_gt)
+  if len(_REC_CACHE) >= 4096:
+    _REC_CACHE.clear()
+  _REC_CACHE[key] = (scene_targets, ests_org, scene_gt, out)
+  return out
+
+
 def gate(error_type, diameter, t_e, t_g):
   """Host pre-check of one tuple: None = evaluate, else the fill value list
   (eval_calc_errors.py:292-339). n_tau is applied by the caller for VSD."""
@@ -193,28 +212,110 @@ def gate(error_type, diameter, t_e, t_g):
 
 # ------------------------------------------------------------------ evaluation
 class Models:
-  """Objects of one dataset resident on the GPU (+ host-side info)."""
+  """Objects of one dataset resident on the GPU (+ host-side info).
+
+  The evaluator (evaluator(device)) keeps its objects between runs: an object
+  whose model file (path, size, mtime) and diameter are unchanged is not
+  uploaded again, and its symmetry set is only (re)computed when the error
+  type needs one that is not registered yet (VSD -> MSSD -> MSPD of one BOP19
+  run: one upload per model, one symmetry set per object). Objects of other
+  models are removed, so ev.objects is exactly this dataset's."""
 
   def __init__(self, ev, p, dp_model, models_info):
     self.ev = ev
     self.info = models_info
     need_syms = p["error_type"] in ("mssd", "mspd")
     self.sym_ids = set(dp_model["symmetric_obj_ids"] or [])
+    reg = ev.__dict__.setdefault("_bopx_reg", {})  # obj_id -> (mesh key, symmetry key)
+    keep = set()
     for obj_id in dp_model["obj_ids"]:
       path = dp_model["model_tpath"].format(obj_id=obj_id)
       if not os.path.exists(path):
         continue
+      st = os.stat(path)
+      dia = models_info[obj_id]["diameter"] if models_info is not None else None
+      mkey = (os.path.abspath(path), st.st_size, st.st_mtime_ns, dia)
+      skey = None
+      if need_syms:
+        info = models_info[obj_id]
+        skey = (p["max_sym_disc_step"], repr(info.get("symmetries_discrete")),
+                repr(info.get("symmetries_continuous")))
+      have = reg.get(obj_id)
+      keep.add(obj_id)
+      if have is not None and have[0] == mkey and obj_id in ev.objects:
+        if need_syms and have[1] != skey:
+          syms = misc.get_symmetry_transformations(models_info[obj_id], p["max_sym_disc_step"])
+          ev.set_symmetries(obj_id, syms)
+          reg[obj_id] = (mkey, skey)
+        continue
+      if obj_id in ev.objects:
+        ev.remove_object(obj_id)
       m = cached_load(inout.load_ply, path)
       syms = None
       if need_syms:
         syms = misc.get_symmetry_transformations(models_info[obj_id], p["max_sym_disc_step"])
-      dia = models_info[obj_id]["diameter"] if models_info is not None else None
       ev.add_object(obj_id, m["pts"], m.get("faces"), syms, dia)
+      reg[obj_id] = (mkey, skey)
+    for obj_id in [o for o in ev.objects if o not in keep]:
+      ev.remove_object(obj_id)
+      reg.pop(obj_id, None)
+
+
+_EVALUATORS = {}  # device -> BatchEvaluator, shared by the runs of one process
+
+
+def evaluator(device):
+  from .batch import BatchEvaluator
+  ev = _EVALUATORS.get(int(device))
+  if ev is None:
+    ev = _EVALUATORS[int(device)] = BatchEvaluator(device)
+  return ev
 
 
 def _pose12(R, t):
   return np.concatenate([np.asarray(R, np.float64).reshape(9),
                          np.asarray(t, np.float64).reshape(3)])
+
+
+def _poses12(Rs, ts):
+  """[n, 12] float64 rows [R row-major | t] of n poses (_pose12 per pose, in one
+  conversion when the shapes agree)."""
+  n = len(Rs)
+  try:
+    return np.concatenate([np.asarray(Rs, np.float64).reshape(n, 9),
+                           np.asarray(ts, np.float64).reshape(n, 3)], 1)
+  except ValueError:
+    return np.stack([_pose12(R, t) for R, t in zip(Rs, ts)]).reshape(n, 12)
+
+
+def gates(error_type, dias, t_es, t_gs):
+  """gate() of many tuples at once: bool array, True = filled (not evaluated).
+  The sphere-projection / distance tests run vectorised; a tuple within a
+  relative 1e-9 of its threshold (or with a zero depth, NaN, ...) is decided by
+  the scalar gate(), so the result is gate()'s for every tuple."""
+  n = len(t_es)
+  fill = np.zeros(n, bool)
+  if n == 0 or error_type not in ("vsd", "cus", "ad", "add", "adi", "mssd"):
+    return fill
+  te = np.asarray(t_es, np.float64).reshape(n, 3)
+  tg = np.asarray(t_gs, np.float64).reshape(n, 3)
+  dia = np.asarray(dias, np.float64)
+  with np.errstate(all="ignore"):
+    if error_type in ("vsd", "cus"):
+      d = te[:, :2] / te[:, 2:3] - tg[:, :2] / tg[:, 2:3]
+      val = np.sqrt(d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1])
+      thr = (0.5 * dia) * (1.0 / te[:, 2] + 1.0 / tg[:, 2])
+    else:
+      e = te - tg
+      val = np.sqrt((e * e).sum(1))
+      thr = dia
+    fill = ~(val < thr)
+    sure = np.abs(val - thr) > 1e-9 * np.maximum(np.abs(val), np.abs(thr))
+    if error_type in ("vsd", "cus"):
+      sure &= (te[:, 2] != 0) & (tg[:, 2] != 0)
+  for i in np.nonzero(~sure)[0]:
+    fill[i] = gate(error_type, float(dia[i]), np.asarray(t_es[i]), np.asarray(t_gs[i])) is not None
+  return fill
 
 
 def plan(p, recs, models_info):
@@ -224,22 +325,32 @@ def plan(p, recs, models_info):
   n_tau = len(p["vsd_taus"])
   errs = [dict() for _ in recs]
   todo = []
-  for ri, r in enumerate(recs):
-    for gt_id, gt in r["gts"]:
-      R_g, t_g = gt["cam_R_m2c"], gt["cam_t_m2c"]
+  pairs = [(ri, gt_id, gt) for ri, r in enumerate(recs) for gt_id, gt in r["gts"]]
+  fills = None
+  if models_info is not None and et in ("vsd", "cus", "ad", "add", "adi", "mssd"):
+    fills = gates(et, [models_info[recs[ri]["obj_id"]]["diameter"] for ri, _, _ in pairs],
+                  [recs[ri]["t"] for ri, _, _ in pairs], [gt["cam_t_m2c"] for _, _, gt in pairs])
+  for k, (ri, gt_id, gt) in enumerate(pairs):
+    r = recs[ri]
+    R_g, t_g = gt["cam_R_m2c"], gt["cam_t_m2c"]
+    if fills is not None:
+      fill = None
+      if fills[k]:
+        fill = "vsd_fill" if et in ("vsd", "cus") else [float("inf")]
+    else:
       dia = models_info[r["obj_id"]]["diameter"] if models_info is not None else None
       fill = gate(et, dia, r["t"], t_g)
-      if fill == "vsd_fill":
-        errs[ri][gt_id] = [1.0] * (n_tau if et == "vsd" else 1)
-      elif fill is not None:
-        errs[ri][gt_id] = fill
-      elif et in ("re", "te", "rete"):
-        e_re = pose_error.re(r["R"], R_g)
-        e_te = pose_error.te(r["t"], t_g)
-        errs[ri][gt_id] = {"re": [e_re], "te": [e_te], "rete": [e_re, e_te]}[et]
-      else:
-        errs[ri][gt_id] = None  # filled from the GPU batch
-        todo.append((ri, gt_id, R_g, t_g))
+    if fill == "vsd_fill":
+      errs[ri][gt_id] = [1.0] * (n_tau if et == "vsd" else 1)
+    elif fill is not None:
+      errs[ri][gt_id] = fill
+    elif et in ("re", "te", "rete"):
+      e_re = pose_error.re(r["R"], R_g)
+      e_te = pose_error.te(r["t"], t_g)
+      errs[ri][gt_id] = {"re": [e_re], "te": [e_te], "rete": [e_re, e_te]}[et]
+    else:
+      errs[ri][gt_id] = None  # filled from the GPU batch
+      todo.append((ri, gt_id, R_g, t_g))
   return errs, todo
 
 
@@ -287,8 +398,8 @@ def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs
   dev = ev.device
   n = len(todo)
   obj = np.array([recs[ri]["obj_id"] for ri, _, _, _ in todo], np.int32)
-  pe = np.stack([_pose12(recs[ri]["R"], recs[ri]["t"]) for ri, _, _, _ in todo])
-  pg = np.stack([_pose12(R_g, t_g) for _, _, R_g, t_g in todo])
+  pe = _poses12([recs[ri]["R"] for ri, _, _, _ in todo], [recs[ri]["t"] for ri, _, _, _ in todo])
+  pg = _poses12([R_g for _, _, R_g, _ in todo], [t_g for _, _, _, t_g in todo])
   T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
   slots = ev.slots(obj)
   d_pe, d_pg = T(pe, torch.float64), T(pg, torch.float64)
@@ -313,8 +424,11 @@ def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs
     from .batch import unique_renders
     # multi-instance images (every estimate x every GT instance of its object,
     # :281-290): each distinct pose rendered once when that saves renders
-    ro, rp, rf, er, gr = unique_renders(obj, pe, pg, fidx_h)
-    if len(ro) <= SHARED_RENDER_RATIO * n:
+    # one tuple per (image, object) (single-instance data): 2 n renders, fused path
+    single = len(np.unique(fidx_h.astype(np.int64) << 32 | obj.astype(np.int64))) == n
+    ro, rp, rf, er, gr = (None,) * 5 if single and SHARED_RENDER_RATIO < 2 else \
+        unique_renders(obj, pe, pg, fidx_h)
+    if ro is not None and len(ro) <= SHARED_RENDER_RATIO * n:
       return ev.vsd_shared(ev.slots(ro), T(rp, torch.float64), T(rf, torch.int32),
                            T(er, torch.int32), T(gr, torch.int32), d_frames,
                            T(cam, torch.float64), delta, p["vsd_taus"], T(dia, torch.float64),
@@ -368,8 +482,9 @@ def todo_costs(objects, p, recs, todo, scene_camera, im_size):
   if et in ("vsd", "cus") and scene_camera is not None:
     lo = np.stack([x["bbox"][0] for x in o])
     hi = np.stack([x["bbox"][1] for x in o])
-    pe = np.stack([_pose12(recs[ri]["R"], recs[ri]["t"]) for ri, _, _, _ in todo])
-    pg = np.stack([_pose12(R_g, t_g) for _, _, R_g, t_g in todo])
+    pe = _poses12([recs[ri]["R"] for ri, _, _, _ in todo],
+                  [recs[ri]["t"] for ri, _, _, _ in todo])
+    pg = _poses12([R_g for _, _, R_g, _ in todo], [t_g for _, _, _, t_g in todo])
     K = np.stack([np.asarray(scene_camera[recs[ri]["im_id"]]["cam_K"], np.float64).reshape(3, 3)
                   for ri, _, _, _ in todo])
     roi = shard.roi_pixels(lo, hi, [pe, pg], K, im_size[0], im_size[1])
@@ -443,7 +558,6 @@ def evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, mode
 def run(p, device=0):
   """Evaluate every result file of p; returns the written file paths."""
   import torch
-  from .batch import BatchEvaluator
 
   if p["error_type"] not in ERROR_TYPES:
     raise ValueError("Unknown pose error function.")
@@ -467,10 +581,7 @@ def run(p, device=0):
       models_info = cached_load(inout.load_json, dp_model["models_info_path"], keys_to_int=True)
     if et not in ("re", "te", "rete"):
       if ev is None:
-        ev = BatchEvaluator(device)
-      for o in list(ev.objects):
-        ev.ctx.remove_object(o)
-      ev.objects.clear()
+        ev = evaluator(device)
       log("Loading object models...")
       Models(ev, p, dp_model, models_info)
     targets = cached_load(inout.load_json, os.path.join(dp_split["base_path"], p["targets_filename"]))
@@ -480,6 +591,12 @@ def run(p, device=0):
     sym_ids = set(dp_model["symmetric_obj_ids"] or [])
     ests_counter = 0
     rank, world = _dist()
+    # VSD test depth goes to the GPU from the prepare thread on a stream of its
+    # own, overlapping the current scene's kernels (the main stream only ever
+    # sees frames already resident)
+    up = None
+    if et == "vsd" and ev is not None and torch.cuda.is_available():
+      up = (torch.cuda.Stream(ev.device), torch.cuda.current_stream(ev.device))
 
     def prepare(scene_id, scene_targets):
       # host side of one scene: annotations, records, gates, this rank's share
@@ -489,7 +606,7 @@ def run(p, device=0):
                                  dp_split["scene_camera_tpath"].format(scene_id=scene_id))
       scene_gt = cached_load(inout.load_scene_gt,
                              dp_split["scene_gt_tpath"].format(scene_id=scene_id))
-      recs, n_ests = scene_records(p, scene_id, scene_targets, ests_org, scene_gt)
+      recs, n_ests = scene_records_cached(p, scene_id, scene_targets, ests_org, scene_gt)
       planned = None
       if recs:
         errs, todo, mine = plan_rank(p, recs, models_info, ev.objects if ev else None,
@@ -498,6 +615,12 @@ def run(p, device=0):
         if et == "vsd" and len(mine):
           depths = load_scene_depths(dp_split, scene_camera, scene_id,
                                      todo_images(recs, [todo[i] for i in mine]), torch)
+          if up is not None and torch.is_tensor(depths):
+            with torch.cuda.stream(up[0]):
+              d = depths.to(ev.device, non_blocking=True)
+            up[0].synchronize()
+            d.record_stream(up[1])  # freed behind the main stream's use
+            depths = d
         planned = (errs, todo, mine, depths)
       return scene_camera, recs, n_ests, planned
 

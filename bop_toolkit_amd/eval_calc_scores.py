@@ -174,12 +174,21 @@ def _score_job(job):
   return [score_error_dir(sp, error_dir_path, cache=cache, do_print=do_print)[0] for sp in sps]
 
 
+def _lower_priority():
+  try:
+    os.nice(5)
+  except OSError:
+    pass
+
+
 class FolderScorer:
   """score_folders in stages: submit(jobs) queues a group of folders (scored
   at once by the pool while the caller goes on, e.g. computes the next error
   type's folders on the GPU), results() returns every group's scores in
-  submission order. The spawned pool starts with the first submit (not
-  earlier: its interpreters would compete with the caller's own host work)."""
+  submission order. The spawned pool starts at once, its workers at a lower
+  CPU priority (nice +5), so their interpreter start-up runs behind the
+  caller's first error pass instead of after it (BOPX_SCORE_EARLY=0: start
+  with the first submit)."""
 
   def __init__(self, n_folders, workers=None, do_print=True):
     if workers is None:
@@ -189,12 +198,17 @@ class FolderScorer:
     self.workers = workers if n_folders > 1 else 1
     self.pool = None
     self.pending = []
+    if self.workers > 1 and os.environ.get("BOPX_SCORE_EARLY", "1") != "0":
+      self._start()
+
+  def _start(self):
+    import multiprocessing as mp
+    self.pool = mp.get_context("spawn").Pool(self.workers, initializer=_lower_priority)
 
   def submit(self, jobs):
     args = [(path, sps, self.do_print) for path, sps in jobs]
     if self.pool is None and self.workers > 1:
-      import multiprocessing as mp
-      self.pool = mp.get_context("spawn").Pool(self.workers)
+      self._start()
     if self.pool is None:
       self.pending.append([[_score_job(a)] for a in args])  # one finished chunk per folder
       return

@@ -190,10 +190,23 @@ def save_json(path, content):
       body = ",\n".join('  "{}": {}'.format(k, _dumps(v)) for k, v in items)
       f.write("{\n" + body + ("\n}" if items else "}"))
     elif isinstance(content, list):
-      body = ",\n".join("  " + _dumps(e) for e in content)
-      f.write("[\n" + body + ("\n]" if content else "]"))
+      f.write(_list_lines(content))
     else:
       json.dump(content, f, sort_keys=True)
+
+
+def _list_lines(content):
+  """A list as save_json writes it ('[\n  e0,\n  e1\n]', empty '[\n]'). A list of dicts is
+  encoded in one C-encoder call and cut at the element boundaries ('}, {'
+  appears exactly there when it appears len - 1 times: every boundary of two
+  dicts has it), the same text as encoding element by element."""
+  if not content:
+    return "[\n]"
+  if all(type(e) is dict for e in content):
+    whole = _dumps(content)
+    if whole.count("}, {") == len(content) - 1:
+      return "[\n  " + whole[1:-1].replace("}, {", "},\n  {") + "\n]"
+  return "[\n" + ",\n".join("  " + _dumps(e) for e in content) + "\n]"
 
 
 def _json_float(v):

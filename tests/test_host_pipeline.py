@@ -125,3 +125,52 @@ def test_unique_renders_dedupes_bitwise():
   pz2 = pz.copy()
   pz2[0, 9] = -0.0
   assert len(unique_renders(obj[:1], pz[:1], pz2[:1], fi[:1])[0]) == 2
+
+
+def test_vectorised_gates_equal_scalar_gate():
+  """ece.gates (vectorised, scalar fallback near the threshold) decides every
+  tuple as ece.gate does (eval_calc_errors.py:292-339, misc.py:309-331):
+  random poses, tuples placed exactly on / next to the thresholds, zero,
+  negative, NaN and infinite depths."""
+  rng = np.random.default_rng(3)
+  n = 4000
+  te = rng.normal(0, 300, (n, 3, 1)) + np.array([[0], [0], [900]])
+  tg = te + rng.normal(0, 60, (n, 3, 1))
+  dia = rng.uniform(50, 250, n)
+  # exactly on the distance threshold, and one ulp either side
+  for k, f in ((0, 1.0), (1, np.nextafter(1.0, 2.0)), (2, np.nextafter(1.0, 0.0))):
+    dv = np.array([[1.0], [2.0], [2.0]]) / 3.0
+    tg[k] = te[k] + dv * dia[k] * f
+  te[10, 2, 0] = 0.0
+  tg[11, 2, 0] = 0.0
+  te[12, 2, 0] = -500.0
+  te[13, 0, 0] = np.nan
+  tg[14, 1, 0] = np.inf
+  tg[15] = te[15]
+  for et in ("vsd", "cus", "mssd", "add", "adi", "ad", "mspd"):
+    want = np.array([ece.gate(et, float(d), a, b) is not None for d, a, b in zip(dia, te, tg)])
+    got = ece.gates(et, dia, list(te), list(tg))
+    assert np.array_equal(got, want), et
+    assert want.any() and (~want).any() or et == "mspd"
+
+
+def test_save_json_list_bytes(tmp_path):
+  """save_json of lists (errors and matches files) is the element-by-element
+  text: dicts with nested dicts / lists, NaN / inf, non-dict elements, and
+  strings holding the element separator."""
+  import json
+  cases = [
+      [],
+      [{"a": 1}],
+      [{"scene_id": 1, "im_id": 2, "error": [0.25], "error_norm": [float("nan")], "valid": True},
+       {"scene_id": 1, "im_id": 3, "error": -1, "error_norm": -1, "valid": False}],
+      [{"errors": {3: [1.0, float("inf")], 1: [0.5]}, "est_id": 0}, {"errors": {}, "est_id": 1}],
+      [{"s": "x}, {y"}, {"s": "z"}],
+      [{"a": [{"b": 1}, {"c": 2}]}, {"d": 3}],
+      [1, {"a": 2}, [3]],
+  ]
+  for k, c in enumerate(cases):
+    path = tmp_path / ("%d.json" % k)
+    inout.save_json(str(path), c)
+    want = "[\n" + ",\n".join("  " + json.dumps(e, sort_keys=True) for e in c) + "\n]" if c else "[\n]"
+    assert path.read_text() == want, k

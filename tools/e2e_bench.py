@@ -173,6 +173,11 @@ def main():
     return out
   ece.run = run_wrap
   ecs.score_error_dir = timed("scores", score0)
+  # host steps of the error passes (the prepare thread's included)
+  from bop_toolkit_amd import inout
+  for mod, name in ((ece, "scene_records"), (ece, "plan_rank"), (ece, "load_scene_depths"),
+                    (ece, "evaluate_batch"), (ece, "evaluate"), (ece, "Models"), (inout, "save_json"), (inout, "save_json_per_value")):
+    setattr(mod, name, timed("host:" + name, getattr(mod, name)))
   p = eval_bop19_pose.parse_args([
       "--result_filenames", result, "--results_path", os.path.join(a.root, "results"),
       "--eval_path", os.path.join(a.root, "eval")])
@@ -203,6 +208,7 @@ def main():
       "calc_gt_info_s": round(phases["calc_gt_info"], 2),
       "errors_s": {k: round(v, 2) for k, v in err_t.items()},
       "scores_s": round(phases.get("scores", 0.0), 2), "eval_bop19_s": round(t_eval, 2),
+      "host_s": {k[5:]: round(v, 3) for k, v in phases.items() if k.startswith("host:")},
       "eval_tuples_per_s": n / t_eval,
       "ar": {k: round(float(v), 4) for k, v in scores.items()}}))
 
