@@ -117,3 +117,46 @@ def test_caller_matches_reference(tmp_path):
           a, b = np.array(g["errors"][k]), np.array(e["errors"][k])
           assert np.array_equal(np.isinf(a), np.isinf(b))
           np.testing.assert_allclose(a[~np.isinf(a)], b[~np.isinf(b)], rtol=1e-9, atol=1e-9)
+
+
+def test_models_registry_reused_across_error_types():
+  """ece.Models on a kept evaluator (eval_bop19_pose: VSD, MSSD, MSPD in one
+  process): one mesh upload per model, symmetry sets attached when an error
+  type first needs them, nothing re-uploaded for the next type; a changed
+  max_sym_disc_step resets the sets only; objects of other datasets leave."""
+  class FakeEv:
+    def __init__(self):
+      self.objects, self.calls = {}, []
+
+    def add_object(self, obj_id, pts, faces=None, syms=None, diameter=None):
+      self.calls.append(("add", obj_id, syms is not None))
+      self.objects[obj_id] = {"ns": 0 if syms is None else len(syms)}
+
+    def remove_object(self, obj_id):
+      self.calls.append(("remove", obj_id))
+      self.objects.pop(obj_id)
+
+    def set_symmetries(self, obj_id, syms):
+      self.calls.append(("syms", obj_id))
+      self.objects[obj_id]["ns"] = len(syms)
+
+  ev = FakeEv()
+  ev.objects[999] = {"ns": 0}  # an object of another dataset
+  runs = []
+  for et, step in (("vsd", 15), ("mssd", 15), ("mspd", 15), ("mssd", 10), ("vsd", 10)):
+    p = _params(et, -1)
+    p["max_sym_disc_step"] = step
+    dp_model = dataset_params.get_model_params(p["datasets_path"], "lmo", "eval")
+    info = inout.load_json(dp_model["models_info_path"], keys_to_int=True)
+    ev.calls = []
+    ece.Models(ev, p, dp_model, info)
+    runs.append(ev.calls)
+  ids = sorted(ev.objects)
+  assert 999 not in ev.objects and ids
+  assert ("remove", 999) in runs[0]
+  assert sorted(c[1] for c in runs[0] if c[0] == "add") == ids  # first pass: every mesh, no syms
+  assert all(not c[2] for c in runs[0] if c[0] == "add")
+  assert sorted(c[1] for c in runs[1]) == ids and all(c[0] == "syms" for c in runs[1])
+  assert runs[2] == []  # MSPD: same symmetry key, nothing to do
+  assert sorted(c[1] for c in runs[3]) == ids and all(c[0] == "syms" for c in runs[3])
+  assert runs[4] == []  # VSD does not need symmetry sets
