@@ -103,3 +103,21 @@ def test_bench_two_ranks_strong_scaling():
   assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 1002
   assert line["scaling"] == "strong" and 0 < line["config"]["tuples_rank0"] < 1002
   assert line["value"] > 0
+
+
+def test_bench_two_ranks_multi_instance():
+  """The multi-instance variant (shared renders) under torchrun, 2 ranks on the
+  one GPU: each rank renders and evaluates its contiguous share of the images;
+  the line reports the whole job."""
+  import json
+  env = dict(os.environ, BOPX_DIST_BACKEND="gloo")
+  cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+         "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(),
+         os.path.join(REPO, "bench.py"), "--gpus", "2", "--config", "5", "--tuples", "1500",
+         "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+  r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=300)
+  assert r.returncode == 0, r.stderr[-3000:]
+  line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+  n = line["config"]["global_batch"]
+  assert line["n_gpus"] == 2 and n > 1000 and 0 < line["config"]["tuples_rank0"] < n  # ~1,500 (random k)
+  assert line["value"] > 0 and line["kernels"]["vsd"]["ms"] > 0
