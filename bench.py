@@ -335,10 +335,13 @@ def load_traffic(dom, args, n):
   return best
 
 
-def cpu_baseline(objs, d, n, seconds):
+def cpu_baseline(objs, d, n, seconds, gpu=None):
   """Oracle (C restatement of the reference per-tuple algorithm: two full-frame
   renders, three full-frame distance images, per-symmetry loops) on the host
-  cores, OpenMP over tuples, on a bounded sample of the same workload."""
+  cores, OpenMP over tuples, on a bounded sample of the same workload. gpu:
+  the timed steps' (vsd, mssd, mspd) outputs, checked against the oracle's
+  results for the sample (`check`: VSD rows bit-identical, largest MSSD / MSPD
+  relative difference)."""
   threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), 16))
   os.environ["OMP_NUM_THREADS"] = str(threads)
   from oracle import oracle
@@ -351,17 +354,31 @@ def cpu_baseline(objs, d, n, seconds):
     remap = np.searchsorted(used, fidx).astype(np.int32)
     fr = frames[used.tolist()].cpu().numpy()
     t0 = time.perf_counter()
-    oracle.bop19_batch(objs, h["obj"][:m], h["pe"][:m], h["pg"][:m], remap, fr, h["cam"][used],
-                       DELTA, TAUS, np.array([objs[o]["diameter"] for o in h["obj"][:m]]))
-    return time.perf_counter() - t0
+    res = oracle.bop19_batch(objs, h["obj"][:m], h["pe"][:m], h["pg"][:m], remap, fr,
+                             h["cam"][used], DELTA, TAUS,
+                             np.array([objs[o]["diameter"] for o in h["obj"][:m]]))
+    return time.perf_counter() - t0, res
 
   m0 = min(n, 2 * threads)
-  t0 = run(m0)
+  t0, _ = run(m0)
   m = int(min(n, max(m0, m0 * seconds / max(t0, 1e-3))))
-  t1 = run(m)
-  return {"value": m / t1, "unit": "tuples/s", "cores": threads, "kind": "port",
-          "sample": "%d tuples (first %d of this rank's workload), BOP19 set, %.1f s wall; "
-                    "oracle/bopx_oracle.c, reference per-tuple algorithm in C" % (m, m, t1)}
+  t1, (ov, om, op) = run(m)
+  out = {"value": m / t1, "unit": "tuples/s", "cores": threads, "kind": "port",
+         "sample": "%d tuples (first %d of this rank's workload), BOP19 set, %.1f s wall; "
+                   "oracle/bopx_oracle.c, reference per-tuple algorithm in C" % (m, m, t1)}
+  if gpu is not None:
+    gv, gm, gp = (t[:m].cpu().numpy() for t in gpu)
+
+    def rel(a, b):
+      fin = np.isfinite(a) & np.isfinite(b)
+      same_inf = np.array_equal(np.isfinite(a), np.isfinite(b)) and np.array_equal(a[~fin],
+                                                                                  b[~fin])
+      r = np.abs(a[fin] - b[fin]) / np.maximum(np.abs(b[fin]), 1e-300)
+      return float(r.max()) if r.size and same_inf else (0.0 if same_inf else float("inf"))
+    out["check"] = {"tuples": m, "vsd_rows_bit_identical": int((gv == ov).all(1).sum()),
+                    "mssd_max_rel": rel(gm, om), "mspd_max_rel": rel(gp, op),
+                    "note": "this run's GPU outputs vs the oracle on the sample (the checker)"}
+  return out
 
 
 def cpu_baseline_point(objs, d, n):
@@ -544,7 +561,7 @@ def main():
                                   "fp32 %.1f TF peaks" % (FP64_PEAK_TF, FP32_PEAK_TF)}}
     cpu = None
     if world == 1 and not args.no_cpu_baseline and len(args.cfg["errors"]) == 3:
-      cpu = cpu_baseline(objs, d, n, args.cpu_seconds)
+      cpu = cpu_baseline(objs, d, n, args.cpu_seconds, (out_vsd, out_mssd, out_mspd))
     elif world == 1 and not args.no_cpu_baseline and args.cfg["errors"] == ("add", "adi"):
       cpu = cpu_baseline_point(objs, d, n)
     line = {
