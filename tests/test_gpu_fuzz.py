@@ -1,0 +1,131 @@
+"""Randomised parity of the fused VSD kernel (raster + VSD, pose_error.py:17-93
+on renderer_vispy.py's depth) and of the shared-render path against the
+oracle, over meshes, cameras, image sizes and poses drawn at random: closed,
+jittered (non-convex), open and winding-flipped meshes with degenerate
+triangles, 6 to 60k triangles; LM-O to 1280x960 cameras with off-centre
+principal points; objects far, close (triangles of hundreds of pixels),
+straddling the image border, partly or wholly behind the camera; random
+delta, taus, normalisation and cost. Step cost bit for bit, tlinear within
+1e-12 absolute.
+
+BOPX_FUZZ_CASES scales the run (default 12 scenes x 8 tuples: ~20 s on the
+card, most of it the oracle's full-frame renders).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CASES = int(os.environ.get("BOPX_FUZZ_CASES", "12"))
+SIZES = [(320, 240), (640, 480), (720, 540), (1280, 960)]
+
+
+def _mesh(rng):
+  from bop_toolkit_amd import synth
+  n_lat, n_lon = int(rng.integers(2, 60)), int(rng.integers(3, 120))
+  if rng.random() < 0.1:
+    n_lat, n_lon = int(rng.integers(120, 180)), int(rng.integers(120, 170))  # ~40-60k tris
+  axes = tuple(rng.uniform(8.0, 150.0, 3))
+  pts, faces = synth.superellipsoid(n_lat, n_lon, axes, float(rng.uniform(0.3, 1.6)))
+  pts = np.asarray(pts, np.float64)
+  kind = rng.integers(0, 4)
+  if kind == 1:  # jittered: non-convex, self-occluding
+    pts = pts + rng.normal(0.0, 0.04 * min(axes), pts.shape)
+  elif kind == 2:  # open: a random tenth of the faces removed
+    faces = faces[rng.random(len(faces)) > 0.1]
+  elif kind == 3:  # winding flipped
+    faces = faces[:, ::-1]
+  if rng.random() < 0.5:  # degenerate triangles (repeated vertex)
+    k = max(1, len(faces) // 50)
+    deg = faces[rng.integers(0, len(faces), k)].copy()
+    deg[:, 2] = deg[:, 1]
+    faces = np.concatenate([faces, deg])
+  return pts.astype(np.float32).astype(np.float64), np.ascontiguousarray(faces, np.uint32)
+
+
+def _poses(rng, n, dia, fx, W):
+  from bop_toolkit_amd import synth
+  Rg = synth.random_rotations(rng, n)
+  z = rng.uniform(3.0 * dia, 30.0 * dia, n)
+  close = rng.random(n) < 0.15
+  z[close] = rng.uniform(0.6 * dia, 1.5 * dia, close.sum())  # large on screen / clipped
+  xy = rng.uniform(-0.45, 0.45, (n, 2)) * (z[:, None] * W / fx)  # some across the border
+  tg = np.concatenate([xy, z[:, None]], 1)
+  Re, te = synth.perturb(rng, Rg, tg, max_deg=25.0, t_sigma=0.1 * dia)
+  behind = rng.random(n) < 0.05
+  te[behind, 2] = -te[behind, 2] * rng.uniform(0.0, 1.0, behind.sum())
+  return Rg, tg, Re, te
+
+
+def _case(oracle_mod, seed):
+  from bop_toolkit_amd import _lib
+  from bop_toolkit_amd._lib import _d, _f, _i32, ptr
+  rng = np.random.default_rng(1000 + seed)
+  W, H = SIZES[rng.integers(0, len(SIZES))]
+  fx = float(rng.uniform(0.7, 2.2) * W)
+  fy = fx * float(rng.uniform(0.98, 1.02))
+  cx, cy = W / 2 + float(rng.uniform(-0.15, 0.15) * W), H / 2 + float(rng.uniform(-0.15, 0.15) * H)
+  pts, faces = _mesh(rng)
+  dia = float(np.linalg.norm(pts.max(0) - pts.min(0)))
+  n = 8
+  Rg, tg, Re, te = _poses(rng, n, dia, fx, W)
+  frames = []
+  for i in range(n):
+    dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, W, H)
+    dt = np.where(dg > 0, dg, float(rng.uniform(500.0, 3000.0))).astype(np.float32)
+    dt += rng.normal(0.0, rng.uniform(0.5, 8.0), dt.shape).astype(np.float32)
+    if rng.random() < 0.5:  # an occluder in front of part of the object
+      y0, x0 = int(rng.integers(0, H)), int(rng.integers(0, W))
+      dt[y0:y0 + H // 4, x0:x0 + W // 4] = float(tg[i, 2] - rng.uniform(5.0, 0.5 * dia))
+    dt[rng.random(dt.shape) < 0.1] = 0.0
+    frames.append(np.round(dt).astype(np.float32))
+  frames = np.stack(frames)
+  delta = float(rng.choice([5.0, 15.0, 15.7]))
+  taus = np.arange(0.05, 0.51, 0.05) if rng.random() < 0.7 else np.sort(rng.uniform(0.0, 0.6, 7))
+  normalized = bool(rng.random() < 0.8)
+  cost = "step" if rng.random() < 0.75 else "tlinear"
+  pe = np.concatenate([Re.reshape(n, 9), te], 1)
+  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
+  ids = np.full(n, 3, np.int32)
+  fi = np.arange(n, dtype=np.int32)
+  cam = np.tile([fx, fy, cx, cy], (n, 1)).astype(np.float64)
+  dias = np.full(n, dia)
+  ctx = _lib.Context(0)
+  try:
+    ctx.add_object(3, pts, faces)
+    out = np.empty((n, len(taus)))
+    ctx.call("bopx_vsd_batch", n, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(fi, _i32),
+             ptr(frames, _f), n, W, H, ptr(cam, _d), delta, 0, ptr(taus, _d), len(taus),
+             int(normalized), ptr(dias, _d), {"step": 0, "tlinear": 1}[cost], ptr(out, _d))
+    # the same tuples through the shared-render path (every render distinct here)
+    rpose = np.concatenate([pe, pg])
+    rid = np.full(2 * n, 3, np.int32)
+    rfi = np.concatenate([fi, fi])
+    er, gr = np.arange(n, dtype=np.int32), np.arange(n, 2 * n, dtype=np.int32)
+    out2 = np.empty((n, len(taus)))
+    ctx.call("bopx_vsd_shared_batch", 2 * n, ptr(rid, _i32), ptr(rpose, _d), ptr(rfi, _i32), n,
+             ptr(er, _i32), ptr(gr, _i32), ptr(frames, _f), n, W, H, ptr(cam, _d), delta, 0,
+             ptr(taus, _d), len(taus), int(normalized), ptr(dias, _d),
+             {"step": 0, "tlinear": 1}[cost], ptr(out2, _d))
+  finally:
+    ctx.close()
+  what = "seed %d: %dx%d, %d tris, %s, delta %g, %s" % (seed, W, H, len(faces), cost, delta,
+                                                        "normalized" if normalized else "raw")
+  for i in range(n):
+    de = oracle_mod.render_depth(pts, faces, Re[i], te[i], fx, fy, cx, cy, W, H)
+    dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, W, H)
+    ref = oracle_mod.vsd_depths(frames[i], de, dg, fx, fy, cx, cy, delta, taus, normalized, dia,
+                                cost)
+    if cost == "step":
+      assert list(out[i]) == ref, (what, i, out[i], ref)
+      assert list(out2[i]) == ref, (what, "shared", i, out2[i], ref)
+    else:
+      np.testing.assert_allclose(out[i], ref, rtol=0, atol=1e-12, err_msg=what)
+      np.testing.assert_allclose(out2[i], ref, rtol=0, atol=1e-12, err_msg=what)
+
+
+@pytest.mark.parametrize("seed", range(CASES))
+def test_fuzz_vsd_vs_oracle(oracle_mod, seed):
+  _case(oracle_mod, seed)
