@@ -6,7 +6,7 @@ triangles, 6 to 60k triangles; LM-O to 1280x960 cameras with off-centre
 principal points; objects far, close (triangles of hundreds of pixels),
 straddling the image border, partly or wholly behind the camera; random
 delta, taus, normalisation and cost. Step cost bit for bit, tlinear within
-1e-12 absolute.
+1e-12 absolute; the silhouette mode (cus / cou_bb_proj) exact on the same poses.
 
 BOPX_FUZZ_CASES scales the run (default 12 scenes x 8 tuples: ~20 s on the
 card, most of it the oracle's full-frame renders).
@@ -59,6 +59,17 @@ def _poses(rng, n, dia, fx, W):
   return Rg, tg, Re, te
 
 
+def _cover_ref(de, dg):
+  """pose_error.cus / cou_bb_proj inputs (pose_error.py:256-330) from two depth
+  maps: union, intersection, est / gt bboxes (empty: INT_MAX, INT_MAX, -1, -1)."""
+  me, mg = de > 0, dg > 0
+  row = [float(np.logical_or(me, mg).sum()), float(np.logical_and(me, mg).sum())]
+  for m in (me, mg):
+    ys, xs = m.nonzero()
+    row += [xs.min(), ys.min(), xs.max(), ys.max()] if len(xs) else [2147483647] * 2 + [-1] * 2
+  return np.array(row, np.float64)
+
+
 def _case(oracle_mod, seed):
   from bop_toolkit_amd import _lib
   from bop_toolkit_amd._lib import _d, _f, _i32, ptr
@@ -109,6 +120,10 @@ def _case(oracle_mod, seed):
              ptr(er, _i32), ptr(gr, _i32), ptr(frames, _f), n, W, H, ptr(cam, _d), delta, 0,
              ptr(taus, _d), len(taus), int(normalized), ptr(dias, _d),
              {"step": 0, "tlinear": 1}[cost], ptr(out2, _d))
+    # silhouette mode (cus, cou_bb_proj) on the same poses
+    out3 = np.empty((n, 10))
+    ctx.call("bopx_cover_batch", n, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(fi, _i32), n, W,
+             H, ptr(cam, _d), ptr(out3, _d))
   finally:
     ctx.close()
   what = "seed %d: %dx%d, %d tris, %s, delta %g, %s" % (seed, W, H, len(faces), cost, delta,
@@ -118,6 +133,7 @@ def _case(oracle_mod, seed):
     dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, W, H)
     ref = oracle_mod.vsd_depths(frames[i], de, dg, fx, fy, cx, cy, delta, taus, normalized, dia,
                                 cost)
+    assert np.array_equal(out3[i], _cover_ref(de, dg)), (what, "cover", i)
     if cost == "step":
       assert list(out[i]) == ref, (what, i, out[i], ref)
       assert list(out2[i]) == ref, (what, "shared", i, out2[i], ref)
