@@ -213,3 +213,67 @@ def _point_case(oracle_mod, seed):
 @pytest.mark.parametrize("seed", range(max(1, CASES // 3)))
 def test_fuzz_point_errors_vs_oracle(oracle_mod, seed):
   _point_case(oracle_mod, seed)
+
+
+def _gt_info_case(oracle_mod, seed):
+  """calc_gt_info (calc_gt_info.py:113-168) of random GT instances: the
+  reference's formulas on the oracle's 3x-canvas render, distance images and
+  bop19 visibility mask, against the GT-info mode of k_vsd (gt_side rows):
+  px_count_all / _valid / _visib, visib_fract and both bboxes exact, objects
+  truncated by the image border included."""
+  import torch
+  from bop_toolkit_amd import gt_side, misc
+  from bop_toolkit_amd.batch import BatchEvaluator
+  rng = np.random.default_rng(9000 + seed)
+  W, H = SIZES[rng.integers(0, 3)]
+  fx = float(rng.uniform(0.7, 2.0) * W)
+  fy = fx * float(rng.uniform(0.98, 1.02))
+  cx, cy = W / 2 + float(rng.uniform(-0.1, 0.1) * W), H / 2 + float(rng.uniform(-0.1, 0.1) * H)
+  pts, faces = _mesh(rng)
+  dia = float(np.linalg.norm(pts.max(0) - pts.min(0)))
+  n = 8
+  Rg, tg, _, _ = _poses(rng, n, dia, fx, W)
+  tg[:, 2] = np.maximum(tg[:, 2], 0.2 * dia)  # GT poses in front of the camera
+  delta = float(rng.choice([5.0, 15.0]))
+  frames = []
+  for i in range(n):
+    dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, W, H)
+    dt = np.where(dg > 0, dg, float(rng.uniform(500.0, 3000.0))).astype(np.float32)
+    dt += rng.normal(0.0, rng.uniform(0.5, 10.0), dt.shape).astype(np.float32)
+    dt[rng.random(dt.shape) < 0.1] = 0.0
+    frames.append(np.round(dt).astype(np.float32))
+  frames = np.stack(frames)
+  ev = BatchEvaluator(0)
+  ev.add_object(2, pts, faces)
+  dev = ev.device
+  t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+  pose = np.concatenate([Rg.reshape(n, 9), tg], 1)
+  cam = np.tile([fx, fy, cx, cy], (n, 1)).astype(np.float64)
+  rows, _ = ev.gt_info(ev.slots([2] * n), t(pose, torch.float64),
+                       t(np.arange(n, dtype=np.int32), torch.int32), t(frames, torch.float32),
+                       t(cam, torch.float64), delta)
+  rows = rows.cpu().numpy()
+  for i in range(n):
+    large = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx + W, cy + H, 3 * W, 3 * H)
+    dgt = large[H:2 * H, W:2 * W]
+    dist_gt = oracle_mod.dist_im(dgt, fx, fy, cx, cy)
+    dist_im = oracle_mod.dist_im(frames[i], fx, fy, cx, cy)
+    visib = oracle_mod.visib_mask(dist_im, dist_gt, delta)
+    n_all = int(np.sum(large > 0))
+    n_valid = int(np.sum(dist_im[dist_gt > 0] > 0))
+    n_visib = int(visib.sum())
+    bbox, bbox_visib = [-1] * 4, [-1] * 4
+    if n_visib > 0:
+      ys, xs = (large > 0).nonzero()
+      bbox = [int(v) for v in misc.calc_2d_bbox(xs - W, ys - H, (W, H))]
+      ys, xs = visib.nonzero()
+      bbox_visib = [int(v) for v in misc.calc_2d_bbox(xs, ys, (W, H))]
+    ref = {"px_count_all": n_all, "px_count_valid": n_valid, "px_count_visib": n_visib,
+           "visib_fract": float(n_visib / float(n_all) if n_all > 0 else 0.0),
+           "bbox_obj": bbox, "bbox_visib": bbox_visib}
+    assert gt_side.info_from_row(rows[i]) == ref, (seed, i)
+
+
+@pytest.mark.parametrize("seed", range(max(1, CASES // 3)))
+def test_fuzz_gt_info_vs_oracle(oracle_mod, seed):
+  _gt_info_case(oracle_mod, seed)
