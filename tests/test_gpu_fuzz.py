@@ -6,7 +6,8 @@ triangles, 6 to 60k triangles; LM-O to 1280x960 cameras with off-centre
 principal points; objects far, close (triangles of hundreds of pixels),
 straddling the image border, partly or wholly behind the camera; random
 delta, taus, normalisation and cost. Step cost bit for bit, tlinear within
-1e-12 absolute; the silhouette mode (cus / cou_bb_proj) exact on the same poses.
+1e-12 absolute; the silhouette mode (cus / cou_bb_proj) exact on the same poses,
+and the foreign-renderer entry (bopx_vsd_from_depths) on the oracle's depth maps.
 
 BOPX_FUZZ_CASES scales the run (default 12 scenes x 8 tuples: ~20 s on the
 card, most of it the oracle's full-frame renders).
@@ -124,22 +125,29 @@ def _case(oracle_mod, seed):
     out3 = np.empty((n, 10))
     ctx.call("bopx_cover_batch", n, ptr(ids, _i32), ptr(pe, _d), ptr(pg, _d), ptr(fi, _i32), n, W,
              H, ptr(cam, _d), ptr(out3, _d))
+    what = "seed %d: %dx%d, %d tris, %s, delta %g, %s" % (seed, W, H, len(faces), cost, delta,
+                                                          "normalized" if normalized else "raw")
+    for i in range(n):
+      de = oracle_mod.render_depth(pts, faces, Re[i], te[i], fx, fy, cx, cy, W, H)
+      dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, W, H)
+      ref = oracle_mod.vsd_depths(frames[i], de, dg, fx, fy, cx, cy, delta, taus, normalized, dia,
+                                  cost)
+      # the foreign-renderer path (k_vsd_depths) on the oracle's depth maps
+      out4 = np.empty(len(taus))
+      ctx.call("bopx_vsd_from_depths", W, H, ptr(frames[i], _f), ptr(de, _f), ptr(dg, _f), fx, fy,
+               cx, cy, delta, 0, ptr(taus, _d), len(taus), int(normalized), dia,
+               {"step": 0, "tlinear": 1}[cost], ptr(out4, _d))
+      assert np.array_equal(out3[i], _cover_ref(de, dg)), (what, "cover", i)
+      if cost == "step":
+        assert list(out[i]) == ref, (what, i, out[i], ref)
+        assert list(out2[i]) == ref, (what, "shared", i, out2[i], ref)
+        assert list(out4) == ref, (what, "from depths", i, out4, ref)
+      else:
+        np.testing.assert_allclose(out[i], ref, rtol=0, atol=1e-12, err_msg=what)
+        np.testing.assert_allclose(out2[i], ref, rtol=0, atol=1e-12, err_msg=what)
+        np.testing.assert_allclose(out4, ref, rtol=0, atol=1e-12, err_msg=what)
   finally:
     ctx.close()
-  what = "seed %d: %dx%d, %d tris, %s, delta %g, %s" % (seed, W, H, len(faces), cost, delta,
-                                                        "normalized" if normalized else "raw")
-  for i in range(n):
-    de = oracle_mod.render_depth(pts, faces, Re[i], te[i], fx, fy, cx, cy, W, H)
-    dg = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, W, H)
-    ref = oracle_mod.vsd_depths(frames[i], de, dg, fx, fy, cx, cy, delta, taus, normalized, dia,
-                                cost)
-    assert np.array_equal(out3[i], _cover_ref(de, dg)), (what, "cover", i)
-    if cost == "step":
-      assert list(out[i]) == ref, (what, i, out[i], ref)
-      assert list(out2[i]) == ref, (what, "shared", i, out2[i], ref)
-    else:
-      np.testing.assert_allclose(out[i], ref, rtol=0, atol=1e-12, err_msg=what)
-      np.testing.assert_allclose(out2[i], ref, rtol=0, atol=1e-12, err_msg=what)
 
 
 @pytest.mark.parametrize("seed", range(CASES))
