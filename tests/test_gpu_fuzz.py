@@ -156,7 +156,7 @@ def test_fuzz_vsd_vs_oracle(oracle_mod, seed):
 
 
 def _point_case(oracle_mod, seed):
-  """MSSD / MSPD / ADD / ADI (pose_error.py:96-184) of random objects: 3 to
+  """MSSD / MSPD / ADD / ADI / PROJ (pose_error.py:96-184, 217-232) of random objects: 3 to
   20k vertices, random discrete symmetry sets of 1 to 130 elements or a
   continuous axis (misc.py:43-90 discretisation), poses far, close, with gross
   outliers and behind the camera; every error within 1e-9 relative of the
@@ -199,7 +199,8 @@ def _point_case(oracle_mod, seed):
   dpe, dpg = t(pe, torch.float64), t(pg, torch.float64)
   got = {"mssd": ev.mssd(slots, dpe, dpg).cpu().numpy(),
          "mspd": ev.mspd(slots, dpe, dpg, t(np.tile(K.reshape(9), (n, 1)), torch.float64)).cpu().numpy(),
-         "add": ev.add(slots, dpe, dpg).cpu().numpy()}
+         "add": ev.add(slots, dpe, dpg).cpu().numpy(),
+         "proj": ev.proj(slots, dpe, dpg, t(np.tile(K.reshape(9), (n, 1)), torch.float64)).cpu().numpy()}
   small = np.nonzero([len(objs[o][0]) <= 1200 for o in obj])[0]
   got["adi"] = ev.adi(slots[t(small, torch.int64)], dpe[t(small, torch.int64)],
                       dpg[t(small, torch.int64)]).cpu().numpy()
@@ -207,7 +208,8 @@ def _point_case(oracle_mod, seed):
     pts, s12 = objs[obj[i]]
     ref = {"mssd": oracle_mod.mssd(pts, s12, pe[i], pg[i]),
            "mspd": oracle_mod.mspd(pts, s12, pe[i], pg[i], K),
-           "add": oracle_mod.add(pts, pe[i], pg[i])}
+           "add": oracle_mod.add(pts, pe[i], pg[i]),
+           "proj": oracle_mod.proj(pts, pe[i], pg[i], K)}
     for k, v in ref.items():
       g = got[k][i]
       assert (np.isnan(g) and np.isnan(v)) or g == v or abs(g - v) <= 1e-9 * abs(v), \
