@@ -230,7 +230,8 @@ def _gt_info_case(oracle_mod, seed):
   reference's formulas on the oracle's 3x-canvas render, distance images and
   bop19 visibility mask, against the GT-info mode of k_vsd (gt_side rows):
   px_count_all / _valid / _visib, visib_fract and both bboxes exact, objects
-  truncated by the image border included."""
+  truncated by the image border included; calc_gt_masks' mask / mask_visib
+  planes pixel for pixel."""
   import torch
   from bop_toolkit_amd import gt_side, misc
   from bop_toolkit_amd.batch import BatchEvaluator
@@ -263,6 +264,11 @@ def _gt_info_case(oracle_mod, seed):
                        t(np.arange(n, dtype=np.int32), torch.int32), t(frames, torch.float32),
                        t(cam, torch.float64), delta)
   rows = rows.cpu().numpy()
+  # calc_gt_masks (calc_gt_masks.py:104-125): image-size render, 0/255 planes
+  _, mk = ev.gt_info(ev.slots([2] * n), t(pose, torch.float64),
+                     t(np.arange(n, dtype=np.int32), torch.int32), t(frames, torch.float32),
+                     t(cam, torch.float64), delta, canvas_scale=1, masks=True)
+  mk = mk.cpu().numpy()
   for i in range(n):
     large = oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx + W, cy + H, 3 * W, 3 * H)
     dgt = large[H:2 * H, W:2 * W]
@@ -282,6 +288,13 @@ def _gt_info_case(oracle_mod, seed):
            "visib_fract": float(n_visib / float(n_all) if n_all > 0 else 0.0),
            "bbox_obj": bbox, "bbox_visib": bbox_visib}
     assert gt_side.info_from_row(rows[i]) == ref, (seed, i)
+    # calc_gt_masks renders at image size (its own float32 projection: not the
+    # crop of calc_gt_info's 3x canvas, whose principal point is offset)
+    dist_m = oracle_mod.dist_im(
+        oracle_mod.render_depth(pts, faces, Rg[i], tg[i], fx, fy, cx, cy, W, H), fx, fy, cx, cy)
+    visib_m = oracle_mod.visib_mask(dist_im, dist_m, delta)
+    assert np.array_equal(mk[i, 0], np.where(dist_m > 0, 255, 0).astype(np.uint8)), (seed, i)
+    assert np.array_equal(mk[i, 1], np.where(visib_m, 255, 0).astype(np.uint8)), (seed, i)
 
 
 @pytest.mark.parametrize("seed", range(max(1, CASES // 3)))
