@@ -194,48 +194,72 @@ def build_workload(ev, objs, args, rank, world, torch):
   return n, d
 
 
-def build_workload_multi(ev, objs, args, rank, world, torch):
-  """configs[5]: images with m objects, k instances of each (k uniform in
-  [kmin, kmax]) and k estimates per (image, object); tuples = every estimate x
-  every GT instance of its object. Test depth as in build_workload, composited
-  from every GT instance. This rank's images: a contiguous share."""
-  from bop_toolkit_amd import synth
-  from bop_toolkit_amd.batch import unique_renders
-  m, kmin, kmax = args.cfg["multi"]
-  rng = np.random.default_rng(args.seed + 2000)
+def plan_multi(cfg, meta, tuples, seed, rank, world, K, width, height):
+  """Host plan of the multi-instance workload (configs[5]): images with m
+  objects, k instances of each (k uniform in [kmin, kmax]) and k estimates
+  per (image, object); tuples = every estimate x every GT instance of its
+  object (k^2 per (image, object), eval_calc_errors.py:281-290). The whole
+  job is generated identically on every rank; images are then assigned to
+  the ranks by LPT on the SURVEY.md §8d per-tuple cost (shard.tuple_cost) —
+  the k^2 tuples per image vary 9x, so contiguous ranges would not balance.
+  meta: per object {"nv", "nf", "ns", "bbox": (lo, hi)}. Returns this rank's
+  tuples (global ids, local frame index), its GT instances, and every rank's
+  tuple count."""
+  from bop_toolkit_amd import shard, synth
+  m, kmin, kmax = cfg["multi"]
+  rng = np.random.default_rng(seed + 2000)
   per_img_mean = m * np.mean([k * k for k in range(kmin, kmax + 1)])
-  n_img_all = int(np.ceil(args.tuples / per_img_mean))
-  lo = rank * n_img_all // world
-  hi = (rank + 1) * n_img_all // world
-  K = getattr(synth, args.cfg["K"])
-  inst_obj, inst_f, inst_pose = [], [], []
-  t_obj, t_f, t_pe, t_pg, t_gid = [], [], [], [], []
-  gid = 0
+  n_img_all = int(np.ceil(tuples / per_img_mean))
+  i_img, i_obj, i_pose = [], [], []  # GT instances
+  t_img, t_obj, t_pe, t_pg = [], [], [], []  # tuples, global id = position
   for f in range(n_img_all):
-    for o in rng.choice(len(objs), m, replace=False):
+    for o in rng.choice(len(meta), m, replace=False):
       k = int(rng.integers(kmin, kmax + 1))
       Rg, tg = synth.gt_poses(rng, k)
       Re, te = synth.perturb(rng, Rg, tg)
       pg = np.concatenate([Rg.reshape(k, 9), tg], 1)
       pe = np.concatenate([Re.reshape(k, 9), te], 1)
-      mine = lo <= f < hi
-      if mine:
-        inst_obj += [o] * k
-        inst_f += [f - lo] * k
-        inst_pose.append(pg)
-      for i in range(k):
-        for j in range(k):
-          if mine:
-            t_obj.append(o)
-            t_f.append(f - lo)
-            t_pe.append(pe[i])
-            t_pg.append(pg[j])
-            t_gid.append(gid)
-          gid += 1
-  n_all, n_img = gid, hi - lo
-  obj = np.array(t_obj, np.int32)
-  frame_idx = np.array(t_f, np.int32)
-  pe, pg = np.stack(t_pe), np.stack(t_pg)
+      i_img += [f] * k
+      i_obj += [int(o)] * k
+      i_pose.append(pg)
+      t_img += [f] * (k * k)
+      t_obj += [int(o)] * (k * k)
+      t_pe.append(np.repeat(pe, k, axis=0))  # estimate i x GT j, i major
+      t_pg.append(np.tile(pg, (k, 1)))
+  t_img, t_obj = np.array(t_img, np.int64), np.array(t_obj, np.int32)
+  t_pe, t_pg = np.concatenate(t_pe), np.concatenate(t_pg)
+  i_img, i_obj, i_pose = np.array(i_img, np.int64), np.array(i_obj, np.int32), np.concatenate(i_pose)
+  n_all = len(t_img)
+  if world > 1:
+    lo = np.stack([meta[o]["bbox"][0] for o in t_obj])
+    hi = np.stack([meta[o]["bbox"][1] for o in t_obj])
+    roi = shard.roi_pixels(lo, hi, [t_pe, t_pg], K, width, height)
+    nv, nf, ns = (np.array([meta[o][k] for o in t_obj]) for k in ("nv", "nf", "ns"))
+    parts = shard.lpt_shard(shard.image_costs(t_img, shard.tuple_cost(nv, nf, ns, roi),
+                                              n_img_all), world)
+  else:
+    parts = [np.arange(n_img_all)]
+  per_img = np.bincount(t_img, minlength=n_img_all)
+  mine = parts[rank]
+  sel = np.nonzero(np.isin(t_img, mine))[0]
+  isel = np.nonzero(np.isin(i_img, mine))[0]
+  return {"gid": sel, "obj": t_obj[sel], "frame_idx": np.searchsorted(mine, t_img[sel]).astype(
+              np.int32), "pe": t_pe[sel], "pg": t_pg[sel],
+          "inst_obj": i_obj[isel], "inst_f": np.searchsorted(mine, i_img[isel]).astype(np.int32),
+          "inst_pose": i_pose[isel], "n_img": len(mine), "n_all": n_all,
+          "counts": [int(per_img[p].sum()) for p in parts]}
+
+
+def build_workload_multi(ev, objs, args, rank, world, torch):
+  """configs[5] on this rank (plan_multi: LPT shard of the images). Test depth
+  as in build_workload, composited from every GT instance."""
+  from bop_toolkit_amd import synth
+  from bop_toolkit_amd.batch import unique_renders
+  K = getattr(synth, args.cfg["K"])
+  meta = [{"nv": len(o["pts"]), "nf": len(o["faces"]), "ns": len(o["syms"]), "bbox": o["bbox"]}
+          for o in objs]
+  pl = plan_multi(args.cfg, meta, args.tuples, args.seed, rank, world, K, W, H)
+  obj, frame_idx, pe, pg, n_img = pl["obj"], pl["frame_idx"], pl["pe"], pl["pg"], pl["n_img"]
   n = len(obj)
   cam = np.tile([K[0, 0], K[1, 1], K[0, 2], K[1, 2]], (n_img, 1)).astype(np.float64)
   dev = ev.device
@@ -245,13 +269,12 @@ def build_workload_multi(ev, objs, args, rank, world, torch):
        "frame_idx": t(frame_idx, torch.int32), "cam": t(cam, torch.float64),
        "K": t(np.tile(K.reshape(9), (n, 1)), torch.float64),
        "diameters": t([objs[o]["diameter"] for o in obj], torch.float64),
-       "gid": t(t_gid, torch.int64), "n_total": n_all,
-       "counts": [None] * world,
+       "gid": t(pl["gid"], torch.int64), "n_total": pl["n_all"], "counts": pl["counts"],
        "renders": {"slots": ev.slots(ro), "pose": t(rp, torch.float64),
                    "frame_idx": t(rf, torch.int32), "est": t(er, torch.int32),
                    "gt": t(gr, torch.int32), "n": len(ro)}}
-  frames = ev.render(ev.slots(inst_obj), t(np.concatenate(inst_pose), torch.float64),
-                     t(inst_f, torch.int32), d["cam"], n_img, W, H)
+  frames = ev.render(ev.slots(pl["inst_obj"]), t(pl["inst_pose"], torch.float64),
+                     t(pl["inst_f"], torch.int32), d["cam"], n_img, W, H)
   g = torch.Generator(device=dev)
   g.manual_seed(args.seed + rank)
   for c0 in range(0, n_img, 1024):
@@ -424,11 +447,6 @@ def main():
   objs = build_objects(ev, args, torch)
   multi = "multi" in args.cfg
   n, d = (build_workload_multi if multi else build_workload)(ev, objs, args, rank, world, torch)
-  if multi and world > 1:  # the shares are uneven: exchange the counts once
-    dv = ev.device if backend == "nccl" else torch.device("cpu")
-    cl = [torch.zeros(1, dtype=torch.int64, device=dv) for _ in range(world)]
-    dist.all_gather(cl, torch.tensor([n], dtype=torch.int64, device=dv))
-    d["counts"] = [int(c.item()) for c in cl]
   meta = os.environ.get("BOPX_BENCH_META")  # tools/pmc.sh: what the counters measured
   if meta and rank == 0:
     with open(meta, "w") as f:

@@ -87,6 +87,11 @@ class BopxError(RuntimeError):
   pass
 
 
+class BopxOOMError(BopxError):
+  """BOPX_E_OOM: device scratch did not fit (the caller may split the batch or
+  take a path with a smaller footprint)."""
+
+
 def load():
   """Load libbopx.so (raises ImportError if it has not been built)."""
   global _lib
@@ -162,6 +167,8 @@ class Context:
       raise ValueError(msg)
     if rc == E_NOT_FOUND:
       raise KeyError(msg)
+    if rc == E_OOM:
+      raise BopxOOMError("%s failed (rc=%d): %s" % (what, rc, msg))
     raise BopxError("%s failed (rc=%d): %s" % (what, rc, msg))
 
   def call(self, name, *args):

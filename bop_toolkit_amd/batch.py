@@ -113,28 +113,55 @@ class BatchEvaluator:
                   _p(out), _stream(self.device))
     return out
 
+  def _vsd_out(self, n, n_tau, out, delta_flags):
+    """Output buffer of a VSD launch: n x n_tau float64, plus n union counts
+    after them when delta_flags carries BOPX_VSD_UNIONS (the kernels write
+    them at out + n * n_tau). A caller-supplied out is checked for size."""
+    need = n * n_tau + (n if delta_flags & _lib.VSD_UNIONS else 0)
+    if out is None:
+      return torch.empty(need, dtype=torch.float64, device=self.device)
+    if (out.dtype != torch.float64 or out.device != self.device or not out.is_contiguous()
+        or out.numel() < need):
+      raise ValueError("VSD out must be a contiguous float64 tensor on %s with >= %d elements"
+                       % (self.device, need))
+    return out
+
+  @staticmethod
+  def _vsd_result(buf, n, n_tau, delta_flags):
+    v = buf.view(-1)[:n * n_tau].view(n, n_tau)
+    if delta_flags & _lib.VSD_UNIONS:
+      return v, buf.view(-1)[n * n_tau:n * n_tau + n]
+    return v
+
   def vsd(self, slots, pose_est, pose_gt, frame_idx, frames, cam, delta, taus, diameters,
           normalized_by_diameter=True, cost_type="step", out=None, delta_flags=0):
+    """VSD [n, n_tau] of every tuple (k_vsd). With BOPX_VSD_UNIONS in
+    delta_flags, returns (vsd, unions [n]) instead."""
     n = slots.numel()
     taus = np.ascontiguousarray(taus, np.float64)
     code = {"step": _lib.COST_STEP, "tlinear": _lib.COST_TLINEAR}.get(cost_type)
     if code is None:
       raise ValueError("Unknown pixel matching cost.")
+    buf = self._vsd_out(n, len(taus), out, delta_flags)
     if len(taus) > _lib.MAX_TAUS:  # one launch per MAX_TAUS thresholds (any number of taus)
-      out = self._out(n, len(taus)) if out is None else out
+      v = buf.view(-1)[:n * len(taus)].view(n, len(taus))
       for k0 in range(0, len(taus), _lib.MAX_TAUS):
         k1 = min(k0 + _lib.MAX_TAUS, len(taus))
-        out[:, k0:k1] = self.vsd(slots, pose_est, pose_gt, frame_idx, frames, cam, delta,
-                                 taus[k0:k1], diameters, normalized_by_diameter, cost_type,
-                                 delta_flags=delta_flags)
-      return out
+        # union counts (the same for every tau) from the first launch only
+        fl = delta_flags if k0 == 0 else delta_flags & ~_lib.VSD_UNIONS
+        r = self.vsd(slots, pose_est, pose_gt, frame_idx, frames, cam, delta, taus[k0:k1],
+                     diameters, normalized_by_diameter, cost_type, delta_flags=fl)
+        if fl & _lib.VSD_UNIONS:
+          r, u = r
+          buf.view(-1)[n * len(taus):n * len(taus) + n] = u
+        v[:, k0:k1] = r
+      return self._vsd_result(buf, n, len(taus), delta_flags)
     H, W = int(frames.shape[-2]), int(frames.shape[-1])
-    out = self._out(n, len(taus)) if out is None else out
     self.ctx.call("bopx_vsd_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(frame_idx),
                   _p(frames), W, H, _p(cam), float(delta), int(delta_flags),
                   taus.ctypes.data_as(_lib._d), len(taus), int(bool(normalized_by_diameter)),
-                  _p(diameters), code, _p(out), _stream(self.device))
-    return out
+                  _p(diameters), code, _p(buf), _stream(self.device))
+    return self._vsd_result(buf, n, len(taus), delta_flags)
 
   def vsd_shared(self, render_slots, render_poses, render_frame_idx, est_render, gt_render,
                  frames, cam, delta, taus, diameters, normalized_by_diameter=True,
@@ -148,22 +175,27 @@ class BatchEvaluator:
     code = {"step": _lib.COST_STEP, "tlinear": _lib.COST_TLINEAR}.get(cost_type)
     if code is None:
       raise ValueError("Unknown pixel matching cost.")
-    out = self._out(n, len(taus)) if out is None else out
+    buf = self._vsd_out(n, len(taus), out, delta_flags)
     if len(taus) > _lib.MAX_TAUS:
+      v = buf.view(-1)[:n * len(taus)].view(n, len(taus))
       for k0 in range(0, len(taus), _lib.MAX_TAUS):
         k1 = min(k0 + _lib.MAX_TAUS, len(taus))
-        out[:, k0:k1] = self.vsd_shared(render_slots, render_poses, render_frame_idx,
-                                        est_render, gt_render, frames, cam, delta, taus[k0:k1],
-                                        diameters, normalized_by_diameter, cost_type,
-                                        delta_flags=delta_flags)
-      return out
+        fl = delta_flags if k0 == 0 else delta_flags & ~_lib.VSD_UNIONS
+        r = self.vsd_shared(render_slots, render_poses, render_frame_idx, est_render, gt_render,
+                            frames, cam, delta, taus[k0:k1], diameters, normalized_by_diameter,
+                            cost_type, delta_flags=fl)
+        if fl & _lib.VSD_UNIONS:
+          r, u = r
+          buf.view(-1)[n * len(taus):n * len(taus) + n] = u
+        v[:, k0:k1] = r
+      return self._vsd_result(buf, n, len(taus), delta_flags)
     H, W = int(frames.shape[-2]), int(frames.shape[-1])
     self.ctx.call("bopx_vsd_shared_batch_dev", render_slots.numel(), _p(render_slots),
                   _p(render_poses), _p(render_frame_idx), n, _p(est_render), _p(gt_render),
                   _p(frames), W, H, _p(cam), float(delta), int(delta_flags),
                   taus.ctypes.data_as(_lib._d), len(taus), int(bool(normalized_by_diameter)),
-                  _p(diameters), code, _p(out), _stream(self.device))
-    return out
+                  _p(diameters), code, _p(buf), _stream(self.device))
+    return self._vsd_result(buf, n, len(taus), delta_flags)
 
   def cover(self, slots, pose_est, pose_gt, frame_idx, cam, width, height, out=None):
     """Silhouette overlap per tuple for cus / cou_bb_proj: float64 [n, 10] =

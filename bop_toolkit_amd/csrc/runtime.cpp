@@ -1092,7 +1092,10 @@ static int vsd_shared_core(bopx_ctx* c, int64_t nr, const int32_t* rslots, const
   if (int r = fill_vsd_args(c, a, width, height, delta, flags, taus, n_tau, normalized,
                             cost_type))
     return r;
-  if (n <= 0 || nr <= 0) return BOPX_OK;
+  if (n <= 0) return BOPX_OK;
+  // tuples without renders: every render index is out of range, and nothing
+  // would write the caller's output
+  if (nr <= 0) return fail(c, BOPX_E_INVALID, "%lld tuples but no renders", (long long)n);
   int4* d_roi = nullptr;
   int64_t* d_off = nullptr;
   uint32_t* d_q = nullptr;
@@ -1123,7 +1126,12 @@ static int vsd_shared_core(bopx_ctx* c, int64_t nr, const int32_t* rslots, const
   }
   // q buffers (0 = background), then the row spans: min 0x7F7F7F7F, max -1
   const size_t qn = (size_t)std::max<int64_t>(total, 1), sn = (size_t)std::max<int64_t>(rows, 1);
-  if (e == hipSuccess && hipMallocAsync((void**)&d_q, 4 * (qn + 2 * sn), s) != hipSuccess) {
+  // BOPX_SHARED_MAX_BYTES caps this scratch (read per call; unset = no cap
+  // beyond the device's free memory): past it the call fails like an OOM
+  const char* cap_env = getenv("BOPX_SHARED_MAX_BYTES");
+  const bool over_cap = cap_env && 4 * (qn + 2 * sn) > (size_t)strtoull(cap_env, nullptr, 10);
+  if (e == hipSuccess &&
+      (over_cap || hipMallocAsync((void**)&d_q, 4 * (qn + 2 * sn), s) != hipSuccess)) {
     (void)hipGetLastError();
     d_q = nullptr;
     (void)hipFreeAsync(d_roi, s);

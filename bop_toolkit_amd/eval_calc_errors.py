@@ -429,11 +429,18 @@ def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs
     ro, rp, rf, er, gr = (None,) * 5 if single and SHARED_RENDER_RATIO < 2 else \
         unique_renders(obj, pe, pg, fidx_h)
     if ro is not None and len(ro) <= SHARED_RENDER_RATIO * n:
-      return ev.vsd_shared(ev.slots(ro), T(rp, torch.float64), T(rf, torch.int32),
-                           T(er, torch.int32), T(gr, torch.int32), d_frames,
-                           T(cam, torch.float64), delta, p["vsd_taus"], T(dia, torch.float64),
-                           normalized_by_diameter=p["vsd_normalized_by_diameter"],
-                           cost_type="step", delta_flags=runtime.delta_flags(delta))
+      from ._lib import BopxOOMError
+      try:
+        return ev.vsd_shared(ev.slots(ro), T(rp, torch.float64), T(rf, torch.int32),
+                             T(er, torch.int32), T(gr, torch.int32), d_frames,
+                             T(cam, torch.float64), delta, p["vsd_taus"], T(dia, torch.float64),
+                             normalized_by_diameter=p["vsd_normalized_by_diameter"],
+                             cost_type="step", delta_flags=runtime.delta_flags(delta))
+      except BopxOOMError:
+        # the shared path's ROI-sized depth buffers (outside torch's caching
+        # allocator) did not fit: the fused kernel needs no such scratch and
+        # gives the same rows bit for bit
+        torch.cuda.empty_cache()
     return ev.vsd(slots, d_pe, d_pg, fidx, d_frames,
                   T(cam, torch.float64), delta, p["vsd_taus"], T(dia, torch.float64),
                   normalized_by_diameter=p["vsd_normalized_by_diameter"], cost_type="step",

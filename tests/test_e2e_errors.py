@@ -160,3 +160,34 @@ def test_models_registry_reused_across_error_types():
   assert runs[2] == []  # MSPD: same symmetry key, nothing to do
   assert sorted(c[1] for c in runs[3]) == ids and all(c[0] == "syms" for c in runs[3])
   assert runs[4] == []  # VSD does not need symmetry sets
+
+
+@pytest.mark.gpu
+def test_caller_shared_oom_falls_back_to_fused(tmp_path, monkeypatch):
+  """when the shared-render scratch does not fit (forced here with
+  BOPX_SHARED_MAX_BYTES=1, read per call), the caller takes the fused kernel
+  for the same tuples: the VSD files stay byte-identical to the reference's."""
+  from bop_toolkit_amd import _lib
+  monkeypatch.setenv("BOPX_SHARED_MAX_BYTES", "1")
+  runs = [r for r in RUNS["runs"] if r[0] == "vsd"]
+  assert runs
+  for et, n_top in runs:
+    p = _params(et, n_top, str(tmp_path))
+    written = ece.run(p, 0)
+    for path in written:
+      rel = os.path.relpath(path, os.path.join(str(tmp_path), "synth_lmo-test"))
+      assert _load(path)[0] == _load(os.path.join(E2E, "expected", rel))[0], rel
+  # and the shared entry itself reports the cap as an OOM
+  import torch
+  from bop_toolkit_amd.batch import BatchEvaluator
+  from bop_toolkit_amd import synth
+  ev = BatchEvaluator(0)
+  pts, faces = synth.superellipsoid(10, 20, (40.0, 30.0, 50.0), 0.7)
+  ev.add_object(1, pts, faces)
+  d = ev.device
+  pose = torch.tensor([[1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 600.0]], dtype=torch.float64, device=d)
+  z = torch.zeros(1, dtype=torch.int32, device=d)
+  with pytest.raises(_lib.BopxOOMError):
+    ev.vsd_shared(ev.slots([1]), pose, z, z, z, torch.zeros((1, 480, 640), device=d),
+                  torch.tensor([[572.0, 573.0, 320.0, 240.0]], dtype=torch.float64, device=d),
+                  15.0, [0.05], torch.tensor([100.0], dtype=torch.float64, device=d))

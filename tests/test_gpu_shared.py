@@ -192,6 +192,51 @@ def test_shared_dev_bad_index_gives_nan():
   assert np.isnan(out[1]).all() and np.isfinite(out[0]).all()
 
 
+def test_shared_dev_zero_renders_refused():
+  """n > 0 tuples with no renders used to return OK with the output
+  unwritten; it is refused now (nothing could be indexed)."""
+  import torch
+  ev, objs, obj, fi, pe, pg, fr, cam, dia, t = _workload(53, n_img=1, ks=(1,))
+  e = torch.zeros(2, dtype=torch.int32, device=ev.device)
+  with pytest.raises(ValueError):
+    ev.vsd_shared(ev.slots([]), t(np.zeros((0, 12)), torch.float64), t([], torch.int32), e, e,
+                  t(fr, torch.float32), t(cam, torch.float64), 15.0,
+                  np.arange(0.05, 0.51, 0.05), t(dia[:2], torch.float64))
+
+
+@pytest.mark.parametrize("ntau", [10, 23])
+def test_unions_flag_batch_api(ntau):
+  """BOPX_VSD_UNIONS through BatchEvaluator gets its own n slots
+  (no write past the tensor): (vsd, unions) returned, vsd equal to the call
+  without the flag, the same unions from the fused and the shared path, and a
+  too-small caller-supplied out is refused."""
+  import torch
+  from bop_toolkit_amd import _lib
+  from bop_toolkit_amd.batch import unique_renders
+  ev, objs, obj, fi, pe, pg, fr, cam, dia, t = _workload(55, n_img=3)
+  taus = np.linspace(0.02, 0.6, ntau)
+  n = len(obj)
+  args = (ev.slots(obj), t(pe, torch.float64), t(pg, torch.float64), t(fi, torch.int32),
+          t(fr, torch.float32), t(cam, torch.float64), 15.0, taus, t(dia, torch.float64))
+  plain = ev.vsd(*args).cpu().numpy()
+  guard = torch.full((n * ntau + n + 64,), 7.0, dtype=torch.float64, device=ev.device)
+  v, u = ev.vsd(*args, out=guard, delta_flags=_lib.VSD_UNIONS)
+  assert np.array_equal(v.cpu().numpy(), plain)
+  assert (guard[n * ntau + n:] == 7.0).all()  # nothing written past the unions
+  un = u.cpu().numpy()
+  assert (un >= 0).all() and (un > 0).any()
+  assert np.array_equal(plain[un == 0], np.ones_like(plain[un == 0]))
+  ro, rp, rf, er, gr = unique_renders(obj, pe, pg, fi)
+  vs, us = ev.vsd_shared(ev.slots(ro), t(rp, torch.float64), t(rf, torch.int32),
+                         t(er, torch.int32), t(gr, torch.int32), t(fr, torch.float32),
+                         t(cam, torch.float64), 15.0, taus, t(dia, torch.float64),
+                         delta_flags=_lib.VSD_UNIONS)
+  assert np.array_equal(vs.cpu().numpy(), plain) and np.array_equal(us.cpu().numpy(), un)
+  with pytest.raises(ValueError):
+    ev.vsd(*args, out=torch.empty((n, ntau), dtype=torch.float64, device=ev.device),
+           delta_flags=_lib.VSD_UNIONS)
+
+
 def test_shared_wide_image_column_blocks(oracle_mod):
   """Unions wider than k_vsd_pair's 2,048-column LDS block (4,096 x 512
   image, estimates shifted right by up to ~3,700 px, one partly off the right

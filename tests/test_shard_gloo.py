@@ -177,3 +177,75 @@ def test_caller_cost_model_shapes_the_shard():
       assert np.ptp(c) > 0
     parts = ece.shard_todo(recs, todo, 3, c)
     assert np.array_equal(np.sort(np.concatenate(parts)), np.arange(len(todo)))
+
+
+def _multi_meta():
+  from bop_toolkit_amd import synth
+  meta = []
+  for o in range(30):
+    pts, faces = synth.superellipsoid(8, 12, (30.0 + o, 40.0, 50.0 - o), 0.7)
+    meta.append({"nv": len(pts), "nf": len(faces), "ns": 1 + o % 8,
+                 "bbox": (pts.min(0), pts.max(0))})
+  return meta
+
+
+def _multi_worker(rank, world, port, out_path):
+  import bench
+  from bop_toolkit_amd import synth
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  pl = bench.plan_multi(bench.CONFIGS[5], _multi_meta(), 3000, 7, rank, world, synth.TLESS_K,
+                        720, 540)
+  n = len(pl["gid"])
+  assert pl["counts"][rank] == n
+  # rows: a function of the tuple's content (pose and object), so the gathered
+  # table shows each global id got the tuple the single-rank plan has there
+  rows = torch.from_numpy(np.concatenate([pl["pe"], pl["pg"], pl["obj"][:, None]], 1))
+  table = shard.gather_rows(rows, torch.from_numpy(pl["gid"]), pl["n_all"], counts=pl["counts"])
+  if rank == 0:
+    np.save(out_path, table.numpy())
+  dist.barrier()
+  dist.destroy_process_group()
+
+
+def test_multi_instance_plan_lpt_covers_every_tuple_once(tmp_path):
+  """bench.py configs[5] under 4 ranks (gloo): images assigned by LPT on the
+  §8d cost (not contiguous ranges), every tuple on exactly one rank (the
+  gather checks ids are a permutation), rows equal to the one-rank plan's,
+  GT instances and frames consistent with the rank's tuples, and the LPT
+  loads tighter than contiguous ranges of the same images."""
+  import sys
+  sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+  import bench
+  from bop_toolkit_amd import synth
+  meta = _multi_meta()
+  one = bench.plan_multi(bench.CONFIGS[5], meta, 3000, 7, 0, 1, synth.TLESS_K, 720, 540)
+  assert np.array_equal(one["gid"], np.arange(one["n_all"]))
+  out = str(tmp_path / "multi.npy")
+  mp.spawn(_multi_worker, args=(4, _free_port(), out), nprocs=4, join=True)
+  table = np.load(out)
+  ref = np.concatenate([one["pe"], one["pg"], one["obj"][:, None]], 1)
+  assert np.array_equal(table, ref)
+  plans = [bench.plan_multi(bench.CONFIGS[5], meta, 3000, 7, r, 4, synth.TLESS_K, 720, 540)
+           for r in range(4)]
+  assert sorted(np.concatenate([p["gid"] for p in plans]).tolist()) == list(range(one["n_all"]))
+  for p in plans:
+    # every tuple's frame holds a GT instance of its object
+    inst = set(zip(p["inst_f"].tolist(), p["inst_obj"].tolist()))
+    assert set(zip(p["frame_idx"].tolist(), p["obj"].tolist())) <= inst
+    assert p["frame_idx"].max() < p["n_img"]
+  # LPT balance vs contiguous image ranges (cost = the planner's own model)
+  from bop_toolkit_amd import shard
+  lo = np.stack([meta[o]["bbox"][0] for o in one["obj"]])
+  hi = np.stack([meta[o]["bbox"][1] for o in one["obj"]])
+  roi = shard.roi_pixels(lo, hi, [one["pe"], one["pg"]], synth.TLESS_K, 720, 540)
+  c = shard.tuple_cost([meta[o]["nv"] for o in one["obj"]], [meta[o]["nf"] for o in one["obj"]],
+                       [meta[o]["ns"] for o in one["obj"]], roi)
+  lpt = [c[p["gid"]].sum() for p in plans]
+  img = one["frame_idx"]
+  n_img = one["n_img"]
+  contig = [c[(img >= r * n_img // 4) & (img < (r + 1) * n_img // 4)].sum() for r in range(4)]
+  assert max(lpt) / np.mean(lpt) <= max(contig) / np.mean(contig) + 1e-12
+  ic = shard.image_costs(img, c, n_img)
+  assert max(lpt) <= np.mean(lpt) + ic.max()  # the LPT bound
