@@ -25,6 +25,12 @@
  *   oracle_render_depth renderer_py.py:422-555 / renderer_vispy.py:433-538
  *                       semantics (eye-Z, pixel centres, no culling, z-test
  *                       LESS, background 0) as specified in DESIGN.md §4.
+ *   oracle_vsd_zbuf_batch  the spec's eye Z passed through a MODEL of vispy's
+ *                       z-buffer (window depth with the per-render near / far of
+ *                       renderer_vispy.py:447-456, stored as float32 or 24 / 16-bit
+ *                       fixed point, read back and linearised as :526-536) before
+ *                       the VSD of pose_error.py:47-93: a study of what the
+ *                       spec's exact eye Z leaves unpinned.
  * Build: oracle/Makefile (gcc -O2 -ffp-contract=off -fopenmp).
  */
 #include <math.h>
@@ -425,6 +431,137 @@ void oracle_coverage(const double* pts, int64_t nv, const uint32_t* faces, int64
             (w2 > 0 || (w2 == 0 && tl2)))
           out[(size_t)r * W + col] += 1;
       }
+  }
+}
+
+/* ------------------------------------------------ z-buffer quantisation model */
+/* The depth vispy returns is not the eye Z but its window depth, stored in the
+   depth render buffer (gloo.RenderBuffer, renderer_vispy.py:294: the driver
+   picks the format, typically 24-bit fixed point, 16 or 32F possible), read
+   back as float32 (:526) and linearised in float64 (:532-535; NumPy 2 promotes
+   the float32 buffer by the float64 scalars, NEP 50). Model, per render:
+   - near / far = min / max over the model's 8 bbox corners (misc.calc_3d_bbox
+     of the float64 PLY points, :313-324) of the float32 view row 2 (:440-452),
+     evaluated in float64;
+   - window depth of a pixel whose spec depth is Z (float32 eye Z):
+     z_w = f (Z - n) / (Z (f - n)) (the y_down projection of _calc_calib_proj,
+     :187-232, glDepthRange 0..1), exact (float64);
+   - stored: bits 32 -> (float)z_w; bits 24 / 16 -> D = round(z_w (2^b - 1))
+     as unorm, read back as (float)(D / (2^b - 1)); z_w < 0 (Z below the near
+     plane by rounding; GL would clip) stored as 0;
+   - background where the read value is 1 (cleared, :534-536), else
+     depth = mult / (zr + addi), mult = n f / (n - f), addi = f / (n - f).
+   bits 0 returns the spec depth itself (widened to float64). */
+static void zbuf_depth(const float* spec, int W, int H, const double* bbmin, const double* bbsz,
+                       const double* pose, int bits, double* out) {
+  const float r6 = (float)pose[6], r7 = (float)pose[7], r8 = (float)pose[8], tz = (float)pose[11];
+  double n = INFINITY, f = -INFINITY;
+  for (int k = 0; k < 8; ++k) {
+    double x = bbmin[0] + ((k >> 2) & 1 ? bbsz[0] : 0.0);
+    double y = bbmin[1] + ((k >> 1) & 1 ? bbsz[1] : 0.0);
+    double z = bbmin[2] + (k & 1 ? bbsz[2] : 0.0);
+    double ez = (((double)r6 * x + (double)r7 * y) + (double)r8 * z) + (double)tz;
+    if (ez < n) n = ez;
+    if (ez > f) f = ez;
+  }
+  const double mult = (n * f) / (n - f), addi = f / (n - f);
+  const double scale = bits == 24 ? 16777215.0 : 65535.0;
+  for (size_t i = 0; i < (size_t)W * H; ++i) {
+    const float Z = spec[i];
+    if (bits == 0 || !(Z > 0.0f)) {
+      out[i] = (double)Z;
+      continue;
+    }
+    double zw = f * ((double)Z - n) / ((double)Z * (f - n));
+    float zr;
+    if (bits == 32) {
+      zr = (float)zw;
+    } else {
+      double D = floor((zw < 0.0 ? 0.0 : zw) * scale + 0.5);
+      if (D > scale) D = scale;
+      zr = (float)(D / scale);
+    }
+    out[i] = zr == 1.0f ? 0.0 : mult / ((double)zr + addi);
+  }
+}
+
+/* VSD of pose_error.py:47-93 (step cost) with float64 model depths. */
+static void vsd_step64(int W, int H, const float* depth_test, const double* de, const double* dg,
+                       double fx, double fy, double cx, double cy, double delta,
+                       const double* taus, int n_tau, double diameter, double* out) {
+  float delta32 = (float)delta;
+  int64_t n_union = 0, n_inter = 0, cnt[64];
+  for (int k = 0; k < n_tau; ++k) cnt[k] = 0;
+  for (int r = 0; r < H; ++r) {
+    double pY = ((double)r - cy) / fy;
+    for (int c = 0; c < W; ++c) {
+      double pX = ((double)c - cx) / fx;
+      size_t i = (size_t)r * W + c;
+      double dep[3] = {(double)depth_test[i], dg[i], de[i]}, dist[3];
+      for (int k = 0; k < 3; ++k) {
+        double d = dep[k], a = pX * d, b = pY * d;
+        dist[k] = sqrt((a * a + b * b) + d * d);
+      }
+      int vg = visib_px(dist[0], dist[1], delta32, delta, 0, 1);
+      int ve = visib_px(dist[0], dist[2], delta32, delta, 0, 1);
+      ve = ve || (vg && dist[2] > 0);
+      if (vg || ve) ++n_union;
+      if (vg && ve) {
+        ++n_inter;
+        double dd = fabs(dist[1] - dist[2]) / diameter;
+        for (int k = 0; k < n_tau; ++k)
+          if (dd >= taus[k]) ++cnt[k];
+      }
+    }
+  }
+  for (int k = 0; k < n_tau; ++k)
+    out[k] = n_union == 0 ? 1.0 : (double)(cnt[k] + (n_union - n_inter)) / (double)n_union;
+}
+
+/* Per tuple: both spec renders once, then the step-cost VSD (normalised by the
+   diameter) under every z-buffer model of `bits` (n_modes entries of 0 / 32 /
+   24 / 16): out[(i * n_modes + m) * n_tau + k]. OpenMP over tuples. */
+void oracle_vsd_zbuf_batch(int64_t n, const int32_t* obj, const int64_t* pts_off,
+                           const int64_t* nv, const double* pts_all, const int64_t* face_off,
+                           const int64_t* nf, const uint32_t* faces_all, const double* pose_est,
+                           const double* pose_gt, const int32_t* frame_idx, const float* frames,
+                           int W, int H, const double* cam, double delta, const double* taus,
+                           int n_tau, const double* diameters, int n_modes, const int32_t* bits,
+                           double* out) {
+#pragma omp parallel
+  {
+    float* se = (float*)malloc(sizeof(float) * (size_t)W * H);
+    float* sg = (float*)malloc(sizeof(float) * (size_t)W * H);
+    double* de = (double*)malloc(sizeof(double) * (size_t)W * H);
+    double* dg = (double*)malloc(sizeof(double) * (size_t)W * H);
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t i = 0; i < n; ++i) {
+      int o = obj[i];
+      const double* pts = pts_all + 3 * pts_off[o];
+      double bmin[3] = {INFINITY, INFINITY, INFINITY}, bmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (int64_t v = 0; v < nv[o]; ++v)
+        for (int a = 0; a < 3; ++a) {
+          if (pts[3 * v + a] < bmin[a]) bmin[a] = pts[3 * v + a];
+          if (pts[3 * v + a] > bmax[a]) bmax[a] = pts[3 * v + a];
+        }
+      double bsz[3] = {bmax[0] - bmin[0], bmax[1] - bmin[1], bmax[2] - bmin[2]};
+      const uint32_t* fc = faces_all + 3 * face_off[o];
+      const double* cm = cam + 4 * frame_idx[i];
+      const double* pe = pose_est + 12 * i;
+      const double* pg = pose_gt + 12 * i;
+      oracle_render_depth(pts, nv[o], fc, nf[o], pe, pe + 9, cm[0], cm[1], cm[2], cm[3], W, H, se);
+      oracle_render_depth(pts, nv[o], fc, nf[o], pg, pg + 9, cm[0], cm[1], cm[2], cm[3], W, H, sg);
+      for (int m = 0; m < n_modes; ++m) {
+        zbuf_depth(se, W, H, bmin, bsz, pe, bits[m], de);
+        zbuf_depth(sg, W, H, bmin, bsz, pg, bits[m], dg);
+        vsd_step64(W, H, frames + (size_t)frame_idx[i] * W * H, de, dg, cm[0], cm[1], cm[2],
+                   cm[3], delta, taus, n_tau, diameters[i], out + ((size_t)i * n_modes + m) * n_tau);
+      }
+    }
+    free(se);
+    free(sg);
+    free(de);
+    free(dg);
   }
 }
 

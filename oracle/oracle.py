@@ -64,6 +64,9 @@ def lib():
     L.oracle_bop19_batch.argtypes = [_I64, _i32, _i64, _i64, _d, _i64, _i64, _u32, _i64, _i64,
                                      _d, _d, _d, _i32, _f, _I, _I, _d, _D, _d, _I, _d, _d, _d,
                                      _d]
+    L.oracle_vsd_zbuf_batch.restype = None
+    L.oracle_vsd_zbuf_batch.argtypes = [_I64, _i32, _i64, _i64, _d, _i64, _i64, _u32, _d, _d,
+                                        _i32, _f, _I, _I, _d, _D, _d, _I, _d, _I, _i32, _d]
     _lib = L
   return _lib
 
@@ -204,3 +207,32 @@ def bop19_batch(objects, obj, pose_est, pose_gt, frame_idx, frames, cam, delta, 
                            len(taus), _p(dia, _d), _p(out_vsd, _d), _p(out_mssd, _d),
                            _p(out_mspd, _d))
   return out_vsd, out_mssd, out_mspd
+
+
+def vsd_zbuf_batch(objects, obj, pose_est, pose_gt, frame_idx, frames, cam, delta, taus,
+                   diameters, bits=(0, 32, 24, 16)):
+  """Step-cost VSD (normalised) per tuple under models of vispy's z-buffer
+  (bopx_oracle.c zbuf_depth; renderer_vispy.py:447-456, 526-536): bits 0 = the
+  spec's eye Z, 32 = float32 window depth, 24 / 16 = unorm depth buffers.
+  Returns n x len(bits) x n_tau."""
+  nv = np.array([len(o["pts"]) for o in objects], np.int64)
+  nf = np.array([len(o["faces"]) for o in objects], np.int64)
+  pts_off = np.concatenate([[0], np.cumsum(nv)[:-1]]).astype(np.int64)
+  face_off = np.concatenate([[0], np.cumsum(nf)[:-1]]).astype(np.int64)
+  pts_all = _f64(np.concatenate([o["pts"] for o in objects]))
+  faces_all = np.ascontiguousarray(np.concatenate([o["faces"] for o in objects]), np.uint32)
+  obj = np.ascontiguousarray(obj, np.int32)
+  pe, pg = _f64(pose_est), _f64(pose_gt)
+  fi = np.ascontiguousarray(frame_idx, np.int32)
+  fr = np.ascontiguousarray(frames, np.float32)
+  cam, taus, dia = _f64(cam), _f64(taus), _f64(diameters)
+  bits = np.ascontiguousarray(bits, np.int32)
+  n = len(obj)
+  H, W = fr.shape[1], fr.shape[2]
+  out = np.empty((n, len(bits), len(taus)), np.float64)
+  lib().oracle_vsd_zbuf_batch(n, _p(obj, _i32), _p(pts_off, _i64), _p(nv, _i64), _p(pts_all, _d),
+                              _p(face_off, _i64), _p(nf, _i64), _p(faces_all, _u32), _p(pe, _d),
+                              _p(pg, _d), _p(fi, _i32), _p(fr, _f), W, H, _p(cam, _d),
+                              float(delta), _p(taus, _d), len(taus), _p(dia, _d), len(bits),
+                              _p(bits, _i32), _p(out, _d))
+  return out
