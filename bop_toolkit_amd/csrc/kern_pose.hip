@@ -484,128 +484,6 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
   }
 }
 
-// MFMA variant of the exhaustive MSSD / MSPD sweep (BOPX_SYM_MFMA=1 with
-// BOPX_SYM_PRUNE=0; an experiment): the per-symmetry affine
-// transform [3S x 4] . [4 x V] (north_star's "batched 3xN vertex transform")
-// on v_mfma_f64_16x16x4_f64. One MFMA = 4 symmetries x 16 vertices: A row r
-// holds component r >> 2 (x, y, z; 3 = zero pad) of symmetry r & 3, k = (x, y,
-// z, 1); B column j = vertex j. With the f64 C/D map (col = lane & 15, row =
-// (lane >> 4) + 4 reg) lane l gets the three components of symmetry l >> 4 at
-// vertex l & 15 in its registers 0..2: the squared norm (MSSD) or the
-// projection difference (MSPD) stays in the lane. Tolerance path: the MFMA's internal rounding differs from the
-// VALU fma chain at the ulp level (results within 1e-9 relative of the oracle).
-// Only the unit's ceil(S / 4) symmetry groups are issued (S = 1: one MFMA per
-// 16 vertices, 1 of its 4 symmetry slots used); the waves split the vertices.
-template <int MODE>
-__global__ __launch_bounds__(kPoseThreads) void k_sym_mfma(const ObjDesc* __restrict__ objs,
-                                                           const int32_t* __restrict__ slots,
-                                                           const double* __restrict__ pe,
-                                                           const double* __restrict__ pg,
-                                                           const double* __restrict__ Km,
-                                                           double* __restrict__ out, int nch,
-                                                           const int32_t* __restrict__ order) {
-  typedef double f64x4 __attribute__((ext_vector_type(4)));
-  constexpr int kGroups = kSymChunk / 4;  // symmetry groups of 4 per unit
-  __shared__ double s_v[MODE ? 5 : 3][kSymStage<MODE>];
-  __shared__ double s_red[kPoseThreads / 64][kSymChunk];
-  const int64_t b = order ? (int64_t)order[blockIdx.x / nch] : (int64_t)(blockIdx.x / nch);
-  const int c = blockIdx.x % nch;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const ObjDesc o = objs[slots[b]];
-  const int nv = o.nv, ns = o.ns, s0 = c * kSymChunk;
-  if (s0 >= ns) return;
-  const int sp = min(ns - s0, kSymChunk);
-  const int ng = (sp + 3) >> 2;  // groups in use (wave-uniform): no idle matrix rows beyond
-  double G[12], E[12], K[9], Pe[12];
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    G[i] = pg[12 * b + i];
-    E[i] = pe[12 * b + i];
-  }
-  if constexpr (MODE == 1) {
-#pragma unroll
-    for (int i = 0; i < 9; ++i) K[i] = Km[9 * b + i];
-    proj_mat(K, E, E + 9, Pe);
-  }
-  // A fragments of the unit's symmetry groups (every wave holds all of them;
-  // the waves split the vertices)
-  const int r = lane & 15, kk = lane >> 4, comp = r >> 2;
-  double Af[kGroups];
-#pragma unroll
-  for (int g = 0; g < kGroups; ++g) {
-    Af[g] = 0.0;
-    if (g < ng) {
-      double A[12];
-      sym_matrix<MODE>(E, K, G, o.syms + 12 * (int64_t)(s0 + min(4 * g + (r & 3), sp - 1)), A);
-      Af[g] = comp < 3 ? A[4 * comp + kk] : 0.0;
-    }
-  }
-  const gptr<const double> px = (gptr<const double>)o.pts;
-  const gptr<const double> py = px + nv;
-  const gptr<const double> pz = py + nv;
-  double m[kGroups];
-#pragma unroll
-  for (int g = 0; g < kGroups; ++g) m[g] = -INFINITY;
-  const f64x4 zero = {0.0, 0.0, 0.0, 0.0};
-  for (int v0 = 0; v0 < nv; v0 += kSymStage<MODE>) {
-    const int nb = min(kSymStage<MODE>, nv - v0);
-    __syncthreads();
-    for (int i = tid; i < nb; i += kPoseThreads) {
-      const double x = px[v0 + i], y = py[v0 + i], z = pz[v0 + i];
-      s_v[0][i] = x;
-      s_v[1][i] = y;
-      s_v[2][i] = z;
-      if constexpr (MODE == 1) est_proj(Pe, x, y, z, s_v[3][i], s_v[4][i]);
-    }
-    __syncthreads();
-    for (int j0 = 16 * wave; j0 < nb; j0 += 64) {  // 16-vertex blocks, strided over the waves
-      const int vi = min(j0 + r, nb - 1);  // a repeated vertex cannot change a max
-      const double bv = kk < 3 ? s_v[kk][vi] : 1.0;
-      double ue = 0.0, ve = 0.0;
-      if constexpr (MODE == 1) {
-        ue = s_v[3][vi];
-        ve = s_v[4][vi];
-      }
-#pragma unroll
-      for (int g = 0; g < kGroups; ++g) {
-        if (g < ng) {
-          const f64x4 D = __builtin_amdgcn_mfma_f64_16x16x4f64(Af[g], bv, zero, 0, 0, 0);
-          double d2;
-          if constexpr (MODE == 0) {
-            d2 = fma(D[2], D[2], fma(D[1], D[1], D[0] * D[0]));
-          } else {
-            const double izg = rcp64(D[2]);
-            const double du = fma(-D[0], izg, ue), dv = fma(-D[1], izg, ve);
-            d2 = fma(dv, dv, du * du);
-          }
-          m[g] = fmax(m[g], d2);
-        }
-      }
-    }
-  }
-  // max over the 16 vertex lanes of each symmetry, over the waves, then min
-#pragma unroll
-  for (int g = 0; g < kGroups; ++g) {
-    if (g < ng) {
-      double v = m[g];
-      for (int off = 1; off < 16; off <<= 1) v = fmax(v, __shfl_xor(v, off, 64));
-      if (r == 0) s_red[wave][4 * g + kk] = v;
-    }
-  }
-  __syncthreads();
-  if (tid < 64) {
-    double mn = INFINITY;
-    if (tid < sp) {
-      double mx = s_red[0][tid];
-      for (int w = 1; w < kPoseThreads / 64; ++w) mx = fmax(mx, s_red[w][tid]);
-      mn = mx;
-    }
-    mn = wave_min(mn);
-    if (tid == 0)
-      atomicMin((unsigned long long*)&out[b], (unsigned long long)__double_as_longlong(mn));
-  }
-}
-
 template <int MODE>  // 0 = ADD, 1 = PROJ
 __global__ __launch_bounds__(kPoseThreads) void k_mean_error(const ObjDesc* __restrict__ objs,
                                                              const int32_t* __restrict__ slots,
@@ -843,15 +721,7 @@ hipError_t launch_sym_error(int mode, const ObjDesc* objs, int max_ns, int64_t n
   const char* pe_env = getenv("BOPX_SYM_PRUNE");  // read per call (tests compare both paths)
   const int prune_env = pe_env ? atoi(pe_env) : BOPX_SYM_PRUNE_MIN;
   const int prune_min = prune_env > 0 ? prune_env : 0x7FFFFFFF;
-  // BOPX_SYM_MFMA=1 (with BOPX_SYM_PRUNE=0): the MFMA form of the exhaustive
-  // sweep (k_sym_mfma, an experiment; DESIGN.md §5 has the measurement)
-  const char* mf_env = getenv("BOPX_SYM_MFMA");
-  const bool mfma = mf_env && atoi(mf_env) > 0 && prune_min == 0x7FFFFFFF;
-  if (mfma && mode == 0)
-    hipLaunchKernelGGL(k_sym_mfma<0>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch, order);
-  else if (mfma)
-    hipLaunchKernelGGL(k_sym_mfma<1>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch, order);
-  else if (mode == 0)
+  if (mode == 0)
     hipLaunchKernelGGL(k_sym_error<0>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch,
                        order, prune_min);
   else

@@ -39,13 +39,7 @@
 
 namespace bopx {
 
-#ifndef BOPX_SCAN_DPP
-#define BOPX_SCAN_DPP 1
-#endif
-#ifndef BOPX_VSD_THREADS
-#define BOPX_VSD_THREADS 512
-#endif
-constexpr int kVsdThreads = BOPX_VSD_THREADS;
+constexpr int kVsdThreads = 512;
 
 // Workload counters for the timing diagnostics (BOPX_VSD_ABLATE bit 2). Not
 // part of the C-ABI; read with bopx_debug_vsd_stats.
@@ -312,21 +306,12 @@ __device__ __forceinline__ bool region_covered(const uint32_t* dep, const Region
 // into the rows above. No LDS round trips (the __shfl_up scan is six dependent
 // ds_bpermute + lgkmcnt waits per call).
 __device__ __forceinline__ int wave_incl_scan(int x) {
-#if BOPX_SCAN_DPP
   x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
   x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
   x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
   x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
   x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
   x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-#else
-  const int lane = __lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int v = __shfl_up(x, d, 64);
-    if (lane >= d) x += v;
-  }
-#endif
   return x;
 }
 
@@ -355,69 +340,34 @@ __device__ __forceinline__ T ld_off(gptr<const T> base, uint32_t byte_off) {
 }
 
 constexpr int kVsdWaves = kVsdThreads / 64;
-#ifndef BOPX_VSD_GROUP
-#define BOPX_VSD_GROUP 2
-#endif
-constexpr int kRowWin = 256;  // row items numbered per window (LDS owner map)
+constexpr int kRowWin = 256;  // row items numbered per window (start flags)
 // covered-pixel list of a wave: its rows w, w + kVsdWaves, ... of the tile
 constexpr int kPixPerWave = (kTileH + kVsdWaves - 1) / kVsdWaves * kTileW;
-// Row records of the walk: in LDS (s_rec, 24 KiB per workgroup) or, with
-// BOPX_VSD_REGREC, kept in the set-up lane's registers and fetched by the
-// walking lane with ds_bpermute: the workgroup then fits 3 per CU (LDS <= 54 KiB).
-// Measured (round 2, same box): 1 % slower than LDS records at 2 workgroups
-// per CU; at 3 per CU the 80-VGPR budget spills (+32 %). Off by default.
-// Next pass's record read issued before this pass's walk: +17 % (33 VGPRs
-// spill at 128; round 2), so off.
-// (Static round-robin assignment of entry groups to waves instead of the
-// claim counter: measured +3 %, round 2 — the dynamic queue balances the
-// raster-end barrier.)
-#ifndef BOPX_WALK_PREFETCH
-#define BOPX_WALK_PREFETCH 0
-#endif
-#ifndef BOPX_WORD_PAIR
-#define BOPX_WORD_PAIR 1
-#endif
-// Walk record read as three 16-B LDS reads (ds_read_b128) instead of the
-// compiler's b96 + 3 x read2_b32 split: -2.0 % (same box, 3 reps, round 2).
-#ifndef BOPX_REC128
-#define BOPX_REC128 1
-#endif
-// Record write as three 16-B LDS writes (experiment).
-#ifndef BOPX_REC128W
-#define BOPX_REC128W 0
-#endif
-// Row-item -> record lookup: start flags + ballot/mbcnt (one flag write per
-// record) instead of an owner byte per row item.
-#ifndef BOPX_WALK_FLAGS
-#define BOPX_WALK_FLAGS 1
-#endif
+// Row records of the walk live in LDS (s_rec, 24 KiB per workgroup), written
+// compacted by rank and read as three 16-B LDS reads (ds_read_b128; the
+// compiler's b96 + 3 x read2_b32 split was 2 % slower). Row item -> record
+// lookup: one start flag per record + ballot / mbcnt. Measured and rejected
+// (DESIGN.md §5-6): records kept in registers and fetched with ds_bpermute
+// (1 % slower at 2 workgroups per CU, spills at 3), the next pass's record read
+// ahead of the walk (+17 %), static round-robin entry assignment (+3 %).
 static_assert(kRowWin == 4 * 64, "start flags are cleared one dword per lane");
-#ifndef BOPX_VSD_REGREC
-#define BOPX_VSD_REGREC 0
-#endif
-static_assert(BOPX_VSD_REGREC || sizeof(RRow) * 64 >= 2 * kPixPerWave,
-              "pixel lists overlay the raster records");
+static_assert(sizeof(RRow) * 64 >= 2 * kPixPerWave, "pixel lists overlay the raster records");
 static_assert(kVsdThreads % kTileW == 0, "pixel-pass rows are wave-uniform");
-constexpr int kGroup = BOPX_VSD_GROUP;  // (pose, meshlet) entries staged together per wave step
+// (pose, meshlet) entries staged together per wave step (1: +3 %, 3: LDS over
+// the two-workgroup budget, round 2)
+constexpr int kGroup = 2;
 // worst case (RPT) of meshlet rectangles per thread
 constexpr int kRectsPerThread = (2 * kMaxMeshlets + kVsdThreads - 1) / kVsdThreads;
 // Wave-private scratch: the staged vertex blocks and compacted triangle refs of
-// an entry group during the raster, the tile's float64 column / row
-// coefficients during the pixel pass.
+// an entry group during the raster, the tile's column / row coefficients
+// (float64 and float32) during the pixel pass.
 constexpr int kStageBytes = kGroup * kMeshletVerts * (int)sizeof(RVtx) + kGroup * kMeshletTris * 4;
-// pixel pass: float64 column / row coefficients (+ the covered-pixel list
-// when the records are not in LDS)
-constexpr int kCoefBytes = 8 * (kTileW + kTileH) + (BOPX_VSD_REGREC ? 2 * kPixPerWave : 0);
+constexpr int kCoefBytes = 8 * (kTileW + kTileH) + 4 * (kTileW + kTileH);
 constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
-#ifndef BOPX_VSD_POSE4
-#define BOPX_VSD_POSE4 1
-#endif
-#ifndef BOPX_VSD_TOUCH
-#define BOPX_VSD_TOUCH 1
-#endif
-// Waves that claim the last entry groups of a tile run at raised issue priority
+// Waves that claim the last entry groups of a tile run at issue priority 3
 // until the raster-end barrier (the tile's critical path; the sibling
-// workgroup's waves yield to them).
+// workgroup's waves yield to them): -0.3 % (round 1).
+constexpr int kVsdPrio = 3;
 // Entry queue order and occlusion culling: per pose, the (pose, meshlet) entries
 // whose nearest OBB corner lies in the near half of that pose's depth range are
 // dealt first (front of s_list), the far ones after them (back of s_list,
@@ -427,29 +377,11 @@ constexpr int kWaveScr = kStageBytes > kCoefBytes ? kStageBytes : kCoefBytes;
 // by that (raster.h), and q-buffer values only grow, so a value read while other
 // waves still write is a lower bound of the final one. The result is
 // bit-identical with or without the test (VsdArgs::cull, BOPX_VSD_CULL=0).
-// Back-face occlusion test (VsdArgs::cull == 3, off by default: +3.5 % on the
-// bench workload, round 2). Its claim-loop block stays compiled in either way:
-// the second loop latch (`continue` of a fully occluded group) changes the
-// register allocation of the whole claim loop from 128 VGPRs + 5 spilled to 114
-// without spills, -2.9 % k_vsd time with the test off (same-box A/B, round 2).
-// BOPX_VSD_BACKCULL=0 drops the block (and that allocation).
-#ifndef BOPX_VSD_BACKCULL
-#define BOPX_VSD_BACKCULL 1
-#endif
-#ifndef BOPX_VSD_PRIO
-#define BOPX_VSD_PRIO 3
-#endif
-// Pixel pass without per-pose branches (all three distances on every lane):
-// measured +0.9 % (round 2, same box; waves whose pixels all miss one pose
-// skip that pose's distance), so off.
-#ifndef BOPX_VSD_PIX_BRANCHFREE
-#define BOPX_VSD_PIX_BRANCHFREE 0
-#endif
-// Software-pipelined VSD pixel loop: measured 2 % slower than the plain loop
-// (same-box A/B, round 2), kept as an option.
-#ifndef BOPX_VSD_PIXPIPE
-#define BOPX_VSD_PIXPIPE 0
-#endif
+// Back-face occlusion test (VsdArgs::cull == 3; automatic for objects of many
+// meshlets). Its claim-loop block is compiled in for every instantiation: the
+// second loop latch (`continue` of a fully occluded group) also gives the
+// whole claim loop a better register allocation (114 VGPRs without spills
+// instead of 128 + 5 spilled, -2.9 % with the test off, round 2).
 // Queue order (VsdArgs::qorder, wave-uniform): 0 = near entries first (depth),
 // 1 = entries overlapping the tile by >= a quarter of its area first (longest
 // first for the raster-end barrier: 1,024 px on the 64x64 tile, round-1 LPT
@@ -462,27 +394,9 @@ constexpr int kLptOverlap = kTileW * kTileH / 4;
 constexpr int kCullAutoMeshlets = 256;
 constexpr int kCullAutoDensity = 12;  // ... and at least this many meshlets per ROI tile
 
-// Tile loop barriers and the entry queue. Each wave's first entry group is
-// pre-assigned (no claim round trip for it): -0.9 % (same-box A/B, round 2).
-// BOPX_VSD_EARLY_RESET resets the queue counters behind the raster-end barrier
-// and drops the tile-start barrier: measured +0.5 % against keeping the
-// barrier, so off.
-#ifndef BOPX_VSD_EARLY_RESET
-#define BOPX_VSD_EARLY_RESET 0
-#endif
-#ifndef BOPX_VSD_LIST_AHEAD
-#define BOPX_VSD_LIST_AHEAD 1
-#endif
-#ifndef BOPX_VSD_XLAT
-#define BOPX_VSD_XLAT 0
-#endif
-#ifndef BOPX_VSD_LDSPAD
-#define BOPX_VSD_LDSPAD 0  // experiment: extra LDS bytes per workgroup (occupancy)
-#endif
-#ifndef BOPX_VSD_PRECLAIM
-#define BOPX_VSD_PRECLAIM 1
-#endif
-constexpr int kVsdFirstClaim = BOPX_VSD_PRECLAIM ? kVsdWaves * kGroup : 0;
+// Each wave's first entry group of a tile is pre-assigned (no claim round trip
+// for it): -0.9 % (same-box A/B, round 2); the rest are claimed from s_next.
+constexpr int kVsdFirstClaim = kVsdWaves * kGroup;
 
 // COST: 0 = step, 1 = tlinear, kCostCover = silhouette overlap, kCostGtInfo = GT stats.
 // NT (step cost): thresholds compared per pixel (>= n_tau; 10 for the BOP taus).
@@ -493,38 +407,31 @@ constexpr int kVsdFirstClaim = BOPX_VSD_PRECLAIM ? kVsdWaves * kGroup : 0;
 // rectangles are not kept but recomputed per tile, kListLen entries per round,
 // each round listed and rasterised into the same q tiles before the pixel pass.
 template <int COST, int RPT, int NT>
-// Workgroups per CU: 3 with register records and <= 512 meshlet entries
-// (6 waves per SIMD: VGPRs <= 80), else 2 (4 waves per SIMD: VGPRs <= 128).
-#ifndef BOPX_VSD_WG3
-#define BOPX_VSD_WG3 1
-#endif
-__global__ __launch_bounds__(kVsdThreads,
-                             (BOPX_VSD_REGREC && BOPX_VSD_WG3 && RPT == 1 ? 3 : 2) * kVsdThreads /
-                                 256)
+// two workgroups per CU (4 waves per SIMD: VGPRs <= 128)
+__global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256)
 void k_vsd(VsdArgs a) {
   // q = 1/Z bits, 0 = empty; rows padded by one dword so lanes that walk the
   // same column on consecutive rows (row-split) hit different LDS banks.
   __shared__ uint32_t s_dep[2][kTileStride * kTileH];
   __shared__ __attribute__((aligned(16))) uint8_t s_wscr[kVsdWaves][kWaveScr];
-#if !BOPX_VSD_REGREC
   __shared__ RRow s_rec[kVsdWaves][64];          // set-up triangles of the current chunk
-#endif
-  // row item -> record (lane) of a window, or (BOPX_WALK_FLAGS) record start flags
+  // record start flags of a window of row items
   __shared__ __attribute__((aligned(4))) uint8_t s_own[kVsdWaves][kRowWin];
   // Tile entry queue. RPT <= 2 (objects of <= 512 meshlets): 32-bit words
   // entry | far << 11 | rectangle in the tile at 2-px granularity (x0/2, x1/2,
   // y0/2, y1/2: 5 bits each from bit 12) for the occlusion test; RPT 4: 16-bit
   // entry indices, no occlusion test (the list would not fit the LDS budget).
-  // row-walk atomics (raster.h BOPX_WALK_MASKED): per instantiation by default
-  constexpr int kWalkMasked = BOPX_WALK_MASKED >= 0 ? BOPX_WALK_MASKED : (RPT == 1 ? 0 : 1);
+  // row-walk atomics (raster.h r_walk_row_max): unmasked for the 1-rectangle
+  // objects, masked above (round 2: -0.9 % / -1.2 % on the two classes)
+  constexpr bool kWalkMasked = RPT != 1;
   constexpr bool kStream = RPT == 0;
   constexpr int kR = kStream ? 4 : RPT;  // rectangles per thread and round
   constexpr bool kCull = RPT >= 1 && RPT <= 2;
   constexpr int kListLen = kR * kVsdThreads;  // >= 2 * nm (launch_vsd) unless kStream
   using ListT = typename std::conditional<kCull, uint32_t, uint16_t>::type;
-  // list-ahead (BOPX_VSD_LIST_AHEAD, objects of <= 256 meshlets): two queues,
+  // list-ahead (objects of <= 256 meshlets, round 3: -0.8 %): two queues,
   // the next tile's listed by each wave in the current tile's raster tail
-  constexpr bool kAhead = BOPX_VSD_LIST_AHEAD && !kStream && RPT == 1;
+  constexpr bool kAhead = !kStream && RPT == 1;
   constexpr int kQueues = kAhead ? 2 : 1;
   __shared__ __attribute__((aligned(4))) ListT s_lists[kQueues][kListLen];
   // Back-face occlusion test (cull 3): per entry, its fragment bound qb as an
@@ -533,10 +440,6 @@ void k_vsd(VsdArgs a) {
   __shared__ float s_qhi[2];
   __shared__ float s_zr[2][2];  // per pose: depth range of the meshlet corners (min, max)
   __shared__ int s_nexts[kQueues];
-#if BOPX_VSD_LDSPAD
-  __shared__ uint8_t s_pad[BOPX_VSD_LDSPAD];
-  if (threadIdx.x == 0) asm volatile("" ::"v"(s_pad + blockIdx.x % 7));
-#endif
   __shared__ __attribute__((aligned(16))) float s_pose[2][12];
   __shared__ int s_roi[4];
   __shared__ int s_nlists[kQueues];
@@ -633,7 +536,7 @@ void k_vsd(VsdArgs a) {
   const int ebase = kOnePose ? nm : 0;
 
   // 1. per-pose meshlet rectangles (kept in registers: entry tid + 512 j) + ROI,
-  // and each entry's nearest corner depth (queue order, see BOPX_VSD_PRIO above).
+  // and each entry's nearest corner depth (queue order, see kLptOverlap above).
   short4 rect[kR];
   float zmin[kR];
   float qbv[kR];            // fragment bound per entry (back-face test)
@@ -838,7 +741,7 @@ void k_vsd(VsdArgs a) {
       // kStream: one round per kListLen entries (a single round otherwise)
       for (int e0 = 0; e0 < (kStream ? 2 * nm : 1); e0 += kListLen) {
       if (kStream && e0 > 0) __syncthreads();  // every wave is done with the last round's queue
-      if ((!BOPX_VSD_EARLY_RESET && !kAhead) || kStream) {
+      if (!kAhead || kStream) {
         if (tid == 0) {
           *p_nlist = 0;
           *p_nsmall = 0;
@@ -862,20 +765,19 @@ void k_vsd(VsdArgs a) {
       // each wave's first group is pre-assigned (wave-th group of the queue),
       // the rest are claimed from s_next, which starts past them
       for (int claimed = 0;; claimed = 1) {
-        int base = BOPX_VSD_PRECLAIM ? wave * kGroup : 0;
-        if (!BOPX_VSD_PRECLAIM || claimed) {
+        int base = wave * kGroup;
+        if (claimed) {
           if (lane == 0) base = atomicAdd(p_next, kGroup);
           base = __builtin_amdgcn_readfirstlane(base);
         }
         VSD_STAMP(12);
         if (base >= nl) break;
-        if (BOPX_VSD_PRIO && base + kGroup * kVsdWaves >= nl) __builtin_amdgcn_s_setprio(BOPX_VSD_PRIO);
+        if (base + kGroup * kVsdWaves >= nl) __builtin_amdgcn_s_setprio(kVsdPrio);
         f32x3 v[kGroup];
         uint32_t pk[kGroup];
         int pose[kGroup];
         int ent[kGroup];
         uint32_t word[kGroup];
-#if BOPX_WORD_PAIR
         // both queue words in flight before the first wait (distinct registers)
         uint32_t wv[kGroup];
 #pragma unroll
@@ -885,14 +787,6 @@ void k_vsd(VsdArgs a) {
         }
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) word[g] = __builtin_amdgcn_readfirstlane(wv[g]);
-#else
-#pragma unroll
-        for (int g = 0; g < kGroup; ++g) {
-          const int q = min(base + g, nl - 1);
-          word[g] = __builtin_amdgcn_readfirstlane(
-              (uint32_t)s_list[q < nnear ? q : kListLen - 1 - (q - nnear)]);
-        }
-#endif
         int mlt[kGroup];
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
@@ -906,7 +800,7 @@ void k_vsd(VsdArgs a) {
         // holds q >= its fragment bound. q values only grow, so a value read
         // while other waves still write is a lower bound of the final one.
         uint32_t dead = 0;  // wave-uniform: bit g = entry g skipped
-        if constexpr (kCull && BOPX_VSD_BACKCULL) {
+        if constexpr (kCull) {
           if (cull_back) {
 #pragma unroll
             for (int g = 0; g < kGroup; ++g) {
@@ -951,16 +845,6 @@ void k_vsd(VsdArgs a) {
                                     make_region(word[g], tx1 - tx0 + 1, ty1 - ty0 + 1), 0, lane);
           }
         }
-#if BOPX_VSD_XLAT
-        // experiment: one extra dependent (L1/L2-hit) load per vertex block, to
-        // measure the kernel's sensitivity to the vertex-load latency
-#pragma unroll
-        for (int g = 0; g < kGroup; ++g) {
-          uint32_t z;
-          asm volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"(__float_as_uint(v[g].x)));
-          v[g] = ld_off(g_mvtx3 + mlt[g] * kMeshletVerts, (uint32_t)lane * 16u + z);
-        }
-#endif
         if (VSD_DIAG(8)) {  // diagnostics: time the vertex-block loads alone
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           VSD_STAMP(13);
@@ -968,22 +852,18 @@ void k_vsd(VsdArgs a) {
         float izl[kGroup];  // this lane's vertex 1/Z (0 for an invalid vertex)
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
-#if BOPX_VSD_POSE4
           const float4* P = reinterpret_cast<const float4*>(&s_pose[pose[g]][0]);
           const float4 p0 = P[0], p1 = P[1], p2 = P[2];  // 3 x ds_read_b128
           const float Rf[12] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y,
                                 p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
           const RVtx rv = r_vertex(Rf, c32, v[g].x, v[g].y, v[g].z);
-#else
-          const RVtx rv = r_vertex(s_pose[pose[g]], c32, v[g].x, v[g].y, v[g].z);
-#endif
           w_stage[g * kMeshletVerts + lane] = rv;
           izl[g] = rv.iz;
         }
         wave_lds_sync();
         VSD_STAMP(8);
         if constexpr (kCull) {
-          // occlusion test of the far entries (see BOPX_VSD_PRIO above)
+          // occlusion test of the far entries (see kLptOverlap above)
 #pragma unroll
           for (int g = 0; g < kGroup; ++g) {
             if (test[g]) {
@@ -1072,38 +952,15 @@ void k_vsd(VsdArgs a) {
           const int inc = wave_incl_scan(h);
           const int first = inc - h;
           const int nrow = __builtin_amdgcn_readlane(inc, 63);
-#if BOPX_VSD_REGREC
-          RRow own;  // this lane's record (defined in every lane: fetched with full exec)
-          r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first, own);
-#elif BOPX_WALK_FLAGS
           // records compacted by rank among the row-owning lanes (ascending first)
           const uint64_t rbal = __builtin_amdgcn_ballot_w64(rows);
           if (rows)
-#if BOPX_REC128W
-          {
-            RRow rr;
-            r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first, rr);
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4* src = reinterpret_cast<const u32x4*>(&rr);
-            u32x4* dst = reinterpret_cast<u32x4*>(&s_rec[wave][__builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(rbal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rbal, 0u))]);
-            const u32x4 w0 = src[0], w1 = src[1], w2 = src[2];
-            dst[0] = w0;
-            dst[1] = w1;
-            dst[2] = w2;
-          }
-#else
             r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first,
                        s_rec[wave][__builtin_amdgcn_mbcnt_hi(
                            (uint32_t)(rbal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rbal, 0u))]);
-#endif
-#else
-          if (rows) r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first, s_rec[wave][lane]);
-#endif
-          int rec_base = 0;  // BOPX_WALK_FLAGS: records started before the current pass
+          int rec_base = 0;  // records started before the current pass
           for (int wb = 0; wb < (VSD_DIAG(32) ? 0 : nrow); wb += kRowWin) {
             wave_lds_sync();  // records written / previous window's owners consumed
-#if BOPX_WALK_FLAGS && !BOPX_VSD_REGREC
             // one start flag per record instead of one owner byte per row item
             reinterpret_cast<uint32_t*>(&s_own[wave][0])[lane] = 0u;
             wave_lds_sync();
@@ -1111,69 +968,11 @@ void k_vsd(VsdArgs a) {
             // read per lane holds its flags for the window's four passes
             if (rows && first >= wb && first < wb + kRowWin)
               s_own[wave][(((first - wb) & 63) << 2) | ((first - wb) >> 6)] = 1u;
-#else
-            for (int k = max(first, wb); k < min(first + h, wb + kRowWin); ++k)
-              s_own[wave][k - wb] = (uint8_t)lane;
-#endif
             wave_lds_sync();
             const int wn = min(nrow - wb, kRowWin);
-#if BOPX_VSD_REGREC
-            // uniform loop: every lane takes part in the record fetch (ds_bpermute
-            // reads the owner's register, so owners must be active)
-            for (int p0 = 0; p0 < wn; p0 += 64) {
-              const int p = p0 + lane;
-              const bool valid = p < wn;
-              const RRow rec = r_fetch_row(own, s_own[wave][valid ? p : 0]);
-              if VSD_DIAG(4) {  // passes, sum over passes of the widest row
-                int wmax = valid ? (int)((rec.meta >> 12) & 63u) + 1 : 0;
-                for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, __shfl_xor(wmax, off, 64));
-                if (lane == 0) {
-                  atomicAdd(&g_vsd_stats[7], 1ull);
-                  atomicAdd(&g_vsd_stats[8], (unsigned long long)wmax);
-                }
-              }
-              if (valid) {
-                const int fr =
-                    VSD_DIAG(16) ? r_walk_row_max<true, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
-                                                        s_dep[(rec.meta >> 18) & 1u])
-                                 : r_walk_row_max<false, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
-                                                  s_dep[(rec.meta >> 18) & 1u]);
-                if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
-              }
-            }
-#elif BOPX_WALK_FLAGS
             // item p's record: the last one that starts at or before p, i.e. the
             // start flags up to p (ballot + mbcnt) past those of earlier passes
             const uint32_t fl4 = reinterpret_cast<const uint32_t*>(&s_own[wave][0])[lane];
-#if BOPX_WALK_PREFETCH
-            // the next pass's record read is issued before this pass's walk (owners
-            // are known from the window's flags; always in [0, 63]: loads unmasked)
-            auto owner_of = [&](int p0, int& base) {
-              const uint64_t M = __builtin_amdgcn_ballot_w64(p0 + lane < wn &&
-                                                             ((fl4 >> (p0 >> 3)) & 0xFFu) != 0u);
-              const int o = base - 1 + (int)((M >> lane) & 1u) +
-                            (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
-              base += __popcll(M);
-              return o;
-            };
-            RRow rec = s_rec[wave][owner_of(0, rec_base)];
-            for (int p0 = 0; p0 < wn; p0 += 64) {
-              RRow nxt;
-              if (p0 + 64 < wn) nxt = s_rec[wave][owner_of(p0 + 64, rec_base)];
-              const int p = p0 + lane;
-              if (p < wn) {
-                const int fr =
-                    VSD_DIAG(16) ? r_walk_row_max<true, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
-                                                        s_dep[(rec.meta >> 18) & 1u])
-                                 : r_walk_row_max<false, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
-                                                  s_dep[(rec.meta >> 18) & 1u]);
-                if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
-              }
-              rec = nxt;
-            }
-            if (false)
-#endif
             for (int p0 = 0; p0 < wn; p0 += 64) {
               const int p = p0 + lane;
               const bool valid = p < wn;
@@ -1184,7 +983,6 @@ void k_vsd(VsdArgs a) {
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
               rec_base += __popcll(M);
               if (valid) {
-#if BOPX_REC128
                 // the 48-B record as three 16-B LDS reads
                 RRow rec;
                 {
@@ -1196,9 +994,6 @@ void k_vsd(VsdArgs a) {
                   dst[1] = r1;
                   dst[2] = r2;
                 }
-#else
-                const RRow rec = s_rec[wave][owner];
-#endif
                 const int fr =
                     VSD_DIAG(16) ? r_walk_row_max<true, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
                                                         s_dep[(rec.meta >> 18) & 1u])
@@ -1207,29 +1002,6 @@ void k_vsd(VsdArgs a) {
                 if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
               }
             }
-#else
-            if VSD_DIAG(4) {  // passes, sum over passes of the widest row
-              for (int p0 = 0; p0 < wn; p0 += 64) {
-                int wmax = p0 + lane < wn
-                               ? (int)((s_rec[wave][s_own[wave][p0 + lane]].meta >> 12) & 63u) + 1
-                               : 0;
-                for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, __shfl_xor(wmax, off, 64));
-                if (lane == 0) {
-                  atomicAdd(&g_vsd_stats[7], 1ull);
-                  atomicAdd(&g_vsd_stats[8], (unsigned long long)wmax);
-                }
-              }
-            }
-            for (int p = lane; p < wn; p += 64) {
-              const RRow rec = s_rec[wave][s_own[wave][p]];
-              const int fr =
-                  VSD_DIAG(16) ? r_walk_row_max<true, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
-                                                      s_dep[(rec.meta >> 18) & 1u])
-                               : r_walk_row_max<false, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
-                                                s_dep[(rec.meta >> 18) & 1u]);
-              if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
-            }
-#endif
           }
           VSD_STAMP(11);
           wave_lds_sync();  // records are rewritten by the next chunk
@@ -1249,7 +1021,6 @@ void k_vsd(VsdArgs a) {
       // test depth of this tile: wave-uniform base, offsets < 64 rows x IW x 4 B
       const gptr<const float> tframe = frame + ((int64_t)ty0 * IW + tx0);
       float touch = 0.0f;
-#if BOPX_VSD_TOUCH
       if constexpr (COST == 0 || COST == 1) {
         if (lane < 3 * (kTileH / kVsdWaves)) {
           const int row = ty0 + wave + kVsdWaves * (lane / 3), k = lane % 3;
@@ -1258,7 +1029,6 @@ void k_vsd(VsdArgs a) {
             touch = ld_off(tframe, (uint32_t)(__mul24(row - ty0, IW) + (col - tx0)) * 4u);
         }
       }
-#endif
       // float64 distance coefficients of the tile's columns / rows (misc.py:137-138),
       // per wave into its scratch (its staging area is dead until the next
       // tile), computed before the raster-end barrier while other waves finish
@@ -1266,11 +1036,11 @@ void k_vsd(VsdArgs a) {
       for (int i = lane; i < kTileH; i += 64) w_pY[i] = ((double)(ty0 + i - oy) - cy) / fy;
       VSD_STAMP(2);
       __syncthreads();
-      if (BOPX_VSD_PRIO) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
       // every wave has read the queue counters (after the list barrier) and is
       // done with s_next: reset them for the next tile (ordered by the
       // pixel-end barrier)
-      if ((BOPX_VSD_EARLY_RESET || kAhead) && tid == 0) {
+      if (kAhead && tid == 0) {
         *p_nlist = 0;
         *p_nsmall = 0;
         *p_next = kVsdFirstClaim;
@@ -1282,11 +1052,7 @@ void k_vsd(VsdArgs a) {
       // list (ballot rank; the raster records are dead here), then evaluates
       // the list with full lanes. Wave-private: no block barrier, and the
       // pixel -> lane assignment is fixed (deterministic float64 sums).
-#if BOPX_VSD_REGREC
-      uint16_t* pix = reinterpret_cast<uint16_t*>(&s_wscr[wave][8 * (kTileW + kTileH)]);
-#else
       uint16_t* pix = reinterpret_cast<uint16_t*>(&s_rec[0][0]) + wave * kPixPerWave;
-#endif
       int npix = 0;
       {
         // lane = column, one wave-uniform tile row per step (rows w, w + 8, ...)
@@ -1315,23 +1081,10 @@ void k_vsd(VsdArgs a) {
         }
       }
       wave_lds_sync();
-      auto ps_of = [](int p) { return (p >> 6) * kTileStride + (p & 63); };
       auto dt_of = [&](int p) {
         return ld_off(tframe, (uint32_t)(__mul24(p >> 6, IW) + (p & 63)) * 4u);
       };
       auto vsd_px = [&](int p, uint32_t qe, uint32_t qg, float dtest) {
-#if BOPX_VSD_PIX_BRANCHFREE
-        // branch-free: a background pose (q = 0) takes 1/1 (no IEEE fallback
-        // in rcp_rn) and depth 0, whose distance is exactly +0 (sqrt_depth(0))
-        const float re = rcp_rn(__uint_as_float(qe ? qe : 0x3F800000u));
-        const float rg = rcp_rn(__uint_as_float(qg ? qg : 0x3F800000u));
-        const float de = qe ? re : 0.0f, dg = qg ? rg : 0.0f;
-        const double pX = w_pX[p % kTileW];
-        const double pY = w_pY[p / kTileW];
-        const double dist_t = dist_of(pX, pY, dtest);
-        const double dist_g = dist_of(pX, pY, dg);
-        const double dist_e = dist_of(pX, pY, de);
-#else
         const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
         const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
         const double pX = w_pX[p % kTileW];
@@ -1339,7 +1092,6 @@ void k_vsd(VsdArgs a) {
         const double dist_t = dist_of(pX, pY, dtest);
         const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
         const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
-#endif
         const bool vg = visib19t(dist_t, dist_g, a.dthr);
         bool ve = visib19t(dist_t, dist_e, a.dthr);
         ve = ve || (vg && dist_e > 0.0);  // visibility.py:74
@@ -1367,8 +1119,6 @@ void k_vsd(VsdArgs a) {
           }
         }
       };
-      if constexpr (COST == kCostCover || COST == kCostGtInfo || COST == kCostRender ||
-                    !BOPX_VSD_PIXPIPE) {
       for (int i = lane; i < npix; i += 64) {
         const int p = pix[i];
         const int row = ty0 + p / kTileW, col = tx0 + p % kTileW;
@@ -1425,37 +1175,6 @@ void k_vsd(VsdArgs a) {
           continue;
         }
         if constexpr (COST == 0 || COST == 1) vsd_px(p, qe, qg, dt_of(p));
-      }
-      } else {
-        // VSD: software-pipelined over the wave's pixel list. Pixel i + 64's q
-        // pair and test depth are in flight (and pixel i + 128's index) while
-        // pixel i is evaluated: the chain index -> (q, depth) -> float64 math
-        // would otherwise pay an LDS and a global round trip per 64 pixels.
-        // Lane -> pixel assignment unchanged (i = lane + 64 k: deterministic sums).
-        if (npix > 0) {
-          const int last = npix - 1;
-          int p0 = pix[min(lane, last)];
-          int p1 = pix[min(lane + 64, last)];
-          uint32_t qe0 = s_dep[0][ps_of(p0)], qg0 = s_dep[1][ps_of(p0)];
-          float dt0 = dt_of(p0);
-          for (int i = lane; i - lane < npix; i += 64) {
-            // next pixel's loads (clamped indices: unpredicated, no serialising waits)
-            const uint32_t qe1 = s_dep[0][ps_of(p1)], qg1 = s_dep[1][ps_of(p1)];
-            const float dt1 = dt_of(p1);
-            const int p2 = pix[min(i + 128, last)];
-            if (i < npix) {
-              s_dep[0][ps_of(p0)] = 0u;  // clean for the next tile (rows are wave-private)
-              s_dep[1][ps_of(p0)] = 0u;
-              if VSD_DIAG(4) atomicAdd(&g_vsd_stats[6], 1ull);
-              vsd_px(p0, qe0, qg0, dt0);
-            }
-            p0 = p1;
-            qe0 = qe1;
-            qg0 = qg1;
-            dt0 = dt1;
-            p1 = p2;
-          }
-        }
       }
       VSD_STAMP(4);
       __syncthreads();
@@ -1818,10 +1537,9 @@ hipError_t launch_pose_roi(const ObjDesc* objs, int64_t n, const int32_t* slots,
 constexpr int kPairThreads = 256;
 constexpr int kPairWaves = kPairThreads / 64;
 constexpr int kPairCols = 2048;  // column coefficients staged in LDS per block of columns
-#ifndef BOPX_PAIR_U
-#define BOPX_PAIR_U 2
-#endif
-constexpr int kPairU = BOPX_PAIR_U;  // pixels per lane and step (loads in flight together)
+// pixels per lane and step, their loads in flight together (round 3, same box:
+// 1 / 2 / 4 / 8 -> 4.3 / 3.85 / 4.03 / 4.4 ms on the multi-instance workload)
+constexpr int kPairU = 2;
 
 template <int COST, int NT>
 __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {

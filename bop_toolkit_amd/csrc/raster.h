@@ -29,19 +29,6 @@
 
 namespace bopx {
 
-// Row-walk atomics (r_walk_row_max's MASKED): 0 = every column issues its
-// atomicMax (0, a no-op on the non-negative q bits, where the centre is
-// outside), 1 = only covered centres (exec-masked), 2 = skipped per column
-// when no lane covers it. -1 (default): k_vsd picks per instantiation. Round 2,
-// same box, 3 reps each: with 1-rect-per-thread objects (the bench shard) 0 is
-// 0.9 % faster than 1 (no exec-mask save/restore around each atomic); with the
-// 2-rect instantiation (T-LESS-like config) 1 is 1.2 % faster; 2 is 1.9 % slower.
-#ifndef BOPX_WALK_MASKED
-#define BOPX_WALK_MASKED -1
-#endif
-#ifndef BOPX_RCP_BALLOT
-#define BOPX_RCP_BALLOT 1
-#endif
 
 // Correctly rounded 1/x, bit-identical to the IEEE 1.0f / x the spec names:
 // hardware reciprocal plus one fused Newton step. Checked against
@@ -54,13 +41,8 @@ __device__ __forceinline__ float rcp_rn(float x) {
   const float r0 = __builtin_amdgcn_rcpf(x);
   const float r = __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
   const bool ok = (__float_as_uint(x) & 0x7FFFFFFFu) - 0x00800000u < 0x7E000000u;
-#if BOPX_RCP_BALLOT
   if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) != 0, 0)) return ok ? r : 1.0f / x;
   return r;
-#else
-  if (__builtin_expect(!ok, 0)) return 1.0f / x;
-  return r;
-#endif
 }
 
 struct Cam32 {
@@ -358,26 +340,6 @@ __device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int 
            ((uint32_t)pose << 18) | ((uint32_t)first << 19);
 }
 
-// The record of lane `owner` of this wave, read from its registers
-// (ds_bpermute; every lane of the wave must be active).
-__device__ __forceinline__ RRow r_fetch_row(const RRow& own, int owner) {
-  const int addr = owner << 2;
-  auto f = [addr](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v); };
-  RRow r;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    r.er[k] = f(own.er[k]);
-    r.duv[k] = f(own.duv[k]);
-  }
-  r.px0u = (int32_t)f((uint32_t)own.px0u);
-  r.py0v = (int32_t)f((uint32_t)own.py0v);
-  r.iz0 = __uint_as_float(f(__float_as_uint(own.iz0)));
-  r.ga = __uint_as_float(f(__float_as_uint(own.ga)));
-  r.gb = __uint_as_float(f(__float_as_uint(own.gb)));
-  r.meta = f(own.meta);
-  return r;
-}
-
 // Walk row j of a record into the LDS z-buffer, branch-free: every column issues one
 // signed atomicMax, with 0 (a no-op on the 0-initialised buffer) where the pixel
 // centre is outside the triangle. Records are regular small triangles only, so q
@@ -386,7 +348,12 @@ __device__ __forceinline__ RRow r_fetch_row(const RRow& own, int owner) {
 // q <= 0 are dropped" without a compare. No exec-mask branches in the loop body.
 // dep: the pose's q tile (row pitch kTileStride). Returns the fragment count
 // (diagnostics).
-template <bool kNoAtomics = false, int MASKED = 1>  // kNoAtomics: timing ablation (diag builds)
+// MASKED: only covered centres issue their atomicMax (exec-masked; fewer bank
+// conflicts on scattered rows) instead of every column (0 where the centre is
+// outside: no exec-mask save / restore). Round 2, same box: unmasked 0.9 %
+// faster for 1-rectangle objects, masked 1.2 % faster for the 2-rectangle
+// class; skipping a column no lane covers (ballot) was 1.9 % slower.
+template <bool kNoAtomics = false, bool MASKED = true>  // kNoAtomics: timing ablation (diag builds)
 __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* dep) {
   // j < 64 and the tile row tr < 64 always; the masks (no-ops) tell the
   // compiler so, which keeps every multiply below on the full-rate 24-bit path.
@@ -424,16 +391,9 @@ __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* de
     frags += (m0 > 0) + ((i + 1 < w) & (m1 > 0));  // diagnostics (dead in the product build)
     if constexpr (kNoAtomics) {
       asm volatile("" ::"v"(m0 > 0 ? q0 : 0.0f), "v"(m1 > 0 ? q1 : 0.0f), "v"(d + i));
-    } else if constexpr (MASKED == 1) {
-      // only covered centres touch LDS (fewer bank conflicts on the scattered rows)
+    } else if constexpr (MASKED) {
       if (m0 > 0) atomicMax(d + i, __float_as_int(q0));
       if (m1 > 0) atomicMax(d + i + 1, __float_as_int(q1));
-    } else if constexpr (MASKED == 2) {
-      // wave-uniform skip of a column with no covered centre, unmasked otherwise
-      if (__builtin_amdgcn_ballot_w64(m0 > 0) != 0)
-        atomicMax(d + i, m0 > 0 ? __float_as_int(q0) : 0);
-      if (__builtin_amdgcn_ballot_w64(m1 > 0) != 0)
-        atomicMax(d + i + 1, m1 > 0 ? __float_as_int(q1) : 0);
     } else {
       atomicMax(d + i, m0 > 0 ? __float_as_int(q0) : 0);
       atomicMax(d + i + 1, m1 > 0 ? __float_as_int(q1) : 0);

@@ -902,40 +902,3 @@ def test_drop_in_vsd_return_types(oracle_mod, monkeypatch):
   with pytest.raises(NotImplementedError):
     create_renderer(640, 480, "vispy", mode="depth")
 
-
-def test_sym_mfma_variant_matches_oracle(ctx, oracle_mod, monkeypatch):
-  """The MFMA form of the exhaustive MSSD / MSPD sweep (k_sym_mfma,
-  v_mfma_f64_16x16x4_f64; BOPX_SYM_MFMA=1 with BOPX_SYM_PRUNE=0) against the
-  oracle: within 1e-9 relative (its internal rounding differs from the VALU
-  fma chain), over 1, 3, 8, 64, 65 (two chunks) and 314 symmetries and a
-  vertex count that is not a multiple of 16."""
-  from bop_toolkit_amd import misc, synth
-  rng = np.random.default_rng(79)
-  objs = []
-  for o, (nd, cont) in enumerate([(1, False), (3, False), (8, False), (64, False), (65, False),
-                                  (1, True)]):
-    pts, faces = synth.superellipsoid(13 + o, 23, (30.0 + 4 * o, 45.0, 55.0 - 3 * o), 0.6)
-    info = synth.models_info_entry(pts, nd, cont)
-    syms = misc.symmetries_to_array(misc.get_symmetry_transformations(info, 0.01))
-    ctx.add_object(800 + o, pts, faces)
-    ctx.set_symmetries(800 + o, syms)
-    objs.append({"pts": pts, "syms": syms})
-  n = 60
-  obj = (np.arange(n) % len(objs)).astype(np.int32)
-  Rg, tg = synth.gt_poses(rng, n)
-  Re, te_ = synth.perturb(rng, Rg, tg, outlier_frac=0.3)
-  pe = np.concatenate([Re.reshape(n, 9), te_], 1)
-  pg = np.concatenate([Rg.reshape(n, 9), tg], 1)
-  K = np.tile(synth.LMO_K.reshape(9), (n, 1))
-  monkeypatch.setenv("BOPX_SYM_PRUNE", "0")
-  monkeypatch.setenv("BOPX_SYM_MFMA", "1")
-  mssd = _batch(ctx, "bopx_mssd_batch", obj + 800, pe, pg)
-  mspd = _batch(ctx, "bopx_mspd_batch", obj + 800, pe, pg, K)
-  for i in range(n):
-    o = objs[obj[i]]
-    want = oracle_mod.mssd(o["pts"], o["syms"], pe[i], pg[i])
-    assert abs(mssd[i] - want) <= 1e-9 * max(1.0, abs(want)), (i, mssd[i], want)
-    want = oracle_mod.mspd(o["pts"], o["syms"], pe[i], pg[i], K[i])
-    assert abs(mspd[i] - want) <= 1e-9 * max(1.0, abs(want)), (i, mspd[i], want)
-  for o in range(len(objs)):
-    ctx.remove_object(800 + o)

@@ -6,7 +6,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
 for env in "BOPX_VSD_CULL=0" "BOPX_VSD_CULL=3" "BOPX_VSD_CULL=1" "BOPX_VSD_QORDER=0" \
            "BOPX_LAUNCH_ORDER=0" "BOPX_VSD_SPLIT=4" "BOPX_VSD_TAIL=300" "BOPX_SYM_PRUNE=0" \
-           "BOPX_ADI_SPLIT=1" "BOPX_SHARED_RENDER_RATIO=0"; do
+           "BOPX_ADI_SPLIT=1" "BOPX_ADI_QSPLIT=1" "BOPX_SHARED_RENDER_RATIO=0" \
+           "BOPX_MESHLET_CURVE=morton"; do
   env $env timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shared.py \
       tests/test_gpu_configs.py -q -x --timeout 240 --timeout-method thread \
       -k "fused or raster or shared or sym or adi or config or cover" > gpurun_out/sw.log 2>&1 \
