@@ -173,6 +173,13 @@ __device__ __forceinline__ void est_proj(const double* Pe, double x, double y, d
 #define BOPX_SYM_SEEDS 128  // seed vertices used of the object's kSymSeeds
 #endif
 constexpr int kPruneSpan = 320;  // symmetry sets up to this size are pruned by one unit
+// vertices per thread and step of the whole-workgroup sweep (step 2; 8 measured
+// slower than 4, profiles/r04/ab_sym.txt)
+#ifndef BOPX_SYM_SWEEP_U
+#define BOPX_SYM_SWEEP_U 4
+#endif
+constexpr int kSweepU = BOPX_SYM_SWEEP_U;
+static_assert(kSweepU % 2 == 0, "pairs of maxima");
 
 // Make LDS written by other lanes of this wave visible (LDS is in order per wave).
 __device__ __forceinline__ void wave_lds_sync_pose() {
@@ -213,7 +220,11 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
   // 0; the tuple's other chunks exit), larger sets chunk by chunk.
   const bool whole = ns <= kPruneSpan;
   const int span = whole ? ns : sp;
-  if (span >= prune_min) {
+  // A single symmetry needs no bounds: the unit is the full sweep of step (2)
+  // alone (round 4; no LDS staging rounds and barriers: the same d2 per vertex
+  // and an exact max, so the same double as the exhaustive path).
+  const bool single = ns == 1;
+  if (span >= prune_min || single) {
     if (whole && c != 0) return;
     static_assert(kSymSeeds <= kPoseThreads && kSymSeeds <= kSymStage<MODE>, "seed staging");
     __shared__ double s_L[kPruneSpan];    // per-symmetry lower bound (max over the seeds)
@@ -253,7 +264,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
     // (1) bounds over the seed vertices, 64 symmetries at a time, lane (k, g) =
     // (symmetry, seed group)
     const int np = min(o.nseed, BOPX_SYM_SEEDS);
-    if (tid < np) {
+    if (!single && tid < np) {
       const gptr<const double> sd = (gptr<const double>)o.seed;
       const int ns_all = o.nseed;  // SoA stride
       const double x = sd[tid], y = sd[ns_all + tid], z = sd[2 * ns_all + tid];
@@ -270,7 +281,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
       s_ncand = 0;
     }
     __syncthreads();
-    for (int kb = 0; kb < span; kb += 64) {
+    for (int kb = 0; kb < (single ? 0 : span); kb += 64) {
       const int bp = min(span - kb, 64), bng = kPoseThreads / bp;
       const int bk = tid % bp, bg = tid / bp;
       double m = -INFINITY;
@@ -291,7 +302,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
       __syncthreads();
     }
     // argmin of (bound, index): per thread, then per wave, then over the waves
-    {
+    if (!single) {
       double L = INFINITY;
       int kk = 0x7FFFFFFF;
       for (int i = tid; i < span; i += kPoseThreads)
@@ -324,23 +335,26 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
       }
       __syncthreads();
     }
-    const int k0 = s_k0;
-    if (!(s_L[k0] <= best_now())) return;  // no symmetry of the unit can win
+    const int k0 = single ? 0 : s_k0;
+    if (!single && !(s_L[k0] <= best_now())) return;  // no symmetry of the unit can win
     // (2) the lowest bound, swept by the whole workgroup
     {
       double A[12];
       sym_matrix<MODE>(E, K, G, syms + 12 * (int64_t)k0, A);
       double m = -INFINITY;
-      for (int v0 = 0; v0 < nv; v0 += 4 * kPoseThreads) {
-        double d[4];
+      // kSweepU vertices per thread and step, all their loads in flight
+      for (int v0 = 0; v0 < nv; v0 += kSweepU * kPoseThreads) {
+        double d[kSweepU];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) d[u] = d2v(A, min(v0 + u * kPoseThreads + tid, nv - 1));
-        m = fmax(m, fmax(fmax(d[0], d[1]), fmax(d[2], d[3])));
+        for (int u = 0; u < kSweepU; ++u) d[u] = d2v(A, min(v0 + u * kPoseThreads + tid, nv - 1));
+#pragma unroll
+        for (int u = 0; u < kSweepU; u += 2) m = fmax(m, fmax(d[u], d[u + 1]));
       }
       m = wave_max(m);
       if (lane == 0) s_red[wave] = m;
       __syncthreads();
       if (tid == 0) publish(fmax(fmax(s_red[0], s_red[1]), fmax(s_red[2], s_red[3])));
+      if (single) return;
       __syncthreads();
     }
     // candidates: the other symmetries whose bound does not exceed the best max
@@ -710,17 +724,22 @@ hipError_t launch_sym_error(int mode, const ObjDesc* objs, int max_ns, int64_t n
                             const double* K, double* out, const int32_t* order,
                             hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  const int nch = (max(max_ns, 1) + kSymChunk - 1) / kSymChunk;
-  if ((int64_t)nch * n > 0x7FFFFFFF) return hipErrorInvalidValue;
-  const dim3 gfix((unsigned)((n + 255) / 256)), bfix(256);
-  hipLaunchKernelGGL(k_sym_init, gfix, bfix, 0, s, out, n);
-  dim3 grid((unsigned)(n * nch)), block(kPoseThreads);
   // BOPX_SYM_PRUNE: units with at least this many symmetries take the pruned
   // path (<= 0: never, every set sweeps exhaustively chunk by chunk, including
   // the whole-set units of up to kPruneSpan; identical results either way)
   const char* pe_env = getenv("BOPX_SYM_PRUNE");  // read per call (tests compare both paths)
   const int prune_env = pe_env ? atoi(pe_env) : BOPX_SYM_PRUNE_MIN;
   const int prune_min = prune_env > 0 ? prune_env : 0x7FFFFFFF;
+  // chunks per tuple: sets of up to kPruneSpan symmetries that are pruned run
+  // as one unit, so only the exhaustive sets (< prune_min) and the larger ones
+  // need more (round 4: the S = 314 object had made every tuple launch 5
+  // blocks, 4 of which exited at once)
+  const int need = max_ns <= kPruneSpan ? min(max_ns, prune_min - 1) : max_ns;
+  const int nch = (max(need, 1) + kSymChunk - 1) / kSymChunk;
+  if ((int64_t)nch * n > 0x7FFFFFFF) return hipErrorInvalidValue;
+  const dim3 gfix((unsigned)((n + 255) / 256)), bfix(256);
+  hipLaunchKernelGGL(k_sym_init, gfix, bfix, 0, s, out, n);
+  dim3 grid((unsigned)(n * nch)), block(kPoseThreads);
   if (mode == 0)
     hipLaunchKernelGGL(k_sym_error<0>, grid, block, 0, s, objs, slots, pe, pg, K, out, nch,
                        order, prune_min);

@@ -105,6 +105,90 @@ __device__ __forceinline__ bool visib19t(double dt, double dm, float dthr) {
   return ((diff <= dthr) || dt == 0.0) && dm > 0.0;
 }
 
+// ---------------------------------------------------------------------------
+// Certified float32 filter of the per-pixel VSD decisions (round 4).
+//
+// The reference decides, per pixel, two visibility tests (visibility.py:35-37:
+// float32 difference of float64 distances vs delta) and, for intersection
+// pixels, n_tau step thresholds (pose_error.py:80-81: float64 |dist_g - dist_e|
+// vs tau, here dd >= T_k). The float64 distances (misc.py:158-161) cost three
+// IEEE sqrt sequences per pixel; yet the decisions are almost never close to
+// their thresholds. The filter evaluates them in float32 from
+//   s = sqrt(1 + pX^2 + pY^2)  (hardware sqrt of A[col] + B[row], float32),
+//   g = rcp(q_g) s, e = rcp(q_e) s, t = |d_test| s  (hardware reciprocal),
+// each within 12u of the float32 rounding of the reference's float64 distance
+// (u = 2^-24; s within 6.5u, the reciprocal within 3u of rcp_rn; DESIGN.md §5
+// derives the bounds), so the visibility difference is within 14u (g + t) of
+// the reference's and the step distance |g - e| within 12u (g + e) of the
+// reference's float64 one.
+// Every decision is taken from float32 only when it is outside a margin of
+// 64u x the distances involved (+ 2^-100 for the subnormal range): visibility
+// when |(g - t) - delta| > E, a threshold when lo = dd - E_d and hi = dd + E_d
+// fall on the same side of it. Otherwise (and for any non-finite or > 2^100
+// value) the lane redoes the pixel with the exact float64 sequence. The
+// counters are integers, so the results are bit-identical to the exact path
+// (tests/test_gpu_parity.py, the fuzz tests; the diag build counts the pixels
+// that take the exact path).
+constexpr float kFilterRel = 0x1p-18f;   // 64u
+constexpr float kFilterAbs = 0x1p-100f;  // subnormal-range absolute errors
+constexpr float kFilterMax = 0x1p100f;   // larger values: exact path
+
+// float32 coefficients of one column / row: A = pX^2, B = 1 + pY^2 (pX, pY the
+// float64 misc.py:137-138 values, rounded to float32)
+__device__ __forceinline__ float filt_a(double pX) {
+  const float x = (float)pX;
+  return x * x;
+}
+__device__ __forceinline__ float filt_b(double pY) {
+  const float y = (float)pY;
+  return 1.0f + y * y;
+}
+
+// Exact per-pixel VSD step decisions (the float64 reference sequence):
+// visibility of gt / est and the step distance (only meaningful when both are
+// visible). pX, pY: float64 coefficients; qe / qg: q bits (0 = no fragment).
+__device__ __forceinline__ void vsd_exact_px(double pX, double pY, uint32_t qe, uint32_t qg,
+                                             float dtest, float dthr, bool& vg, bool& ve,
+                                             double& dd) {
+  const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
+  const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
+  const double dist_t = dist_of(pX, pY, dtest);
+  const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
+  const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
+  vg = visib19t(dist_t, dist_g, dthr);
+  ve = visib19t(dist_t, dist_e, dthr) || (vg && dist_e > 0.0);  // visibility.py:74
+  dd = fabs(dist_g - dist_e);
+}
+
+// Float32 pass of the filter. s2 = A[col] + B[row]. Returns vg / ve, the step
+// distance bracket [lo, hi] of |dist_g - dist_e| and whether the visibility
+// decisions (or the magnitudes) need the exact path.
+__device__ __forceinline__ bool vsd_filter_px(float s2, uint32_t qe, uint32_t qg, float dtest,
+                                              float dthr, bool& vg, bool& ve, float& lo,
+                                              float& hi) {
+  const float s = __builtin_amdgcn_sqrtf(s2);
+  const float g = qg ? __builtin_amdgcn_rcpf(__uint_as_float(qg)) * s : 0.0f;
+  const float e = qe ? __builtin_amdgcn_rcpf(__uint_as_float(qe)) * s : 0.0f;
+  const float t = fabsf(dtest) * s;
+  const bool dtz = dtest == 0.0f;  // dist_t == 0
+  const float gt = g + t, et = e + t, ge = g + e;
+  const float xg = (g - t) - dthr, xe = (e - t) - dthr;
+  const bool cg = fabsf(xg) > __builtin_fmaf(gt, kFilterRel, kFilterAbs);
+  const bool ce = fabsf(xe) > __builtin_fmaf(et, kFilterRel, kFilterAbs);
+  // bitwise forms: no short-circuit branches in the pixel loop
+  const bool hg = qg != 0u, he = qe != 0u;
+  vg = hg & (dtz | (xg < 0.0f));
+  ve = he & (dtz | (xe < 0.0f) | vg);
+  const float dd = fabsf(g - e), ed = __builtin_fmaf(ge, kFilterRel, kFilterAbs);
+  lo = dd - ed;
+  hi = dd + ed;
+  return !(gt + e < kFilterMax) | (hg & !dtz & !cg) | (he & !dtz & !vg & !ce);
+}
+
+// float32 form of a step threshold T for the filter: T <= 0 passes every
+// distance (-inf), otherwise RN(T) (NaN and +inf stay).
+__device__ __forceinline__ float filt_thr(double T) { return T <= 0.0 ? -INFINITY : (float)T; }
+
 // Step cost of normalised distances (pose_error.py:66-68,80-81):
 // RN(dd / diameter) >= tau is monotone in dd >= 0 for a finite diameter > 0,
 // so it is dd >= T for the least double T that passes it. T is found once per
@@ -465,6 +549,8 @@ void k_vsd(VsdArgs a) {
       reinterpret_cast<uint32_t*>(&s_wscr[wave][kGroup * kMeshletVerts * sizeof(RVtx)]);
   double* const w_pX = reinterpret_cast<double*>(&s_wscr[wave][0]);
   double* const w_pY = w_pX + kTileW;
+  float* const w_fA = reinterpret_cast<float*>(w_pY + kTileH);  // filter: pX^2, 1 + pY^2
+  float* const w_fB = w_fA + kTileW;
   unsigned long long ph[16] = {}, t_prev = 0;
   if (VSD_DIAG(8)) t_prev = __builtin_amdgcn_s_memtime();
   const ObjDesc o = a.objs[a.slots[b]];
@@ -657,13 +743,14 @@ void k_vsd(VsdArgs a) {
       }
     }
   }
-  double thr[NT];  // wave-uniform (SGPRs)
+  // float32 step thresholds of the filter (wave-uniform, SGPRs); the exact
+  // path reads the float64 ones from s_thr
+  float thr32[NT];
 #pragma unroll
-  for (int k = 0; k < NT; ++k) {
-    const double v = COST == 0 ? s_thr[k] : 0.0;
-    thr[k] = __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
-                              __builtin_amdgcn_readfirstlane(__double2loint(v)));
-  }
+  for (int k = 0; k < NT; ++k)
+    thr32[k] = __int_as_float(
+        __builtin_amdgcn_readfirstlane(__float_as_int(COST == 0 ? filt_thr(s_thr[k]) : 0.0f)));
+  const bool filter = COST == 0 && !divide;
 
   uint32_t c_union = 0, c_inter = 0, c_valid = 0;
   // cover mode: est / gt silhouette bboxes (x0, y0, x1, y1), empty = (INT_MAX, INT_MAX, -1, -1)
@@ -1032,8 +1119,16 @@ void k_vsd(VsdArgs a) {
       // float64 distance coefficients of the tile's columns / rows (misc.py:137-138),
       // per wave into its scratch (its staging area is dead until the next
       // tile), computed before the raster-end barrier while other waves finish
-      for (int i = lane; i < kTileW; i += 64) w_pX[i] = ((double)(tx0 + i - ox) - cx) / fx;
-      for (int i = lane; i < kTileH; i += 64) w_pY[i] = ((double)(ty0 + i - oy) - cy) / fy;
+      for (int i = lane; i < kTileW; i += 64) {
+        const double pX = ((double)(tx0 + i - ox) - cx) / fx;
+        w_pX[i] = pX;
+        if constexpr (COST == 0) w_fA[i] = filt_a(pX);
+      }
+      for (int i = lane; i < kTileH; i += 64) {
+        const double pY = ((double)(ty0 + i - oy) - cy) / fy;
+        w_pY[i] = pY;
+        if constexpr (COST == 0) w_fB[i] = filt_b(pY);
+      }
       VSD_STAMP(2);
       __syncthreads();
       __builtin_amdgcn_s_setprio(0);
@@ -1081,33 +1176,73 @@ void k_vsd(VsdArgs a) {
         }
       }
       wave_lds_sync();
+      // step cost: the certified float32 filter, the exact float64 sequence for
+      // the pixels it cannot decide (and for every pixel of a tuple with a
+      // pathological diameter / tau, `divide`)
       auto dt_of = [&](int p) {
         return ld_off(tframe, (uint32_t)(__mul24(p >> 6, IW) + (p & 63)) * 4u);
       };
-      auto vsd_px = [&](int p, uint32_t qe, uint32_t qg, float dtest) {
-        const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
-        const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
-        const double pX = w_pX[p % kTileW];
-        const double pY = w_pY[p / kTileW];
-        const double dist_t = dist_of(pX, pY, dtest);
-        const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
-        const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
-        const bool vg = visib19t(dist_t, dist_g, a.dthr);
-        bool ve = visib19t(dist_t, dist_e, a.dthr);
-        ve = ve || (vg && dist_e > 0.0);  // visibility.py:74
+      auto step_exact = [&](int p, uint32_t qe, uint32_t qg, float dtest) {
+        bool vg, ve;
+        double dd;
+        vsd_exact_px(w_pX[p % kTileW], w_pY[p / kTileW], qe, qg, dtest, a.dthr, vg, ve, dd);
         c_union += (vg || ve);
         if (vg && ve) {
           ++c_inter;
-          double dd = fabs(dist_g - dist_e);
-          if constexpr (COST == 0) {
-            if (divide) {  // rare: a real branch, not a speculated division
-              dd /= diam;
-              asm volatile("" : "+v"(dd));
-            }
+          if (divide) {  // rare: a real branch, not a speculated division
+            dd /= diam;
+            asm volatile("" : "+v"(dd));
+          }
 #pragma unroll
-            for (int k = 0; k < NT; ++k)
-              c_tau[k >> 1] += (uint32_t)(dd >= thr[k]) << (16 * (k & 1));
-          } else {
+          for (int k = 0; k < NT; ++k)
+            c_tau[k >> 1] += (uint32_t)(dd >= s_thr[k]) << (16 * (k & 1));
+        }
+      };
+      auto vsd_px = [&](int p, uint32_t qe, uint32_t qg, float dtest) {
+        if constexpr (COST == 0) {
+          if (!filter) {
+            step_exact(p, qe, qg, dtest);
+            return;
+          }
+          bool vg, ve;
+          float lo, hi;
+          bool unc = vsd_filter_px(w_fA[p % kTileW] + w_fB[p / kTileW], qe, qg, dtest, a.dthr,
+                                   vg, ve, lo, hi);
+          const bool in = vg & ve;
+          c_union += vg | ve;
+          c_inter += in;
+#pragma unroll
+          for (int k = 0; k < NT; ++k) {
+            const bool ge_lo = in & (lo >= thr32[k]), ge_hi = in & (hi >= thr32[k]);
+            c_tau[k >> 1] += (uint32_t)ge_lo << (16 * (k & 1));
+            unc |= ge_lo != ge_hi;
+          }
+          if (__builtin_expect(__builtin_amdgcn_ballot_w64(unc) != 0, 0)) {
+            if (unc) {  // undo the float32 increments, redo the pixel exactly
+              if VSD_DIAG(4) atomicAdd(&g_vsd_stats[14], 1ull);
+              c_union -= vg | ve;
+              c_inter -= in;
+#pragma unroll
+              for (int k = 0; k < NT; ++k)
+                c_tau[k >> 1] -= (uint32_t)(in & (lo >= thr32[k])) << (16 * (k & 1));
+              step_exact(p, qe, qg, dtest);
+            }
+          }
+        } else {  // tlinear: float64 sums, exact sequence
+          const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
+          const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
+          const double pX = w_pX[p % kTileW];
+          const double pY = w_pY[p / kTileW];
+          const double dist_t = dist_of(pX, pY, dtest);
+          const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
+          const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
+          const bool vg = visib19t(dist_t, dist_g, a.dthr);
+          bool ve = visib19t(dist_t, dist_e, a.dthr);
+          ve = ve || (vg && dist_e > 0.0);  // visibility.py:74
+          c_union += (vg || ve);
+          if (vg && ve) {
+            ++c_inter;
+            double dd = fabs(dist_g - dist_e);
             if (a.normalized) dd /= a.diameters[b];
 #pragma unroll
             for (int k = 0; k < kMaxTaus; ++k) {
@@ -1536,7 +1671,7 @@ hipError_t launch_pose_roi(const ObjDesc* objs, int64_t n, const int32_t* slots,
 // deterministic float64 sums), with the fused kernel's per-pixel arithmetic.
 constexpr int kPairThreads = 256;
 constexpr int kPairWaves = kPairThreads / 64;
-constexpr int kPairCols = 2048;  // column coefficients staged in LDS per block of columns
+constexpr int kPairCols = 1024;  // column coefficients staged in LDS per block of columns
 // pixels per lane and step, their loads in flight together (round 3, same box:
 // 1 / 2 / 4 / 8 -> 4.3 / 3.85 / 4.03 / 4.4 ms on the multi-instance workload)
 constexpr int kPairU = 2;
@@ -1544,6 +1679,7 @@ constexpr int kPairU = 2;
 template <int COST, int NT>
 __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {
   __shared__ double s_pX[kPairCols];
+  __shared__ float s_fA[kPairCols];  // filter: pX^2 per column
   __shared__ double s_thr[kMaxTaus];
   __shared__ uint32_t s_cnt[kPairWaves][2 + kMaxTaus];
   __shared__ double s_lin[kPairWaves][kMaxTaus];
@@ -1587,13 +1723,12 @@ __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {
   const int ux1 = ee ? Rg.z : (ge ? Re.z : max(Re.z, Rg.z));
   const int uy1 = ee ? Rg.w : (ge ? Re.w : max(Re.w, Rg.w));
   __syncthreads();
-  double thr[NT];
+  float thr32[NT];  // the filter's float32 thresholds (SGPRs), as in k_vsd
 #pragma unroll
-  for (int k = 0; k < NT; ++k) {
-    const double v = COST == 0 ? s_thr[k] : 0.0;
-    thr[k] = __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
-                              __builtin_amdgcn_readfirstlane(__double2loint(v)));
-  }
+  for (int k = 0; k < NT; ++k)
+    thr32[k] = __int_as_float(
+        __builtin_amdgcn_readfirstlane(__float_as_int(COST == 0 ? filt_thr(s_thr[k]) : 0.0f)));
+  const bool filter = COST == 0 && !divide;
   uint32_t c_union = 0, c_inter = 0;
   uint32_t c_tau[(NT + 1) / 2];
   double lin[kMaxTaus];
@@ -1605,7 +1740,11 @@ __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {
   for (int cb = ux0; cb <= ux1; cb += kPairCols) {  // blocks of columns (wide images)
     const int cb1 = min(cb + kPairCols - 1, ux1);
     __syncthreads();  // the previous block's coefficients are consumed
-    for (int i = tid; i <= cb1 - cb; i += kPairThreads) s_pX[i] = ((double)(cb + i) - cx) / fx;
+    for (int i = tid; i <= cb1 - cb; i += kPairThreads) {
+      const double pX = ((double)(cb + i) - cx) / fx;
+      s_pX[i] = pX;
+      if constexpr (COST == 0) s_fA[i] = filt_a(pX);
+    }
     __syncthreads();
     for (int row = uy0 + wave; row <= uy1; row += kPairWaves) {
       const bool rin_e = row >= Re.y && row <= Re.w, rin_g = row >= Rg.y && row <= Rg.w;
@@ -1626,28 +1765,66 @@ __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {
       // kPairU pixels per lane and step: every load of the step in flight
       // before the first use (the loop is latency-bound on the q / test-depth
       // reads otherwise); lane -> pixel map fixed (col = L + lane + 64 i)
-      auto vsd_pixel = [&](uint32_t qe, uint32_t qg, float dtest, int col) {
-        const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
-        const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
-        const double pX = s_pX[col - cb];
-        const double dist_t = dist_of(pX, pY, dtest);
-        const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
-        const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
-        const bool vg = visib19t(dist_t, dist_g, a.dthr);
-        bool ve = visib19t(dist_t, dist_e, a.dthr);
-        ve = ve || (vg && dist_e > 0.0);  // visibility.py:74
+      const float fB = filt_b(pY);
+      // step cost: k_vsd's certified float32 filter with the exact fallback
+      auto step_exact = [&](uint32_t qe, uint32_t qg, float dtest, int col) {
+        bool vg, ve;
+        double dd;
+        vsd_exact_px(s_pX[col - cb], pY, qe, qg, dtest, a.dthr, vg, ve, dd);
         c_union += (vg || ve);
         if (vg && ve) {
           ++c_inter;
-          double dd = fabs(dist_g - dist_e);
-          if constexpr (COST == 0) {
-            if (divide) {
-              dd /= diam;
-              asm volatile("" : "+v"(dd));
-            }
+          if (divide) {
+            dd /= diam;
+            asm volatile("" : "+v"(dd));
+          }
 #pragma unroll
-            for (int k = 0; k < NT; ++k) c_tau[k >> 1] += (uint32_t)(dd >= thr[k]) << (16 * (k & 1));
-          } else {
+          for (int k = 0; k < NT; ++k)
+            c_tau[k >> 1] += (uint32_t)(dd >= s_thr[k]) << (16 * (k & 1));
+        }
+      };
+      auto vsd_pixel = [&](uint32_t qe, uint32_t qg, float dtest, int col) {
+        if constexpr (COST == 0) {
+          if (!filter) {
+            step_exact(qe, qg, dtest, col);
+            return;
+          }
+          bool vg, ve;
+          float lo, hi;
+          bool unc = vsd_filter_px(s_fA[col - cb] + fB, qe, qg, dtest, a.dthr, vg, ve, lo, hi);
+          const bool in = vg & ve;
+          c_union += vg | ve;
+          c_inter += in;
+#pragma unroll
+          for (int k = 0; k < NT; ++k) {
+            const bool ge_lo = in & (lo >= thr32[k]), ge_hi = in & (hi >= thr32[k]);
+            c_tau[k >> 1] += (uint32_t)ge_lo << (16 * (k & 1));
+            unc |= ge_lo != ge_hi;
+          }
+          if (__builtin_expect(__builtin_amdgcn_ballot_w64(unc) != 0, 0)) {
+            if (unc) {  // undo the float32 increments, redo the pixel exactly
+              c_union -= vg | ve;
+              c_inter -= in;
+#pragma unroll
+              for (int k = 0; k < NT; ++k)
+                c_tau[k >> 1] -= (uint32_t)(in & (lo >= thr32[k])) << (16 * (k & 1));
+              step_exact(qe, qg, dtest, col);
+            }
+          }
+        } else {  // tlinear: float64 sums, exact sequence
+          const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
+          const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
+          const double pX = s_pX[col - cb];
+          const double dist_t = dist_of(pX, pY, dtest);
+          const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
+          const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
+          const bool vg = visib19t(dist_t, dist_g, a.dthr);
+          bool ve = visib19t(dist_t, dist_e, a.dthr);
+          ve = ve || (vg && dist_e > 0.0);  // visibility.py:74
+          c_union += (vg || ve);
+          if (vg && ve) {
+            ++c_inter;
+            double dd = fabs(dist_g - dist_e);
             if (a.normalized) dd /= a.diameters[b];
 #pragma unroll
             for (int k = 0; k < kMaxTaus; ++k) {

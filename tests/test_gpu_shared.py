@@ -238,7 +238,7 @@ def test_unions_flag_batch_api(ntau):
 
 
 def test_shared_wide_image_column_blocks(oracle_mod):
-  """Unions wider than k_vsd_pair's 2,048-column LDS block (4,096 x 512
+  """Unions wider than k_vsd_pair's 1,024-column LDS block (4,096 x 512
   image, estimates shifted right by up to ~3,700 px, one partly off the right
   edge): equal to the fused kernel bit for bit and to the oracle."""
   import torch

@@ -34,6 +34,14 @@ PER_IMG = 6
 SCENES = list(range(48, 60))
 
 
+def progress(msg):
+  """Progress line on stderr (long generations: the GPU runner wants output)."""
+  print("[e2e %.0fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+
+T_START = time.perf_counter()
+
+
 def make_dataset(root, n_im, seed, torch, inst=1):
   from PIL import Image
   from concurrent.futures import ThreadPoolExecutor
@@ -85,8 +93,10 @@ def make_dataset(root, n_im, seed, torch, inst=1):
   frames = torch.where(occ, torch.full_like(frames, 450.0), frames)
   frames = frames + 2.0 * torch.randn(frames.shape, device=dev, generator=g)
   frames[torch.rand(frames.shape, device=dev, generator=g) < 0.1] = 0.0
-  png = torch.round(frames / DEPTH_SCALE).clamp_(0, 65535).to(torch.int32).cpu().numpy()
-  png = png.astype(np.uint16)
+  png = torch.round(frames / DEPTH_SCALE).clamp_(0, 65535).to(torch.int32).to(torch.int16)
+  png = png.cpu().numpy().view(np.uint16)  # 0..65535 through the int16 bit pattern
+  del frames
+  progress("rendered %d frames" % n_im)
 
   scene_of = np.array([SCENES[i * len(SCENES) // n_im] for i in range(n_im)])
   targets, lines = [], ["scene_id,im_id,obj_id,score,R,t,time"]
@@ -112,8 +122,15 @@ def make_dataset(root, n_im, seed, torch, inst=1):
       json.dump(cams, f)
     with open(os.path.join(sdir, "scene_gt.json"), "w") as f:
       json.dump(gts, f)
+  done = [0]
+
+  def save(j):
+    Image.fromarray(png[j[1]]).save(j[0])
+    done[0] += 1
+    if done[0] % 1000 == 0:
+      progress("%d / %d PNGs written" % (done[0], len(jobs)))
   with ThreadPoolExecutor(16) as pool:
-    list(pool.map(lambda j: Image.fromarray(png[j[1]]).save(j[0]), jobs))
+    list(pool.map(save, jobs))
   with open(os.path.join(ds, "test_targets_bop19.json"), "w") as f:
     json.dump(targets, f)
   os.makedirs(os.path.join(root, "results"))

@@ -42,7 +42,7 @@ def main():
   fn(ev.ctx.h, st, 1)
   names = ["tiles", "meshlet_entries", "tri_setups", "bbox_iters", "rows",
            "fragments", "covered_px", "row_passes", "pass_max_w_sum", "culled_entries",
-           "slow_tris", "slow_bbox_px", "slow_waves", "large_tris"]
+           "slow_tris", "slow_bbox_px", "slow_waves", "large_tris", "exact_px"]
   for i, k in enumerate(names):
     print("%-20s total %14d  per tuple %12.1f" % (k, st[i], st[i] / n))
   ph = ["clear+coeffs", "list", "raster work", "raster barrier", "pixel work",
