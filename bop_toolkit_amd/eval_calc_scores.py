@@ -85,14 +85,17 @@ class _Cache:
   eval_bop19_pose scores every folder at 10 thresholds in a row."""
 
   def __init__(self):
+    import threading
     self.d = {}
     self._folder = None
     self._errs = {}
+    self._lock = threading.RLock()  # FolderScorer's threads share one cache
 
   def get(self, key, fn):
-    if key not in self.d:
-      self.d[key] = fn()
-    return self.d[key]
+    with self._lock:
+      if key not in self.d:
+        self.d[key] = fn()
+      return self.d[key]
 
   def errors(self, folder, path, fn):
     if folder != self._folder:
@@ -171,7 +174,160 @@ def score_error_dir(p, error_dir_path, correct_th=None, cache=None, do_print=Tru
 def _score_job(job):
   error_dir_path, sps, do_print = job
   cache = _Cache()
+  if os.environ.get("BOPX_SCORE_NATIVE", "1") != "0":
+    out = score_error_dir_native(sps, error_dir_path, cache=cache, do_print=do_print)
+    if out is not None:
+      return [sc for sc, _ in out]
   return [score_error_dir(sp, error_dir_path, cache=cache, do_print=do_print)[0] for sp in sps]
+
+
+_SCORE_LIB = None
+
+
+def _score_lib():
+  """ctypes handle of bopx_score_folder (include/bopx_score.h) in libbopx_io.so."""
+  global _SCORE_LIB
+  if _SCORE_LIB is None:
+    import ctypes as C
+
+    class Args(C.Structure):
+      _fields_ = [("n_gt", C.c_int64), ("gt_scene", C.c_void_p), ("gt_im", C.c_void_p),
+                  ("gt_obj", C.c_void_p), ("gt_id", C.c_void_p), ("gt_valid", C.c_void_p),
+                  ("n_im", C.c_int64), ("im_off", C.c_void_p), ("im_file", C.c_void_p),
+                  ("n_files", C.c_int), ("err_paths", C.POINTER(C.c_char_p)),
+                  ("norm", C.c_int), ("n_diam", C.c_int), ("diam", C.c_void_p),
+                  ("width_factor", C.c_double), ("n_top", C.c_int), ("n_settings", C.c_int),
+                  ("n_th", C.c_int), ("th", C.c_void_p), ("matches_paths", C.POINTER(C.c_char_p)),
+                  ("matched", C.c_void_p), ("threads", C.c_int)]
+    lib = inout._io_lib()
+    lib.bopx_score_folder.argtypes = [C.POINTER(Args), C.c_char_p, C.c_int]
+    lib.bopx_score_folder.restype = C.c_int
+    _SCORE_LIB = (lib, Args)
+  return _SCORE_LIB
+
+
+def _gt_table(cache, dp_split, targets_org, visib_gt_min):
+  """The matches file's GT records in order (targets' scenes and images, every
+  GT of an image) as arrays, with per-image offsets and scene index
+  (score_error_dir's scene_gt / gt_valid, eval_calc_scores.py:183-214)."""
+  import numpy as np
+
+  def build():
+    sc, im, ob, gid, val, off, fi = [], [], [], [], [], [0], []
+    from .eval_calc_errors import cached_load  # the error passes' parses (same process)
+    for k, (scene_id, scene_targets) in enumerate(targets_org.items()):
+      scene_gt = cached_load(inout.load_scene_gt,
+                             dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+      scene_gt_info = cached_load(inout.load_json,
+                                  dp_split["scene_gt_info_tpath"].format(scene_id=scene_id),
+                                  keys_to_int=True)
+      for im_id, tg in scene_targets.items():
+        im_gts = scene_gt[im_id]
+        valid = valid_gts(im_gts, scene_gt_info[im_id], tg, visib_gt_min)
+        for g, gt in enumerate(im_gts):
+          sc.append(scene_id)
+          im.append(im_id)
+          ob.append(gt["obj_id"])
+          gid.append(g)
+          val.append(bool(valid[g]))
+        off.append(len(sc))
+        fi.append(k)
+    i32 = lambda a: np.ascontiguousarray(a, np.int32)
+    return (i32(sc), i32(im), i32(ob), i32(gid), np.ascontiguousarray(val, np.uint8),
+            np.ascontiguousarray(off, np.int64), i32(fi))
+  key = ("gt_table", dp_split["base_path"], id(targets_org), visib_gt_min)
+  return cache.get(key, build)
+
+
+def score_error_dir_native(sps, error_dir_path, cache=None, do_print=True, threads=0):
+  """score_error_dir for every setting in sps (one errors folder; the settings
+  differ only in correct_th) through the native scorer (bopx_score_folder:
+  the errors files parsed once, the matches files written by C++, the same
+  bytes). Returns [(scores, score_sign)] in sps order, or None when the
+  scorer declines the inputs (the Python path then runs and raises what the
+  reference raises)."""
+  import ctypes as C
+
+  import numpy as np
+  if not sps:
+    return []
+  p = sps[0]
+  cache = cache or _Cache()
+  error_sign = os.path.basename(error_dir_path)
+  err_type = str(error_sign.split("_")[0].split("=")[1])
+  n_top = int(error_sign.split("_")[1].split("=")[1])
+  for sp in sps[1:]:
+    if any(sp[k] != p[k] for k in p if k != "correct_th"):
+      return None
+  ths = [sp["correct_th"][err_type] for sp in sps]
+  if len(set(len(t) for t in ths)) != 1:
+    return None
+  info = os.path.basename(os.path.dirname(error_dir_path)).split("_")
+  method, ds = info[0], info[1].split("-")
+  dataset, split = ds[0], ds[1]
+  split_type = ds[2] if len(ds) > 2 else None
+  dp_split = dataset_params.get_split_params(p["datasets_path"], dataset, split, split_type)
+  dp_model = dataset_params.get_model_params(p["datasets_path"], dataset, "eval")
+  models_info = cache.get(("info", dp_model["models_info_path"]), lambda: inout.load_json(
+      dp_model["models_info_path"], keys_to_int=True))
+  tpath = os.path.join(dp_split["base_path"], p["targets_filename"])
+  targets = cache.get(("targets", tpath), lambda: inout.load_json(tpath))
+
+  def org():
+    t_org = {}
+    for t in targets:
+      t_org.setdefault(t["scene_id"], {}).setdefault(t["im_id"], {})[t["obj_id"]] = t
+    return t_org
+  targets_org = cache.get(("targets_org", tpath), org)
+  sc, im, ob, gid, val, off, fi = _gt_table(cache, dp_split, targets_org, p["visib_gt_min"])
+  err_paths = [p["error_tpath"].format(eval_path=p["eval_path"], error_dir_path=error_dir_path,
+                                       scene_id=scene_id) for scene_id in targets_org]
+  signs = [misc.get_score_signature(th, p["visib_gt_min"]) for th in ths]
+  mpaths = [p["out_matches_tpath"].format(eval_path=p["eval_path"], error_dir_path=error_dir_path,
+                                          score_sign=sg) for sg in signs]
+  lib, Args = _score_lib()
+  norm, diam, factor = 0, np.zeros(1), 0.0
+  if err_type in p["normalized_by_diameter"]:
+    ids = [o for o in models_info if isinstance(o, int) and o >= 0]
+    if not ids or len(ids) != len(models_info):
+      return None
+    diam = np.full(max(ids) + 1, np.nan)
+    for o in ids:
+      diam[o] = float(models_info[o]["diameter"])
+    norm = 1
+  elif err_type in p["normalized_by_im_width"]:
+    norm, factor = 2, 640.0 / float(dp_split["im_size"][0])
+  th = np.ascontiguousarray(ths, np.float64)
+  matched = np.zeros((len(sps), len(sc)), np.uint8)
+  paths_c = (C.c_char_p * len(err_paths))(*[x.encode() for x in err_paths])
+  mpaths_c = (C.c_char_p * len(mpaths))(*[x.encode() for x in mpaths])
+  diam = np.ascontiguousarray(diam, np.float64)
+  ptr = lambda a: a.ctypes.data
+  a = Args(len(sc), ptr(sc), ptr(im), ptr(ob), ptr(gid), ptr(val), len(off) - 1, ptr(off),
+           ptr(fi), len(err_paths), paths_c, norm, len(diam), ptr(diam), factor, n_top,
+           len(sps), th.shape[1], ptr(th), mpaths_c, ptr(matched),
+           int(os.environ.get("BOPX_SCORE_THREADS", "0")) or threads or min(len(sps), 8))
+  for sg in signs:
+    misc.log("Calculating score - error: {}, method: {}, dataset: {}.".format(
+        err_type, method, dataset))
+  msg = C.create_string_buffer(512)
+  st = lib.bopx_score_folder(C.byref(a), msg, len(msg))
+  if st in (1, 2, 3):
+    # unreadable / unparsable errors files or inputs the scorer does not take
+    # (BOPX_SCORE_READ, _PARSE, _UNSUPPORTED): the Python path, which raises
+    # what the reference raises for bad files
+    return None
+  if st != 0:
+    raise RuntimeError("bopx_score_folder: %s (status %d)" % (msg.value.decode(), st))
+  scorer = cache.get(("scorer", id(sc), n_top), lambda: score.ArrayScorer(
+      dp_split["scene_ids"], dp_model["obj_ids"], sc, im, ob, val, n_top))
+  out = []
+  for k, sg in enumerate(signs):
+    scores = scorer.scores(matched[k], do_print=do_print)
+    fmt = dict(eval_path=p["eval_path"], error_dir_path=error_dir_path, score_sign=sg)
+    inout.save_json(p["out_scores_tpath"].format(**fmt), scores)
+    out.append((scores, sg))
+  return out
 
 
 def _lower_priority():
@@ -181,24 +337,57 @@ def _lower_priority():
     pass
 
 
+def _score_job_threaded(job, cache, threads):
+  """_score_job in a thread of the calling process (native scorer: the GIL is
+  released while it runs; the GT side is parsed once for all folders)."""
+  error_dir_path, sps, do_print = job
+  out = score_error_dir_native(sps, error_dir_path, cache=cache, do_print=do_print,
+                               threads=threads)
+  if out is not None:
+    return [sc for sc, _ in out]
+  own = _Cache()  # the Python path (inputs the native scorer declines)
+  return [score_error_dir(sp, error_dir_path, cache=own, do_print=do_print)[0] for sp in sps]
+
+
+def _native_available():
+  if os.environ.get("BOPX_SCORE_NATIVE", "1") == "0":
+    return False
+  try:
+    _score_lib()
+    return True
+  except (OSError, AttributeError, RuntimeError):
+    return False
+
+
 class FolderScorer:
   """score_folders in stages: submit(jobs) queues a group of folders (scored
-  at once by the pool while the caller goes on, e.g. computes the next error
-  type's folders on the GPU), results() returns every group's scores in
-  submission order. The spawned pool starts at once, its workers at a lower
-  CPU priority (nice +5), so their interpreter start-up runs behind the
-  caller's first error pass instead of after it (BOPX_SCORE_EARLY=0: start
-  with the first submit)."""
+  at once while the caller goes on, e.g. computes the next error type's
+  folders on the GPU), results() returns every group's scores in submission
+  order.
+
+  Native scorer (libbopx_io.so, the default): a pool of threads of this
+  process, each folder one bopx_score_folder call over all its settings, the
+  GT side parsed once (shared with the error passes' file cache). Without it
+  (BOPX_SCORE_NATIVE=0): a pool of spawned processes running the Python
+  scorer, started at once at a lower CPU priority (nice +5), so their
+  interpreter start-up runs behind the caller's first error pass
+  (BOPX_SCORE_EARLY=0: start with the first submit)."""
 
   def __init__(self, n_folders, workers=None, do_print=True):
+    self.native = _native_available()
     if workers is None:
       workers = int(os.environ.get("BOPX_SCORE_WORKERS", "0")) or \
-          min(n_folders, os.cpu_count() or 1, 16)
+          min(n_folders, os.cpu_count() or 1, 8 if self.native else 16)
     self.do_print = do_print
     self.workers = workers if n_folders > 1 else 1
     self.pool = None
+    self.tpool = None
+    self.cache = _Cache()
     self.pending = []
-    if self.workers > 1 and os.environ.get("BOPX_SCORE_EARLY", "1") != "0":
+    if self.native:
+      from concurrent.futures import ThreadPoolExecutor
+      self.tpool = ThreadPoolExecutor(max(1, self.workers))
+    elif self.workers > 1 and os.environ.get("BOPX_SCORE_EARLY", "1") != "0":
       self._start()
 
   def _start(self):
@@ -207,6 +396,12 @@ class FolderScorer:
 
   def submit(self, jobs):
     args = [(path, sps, self.do_print) for path, sps in jobs]
+    if self.tpool is not None:
+      # native threads per folder: the host's scoring share (16) over the group
+      thr = max(1, 16 // max(1, len(args)))
+      self.pending.append([[self.tpool.submit(_score_job_threaded, a, self.cache, thr)]
+                           for a in args])
+      return
     if self.pool is None and self.workers > 1:
       self._start()
     if self.pool is None:
@@ -230,17 +425,23 @@ class FolderScorer:
       out = []
       for group in self.pending:  # per folder: its chunks' scores in setting order
         for chunks in group:
-          out.append([s for c in chunks for s in (c if isinstance(c, list) else c.get())])
+          got = []
+          for c in chunks:
+            got += c if isinstance(c, list) else (c.result() if hasattr(c, "result") else c.get())
+          out.append(got)
       return out
     finally:
       self.close()
 
   def close(self):
-    """Stops the pool (after results(), or on an error: terminates it)."""
+    """Stops the pools (after results(), or on an error: terminates them)."""
     if self.pool is not None:
       self.pool.terminate()
       self.pool.join()
       self.pool = None
+    if self.tpool is not None:
+      self.tpool.shutdown(wait=True)
+      self.tpool = None
 
 
 def score_folders(jobs, workers=None, do_print=True):

@@ -52,6 +52,13 @@ def calc_localization_scores(scene_ids, obj_ids, matches, n_top, do_print=True):
       tps += 1
       obj_tps[m["obj_id"]] += 1
       scene_tps[m["scene_id"]] += 1
+  return _scores(obj_ids, scene_ids, len(matches), tars, tps, obj_tars, obj_tps, scene_tars,
+                 scene_tps, do_print)
+
+
+def _scores(obj_ids, scene_ids, gt_count, tars, tps, obj_tars, obj_tps, scene_tars, scene_tps,
+            do_print):
+  """The scores dict of score.py:126-157 from the target / true-positive counts."""
   obj_recalls = {o: calc_recall(obj_tps[o], obj_tars[o]) for o in obj_ids}
   scene_recalls = {s: float(calc_recall(scene_tps[s], scene_tars[s])) for s in scene_ids}
   scores = {
@@ -60,7 +67,7 @@ def calc_localization_scores(scene_ids, obj_ids, matches, n_top, do_print=True):
       "mean_obj_recall": float(float(np.mean(list(obj_recalls.values())).squeeze())),
       "scene_recalls": scene_recalls,
       "mean_scene_recall": float(float(np.mean(list(scene_recalls.values())).squeeze())),
-      "gt_count": len(matches),
+      "gt_count": gt_count,
       "targets_count": int(tars),
       "tp_count": int(tps),
   }
@@ -78,3 +85,54 @@ def calc_localization_scores(scene_ids, obj_ids, matches, n_top, do_print=True):
         "{}: {:.3f}".format(i, v) for i, v in scene_recalls.items())))
     misc.log("")
   return scores
+
+
+class ArrayScorer:
+  """calc_localization_scores for many match outcomes of one GT table (arrays
+  in the matches file's order: scene, image, object, validity): the targets
+  (valid GT instances per (object, scene, image), capped at n_top) are counted
+  once; each outcome (`matched` flags) then only counts its true positives.
+  The same integer counts and float expressions as calc_localization_scores,
+  without building the match dicts. A valid record of an object or scene
+  outside obj_ids / scene_ids raises KeyError, as the reference's lookups do."""
+
+  def __init__(self, scene_ids, obj_ids, gt_scene, gt_im, gt_obj, gt_valid, n_top):
+    self.scene_ids, self.obj_ids, self.n_top = list(scene_ids), list(obj_ids), n_top
+    self.valid = np.asarray(gt_valid, bool)
+    obj = np.asarray(gt_obj, np.int64)[self.valid]
+    scn = np.asarray(gt_scene, np.int64)[self.valid]
+    im = np.asarray(gt_im, np.int64)[self.valid]
+    oix = {o: k for k, o in enumerate(self.obj_ids)}
+    six = {sc: k for k, sc in enumerate(self.scene_ids)}
+    for o in np.unique(obj).tolist():
+      if o not in oix:
+        raise KeyError(o)
+    for sc in np.unique(scn).tolist():
+      if sc not in six:
+        raise KeyError(sc)
+    lut = lambda ids, ix: np.array([ix[v] for v in ids.tolist()], np.int64) if len(ids) else \
+        np.zeros(0, np.int64)
+    uo, io = np.unique(obj, return_inverse=True)
+    us, is_ = np.unique(scn, return_inverse=True)
+    self.oi = lut(uo, oix)[io] if len(obj) else np.zeros(0, np.int64)
+    self.si = lut(us, six)[is_] if len(scn) else np.zeros(0, np.int64)
+    # targets: valid instances per (object, scene, image), capped at n_top
+    key = (self.oi * len(self.scene_ids) + self.si) * (int(im.max()) + 1 if len(im) else 1) + \
+        (im - (int(im.min()) if len(im) else 0))
+    uk, first, cnt = np.unique(key, return_index=True, return_counts=True)
+    if n_top > 0:
+      cnt = np.minimum(n_top, cnt)
+    self.obj_tars = np.bincount(self.oi[first], cnt, len(self.obj_ids)).astype(np.int64)
+    self.scene_tars = np.bincount(self.si[first], cnt, len(self.scene_ids)).astype(np.int64)
+    self.tars = int(cnt.sum())
+    self.gt_count = len(self.valid)
+
+  def scores(self, matched, do_print=True):
+    tp = np.asarray(matched, bool)[self.valid]
+    obj_tps = np.bincount(self.oi[tp], minlength=len(self.obj_ids))
+    scene_tps = np.bincount(self.si[tp], minlength=len(self.scene_ids))
+    return _scores(self.obj_ids, self.scene_ids, self.gt_count, self.tars, int(tp.sum()),
+                   dict(zip(self.obj_ids, self.obj_tars.tolist())),
+                   dict(zip(self.obj_ids, obj_tps.tolist())),
+                   dict(zip(self.scene_ids, self.scene_tars.tolist())),
+                   dict(zip(self.scene_ids, scene_tps.tolist())), do_print)

@@ -57,11 +57,25 @@ def test_cached_load_rereads_changed_files(tmp_path):
 def test_folder_scorer_in_order_without_pool(monkeypatch):
   """One worker: groups scored at submit time, results in submission order;
   close() is idempotent."""
+  monkeypatch.setenv("BOPX_SCORE_NATIVE", "0")  # the Python scorer's process-pool mode
   monkeypatch.setattr(ecs, "_score_job", lambda job: [job[0] + ":" + s for s in job[1]])
   fs = ecs.FolderScorer(3, workers=1)
   fs.submit([("a", ["1", "2"])])
   fs.submit([("b", ["1"]), ("c", [])])
   assert fs.results() == [["a:1", "a:2"], ["b:1"], []]
+  fs.close()
+
+
+def test_folder_scorer_threads_in_order(monkeypatch):
+  """Native scorer mode: folders on a thread pool, results in submission order."""
+  import time
+  monkeypatch.setattr(ecs, "_score_job_threaded", lambda job, cache, thr: (
+      time.sleep(0.01 * len(job[1])), [job[0] + ":" + s for s in job[1]])[1])
+  fs = ecs.FolderScorer(3, workers=3)
+  assert fs.tpool is not None
+  fs.submit([("a", ["1", "2", "3"])])
+  fs.submit([("b", ["1"]), ("c", [])])
+  assert fs.results() == [["a:1", "a:2", "a:3"], ["b:1"], []]
   fs.close()
 
 
