@@ -339,6 +339,58 @@ struct Groups {
 
 extern "C" int bopx_py_float_repr(double v, char* out) { return py_repr(v, out); }
 
+extern "C" int bopx_write_errors(const char* const* paths, int n_values, int64_t n_rec,
+                                 const int64_t* rec_im, const int64_t* rec_obj,
+                                 const int64_t* rec_est, const double* rec_score,
+                                 const int64_t* pair_off, const int64_t* pair_gt,
+                                 const double* values) {
+  if (n_values <= 0 || n_rec < 0) return BOPX_SCORE_INVALID;
+  std::atomic<int> next{0}, status{BOPX_SCORE_OK};
+  // the record text around its values (shared by the n_values files)
+  std::vector<std::string> tail((size_t)n_rec);
+  for (int64_t r = 0; r < n_rec; ++r) {
+    std::string& t = tail[(size_t)r];
+    t += pair_off[r + 1] > pair_off[r] ? "]}, \"est_id\": " : "}, \"est_id\": ";
+    put_int(t, rec_est[r]);
+    t += ", \"im_id\": ";
+    put_int(t, rec_im[r]);
+    t += ", \"obj_id\": ";
+    put_int(t, rec_obj[r]);
+    t += ", \"score\": ";
+    put_num(t, Num{rec_score[r], 0, false});
+    t += '}';
+  }
+  auto work = [&]() {
+    std::string out;
+    char b[40];
+    for (int k; (k = next.fetch_add(1)) < n_values;) {
+      out.clear();
+      out += n_rec ? "[\n  " : "[\n";
+      for (int64_t r = 0; r < n_rec; ++r) {
+        if (r) out += ",\n  ";
+        out += "{\"errors\": {";
+        for (int64_t q = pair_off[r]; q < pair_off[r + 1]; ++q) {
+          out += q > pair_off[r] ? "], \"" : "\"";
+          put_int(out, pair_gt[q]);
+          out += "\": [";
+          out.append(b, py_repr(values[q * n_values + k], b));
+        }
+        out += tail[(size_t)r];
+      }
+      out += n_rec ? "\n]" : "]";
+      FILE* fp = std::fopen(paths[k], "wb");
+      if (!fp || std::fwrite(out.data(), 1, out.size(), fp) != out.size()) status = BOPX_SCORE_READ;
+      if (fp) std::fclose(fp);
+    }
+  };
+  const int nt = std::max(1, std::min(n_values, 4));
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  return status.load();
+}
+
 extern "C" int bopx_score_folder(const bopx_score_args* a, char* msg_out, int msg_len) {
   std::string msg;
   auto ret = [&](int code) {

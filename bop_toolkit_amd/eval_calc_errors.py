@@ -369,15 +369,28 @@ def todo_images(recs, todo):
   return sorted({recs[ri]["im_id"] for ri, _, _, _ in todo})
 
 
-def load_scene_depths(dp_split, scene_camera, scene_id, ims, torch=None):
+_PINNED = [None]  # the page-locked staging buffer reused by load_scene_depths(reuse=True)
+
+
+def load_scene_depths(dp_split, scene_camera, scene_id, ims, torch=None, reuse=False):
   """Test depth of the images ims in mm, float32 (eval_calc_errors.py:240-243),
   decoded straight into one (n, H, W) array — page-locked when torch is given,
-  so the upload to the GPU is one DMA — or a list when the sizes differ."""
+  so the upload to the GPU is one DMA — or a list when the sizes differ.
+  reuse: the frames land in one page-locked buffer kept across calls (grown
+  when needed; page-locking a scene's 1-2 GB anew per scene is slow), valid
+  until the next such call — the caller uploads and synchronises first."""
   paths = [dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id) for im_id in ims]
   scales = [scene_camera[im_id]["depth_scale"] for im_id in ims]  # float32 in place, :242-243
   W, H = dp_split["im_size"]
   if torch is not None and torch.cuda.is_available() and os.environ.get("BOPX_PIN", "1") != "0":
-    buf = torch.empty((len(ims), H, W), dtype=torch.float32, pin_memory=True)
+    if reuse:
+      need = len(ims) * H * W
+      if _PINNED[0] is None or _PINNED[0].numel() < need:
+        _PINNED[0] = None
+        _PINNED[0] = torch.empty(max(need, 1), dtype=torch.float32, pin_memory=True)
+      buf = _PINNED[0][:need].view(len(ims), H, W)
+    else:
+      buf = torch.empty((len(ims), H, W), dtype=torch.float32, pin_memory=True)
     try:
       inout.load_depths(paths, scales=scales, out=buf.numpy())
       return buf
@@ -388,6 +401,45 @@ def load_scene_depths(dp_split, scene_camera, scene_id, ims, torch=None):
     return inout.load_depths(paths, scales=scales, out=buf)
   except ValueError:
     return inout.load_depths(paths, scales=scales)
+
+
+def _vsd_launch(ev, torch, p, dataset, slots, d_pe, d_pg, obj, pe, pg, fidx_h, fidx, cam, depths,
+                models_info):
+  """The GPU VSD rows of one scene batch: the fused kernel, or shared renders
+  for multi-instance batches (SHARED_RENDER_RATIO)."""
+  n = len(obj)
+  dev = ev.device
+  T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+  if isinstance(depths, list):
+    depths = np.stack(depths)
+  d_frames = depths.to(dev, non_blocking=True) if torch.is_tensor(depths) else T(depths, torch.float32)
+  dia = np.array([models_info[o]["diameter"] for o in obj], np.float64)
+  delta = p["vsd_deltas"][dataset]
+  from . import runtime
+  from .batch import unique_renders
+  # multi-instance images (every estimate x every GT instance of its object,
+  # :281-290): each distinct pose rendered once when that saves renders
+  # one tuple per (image, object) (single-instance data): 2 n renders, fused path
+  single = len(np.unique(fidx_h.astype(np.int64) << 32 | obj.astype(np.int64))) == n
+  ro, rp, rf, er, gr = (None,) * 5 if single and SHARED_RENDER_RATIO < 2 else \
+      unique_renders(obj, pe, pg, fidx_h)
+  if ro is not None and len(ro) <= SHARED_RENDER_RATIO * n:
+    from ._lib import BopxOOMError
+    try:
+      return ev.vsd_shared(ev.slots(ro), T(rp, torch.float64), T(rf, torch.int32),
+                           T(er, torch.int32), T(gr, torch.int32), d_frames,
+                           T(cam, torch.float64), delta, p["vsd_taus"], T(dia, torch.float64),
+                           normalized_by_diameter=p["vsd_normalized_by_diameter"],
+                           cost_type="step", delta_flags=runtime.delta_flags(delta))
+    except BopxOOMError:
+      # the shared path's ROI-sized depth buffers (outside torch's caching
+      # allocator) did not fit: the fused kernel needs no such scratch and
+      # gives the same rows bit for bit
+      torch.cuda.empty_cache()
+  return ev.vsd(slots, d_pe, d_pg, fidx, d_frames,
+                T(cam, torch.float64), delta, p["vsd_taus"], T(dia, torch.float64),
+                normalized_by_diameter=p["vsd_normalized_by_diameter"], cost_type="step",
+                delta_flags=runtime.delta_flags(delta))
 
 
 def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs, models_info,
@@ -415,36 +467,8 @@ def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs
       return ev.cover(slots, d_pe, d_pg, fidx, T(cam, torch.float64), W, H)
     if depths is None:
       depths = load_scene_depths(dp_split, scene_camera, scene_id, ims, torch)
-    if isinstance(depths, list):
-      depths = np.stack(depths)
-    d_frames = depths.to(dev, non_blocking=True) if torch.is_tensor(depths) else T(depths, torch.float32)
-    dia = np.array([models_info[o]["diameter"] for o in obj], np.float64)
-    delta = p["vsd_deltas"][dataset]
-    from . import runtime
-    from .batch import unique_renders
-    # multi-instance images (every estimate x every GT instance of its object,
-    # :281-290): each distinct pose rendered once when that saves renders
-    # one tuple per (image, object) (single-instance data): 2 n renders, fused path
-    single = len(np.unique(fidx_h.astype(np.int64) << 32 | obj.astype(np.int64))) == n
-    ro, rp, rf, er, gr = (None,) * 5 if single and SHARED_RENDER_RATIO < 2 else \
-        unique_renders(obj, pe, pg, fidx_h)
-    if ro is not None and len(ro) <= SHARED_RENDER_RATIO * n:
-      from ._lib import BopxOOMError
-      try:
-        return ev.vsd_shared(ev.slots(ro), T(rp, torch.float64), T(rf, torch.int32),
-                             T(er, torch.int32), T(gr, torch.int32), d_frames,
-                             T(cam, torch.float64), delta, p["vsd_taus"], T(dia, torch.float64),
-                             normalized_by_diameter=p["vsd_normalized_by_diameter"],
-                             cost_type="step", delta_flags=runtime.delta_flags(delta))
-      except BopxOOMError:
-        # the shared path's ROI-sized depth buffers (outside torch's caching
-        # allocator) did not fit: the fused kernel needs no such scratch and
-        # gives the same rows bit for bit
-        torch.cuda.empty_cache()
-    return ev.vsd(slots, d_pe, d_pg, fidx, d_frames,
-                  T(cam, torch.float64), delta, p["vsd_taus"], T(dia, torch.float64),
-                  normalized_by_diameter=p["vsd_normalized_by_diameter"], cost_type="step",
-                  delta_flags=runtime.delta_flags(delta))
+    return _vsd_launch(ev, torch, p, dataset, slots, d_pe, d_pg, obj, pe, pg, fidx_h, fidx, cam,
+                       depths, models_info)
   if et in ("mspd", "proj"):
     K = np.stack([scene_camera[recs[ri]["im_id"]]["cam_K"].reshape(9) for ri, _, _, _ in todo])
     fn = ev.mspd if et == "mspd" else ev.proj
@@ -461,6 +485,98 @@ def evaluate_batch(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs
         out[ii] = fn(slots[ii], d_pe[ii], d_pg[ii])
     return out.view(n, 1)
   raise ValueError("Unknown pose error function.")
+
+
+# ---------------------------------------------------- array path (BOP19 types)
+# The error types of a BOP19 evaluation (VSD, MSSD, MSPD) on one process: the
+# records of a scene and their (record, GT) pairs as arrays, the gates and the
+# GPU rows written into one values array, the errors files by the native
+# writer (inout.save_errors_arrays): no per-tuple Python dicts. The same tuples,
+# fills and bytes as plan / evaluate / save_json (tests/test_e2e_errors.py);
+# BOPX_ERRORS_ARRAYS=0 takes the record-dict path.
+ARRAY_TYPES = ("vsd", "mssd", "mspd")
+
+
+def scene_arrays(recs):
+  """Records of a scene (scene_records) as arrays: rec_im / rec_obj / rec_est
+  int64, rec_score float64, pose [n_rec, 12]; their GT pairs in record order
+  (ascending GT id) pair_off [n_rec + 1], pair_ri, pair_gt, pg [n_pairs, 12]."""
+  n = len(recs)
+  rec_im = np.fromiter((r["im_id"] for r in recs), np.int64, n)
+  rec_obj = np.fromiter((r["obj_id"] for r in recs), np.int64, n)
+  rec_est = np.fromiter((r["est_id"] for r in recs), np.int64, n)
+  rec_score = np.fromiter((r["score"] for r in recs), np.float64, n)
+  cnt = np.fromiter((len(r["gts"]) for r in recs), np.int64, n)
+  pair_off = np.zeros(n + 1, np.int64)
+  np.cumsum(cnt, out=pair_off[1:])
+  m = int(pair_off[-1])
+  pair_ri = np.repeat(np.arange(n, dtype=np.int64), cnt)
+  pair_gt = np.fromiter((g for r in recs for g, _ in r["gts"]), np.int64, m)
+  pe = _poses12([r["R"] for r in recs], [r["t"] for r in recs]) if n else np.zeros((0, 12))
+  pg = _poses12([gt["cam_R_m2c"] for r in recs for _, gt in r["gts"]],
+                [gt["cam_t_m2c"] for r in recs for _, gt in r["gts"]]) if m else np.zeros((0, 12))
+  return {"rec_im": rec_im, "rec_obj": rec_obj, "rec_est": rec_est, "rec_score": rec_score,
+          "pe": pe, "pair_off": pair_off, "pair_ri": pair_ri, "pair_gt": pair_gt, "pg": pg}
+
+
+_ARR_CACHE = {}
+
+
+def scene_arrays_cached(recs):
+  """scene_arrays, shared by the error types of one BOP19 run (recs is the
+  cached record list: keyed on its identity)."""
+  hit = _ARR_CACHE.get(id(recs))
+  if hit is not None and hit[0] is recs:
+    return hit[1]
+  out = scene_arrays(recs)
+  if len(_ARR_CACHE) >= 4096:
+    _ARR_CACHE.clear()
+  _ARR_CACHE[id(recs)] = (recs, out)
+  return out
+
+
+def plan_arrays(p, arr, models_info):
+  """plan() on the arrays: the values array [n_pairs, n_values] with the gate
+  fills (VSD 1.0, MSSD inf; MSPD ungated, :296-339) and the pair indices left
+  for the GPU."""
+  et = p["error_type"]
+  nv = len(p["vsd_taus"]) if et == "vsd" else 1
+  m = len(arr["pair_gt"])
+  vals = np.empty((m, nv), np.float64)
+  fill = np.zeros(m, bool)
+  if m and et in ("vsd", "mssd"):
+    objs, inv = np.unique(arr["rec_obj"][arr["pair_ri"]], return_inverse=True)
+    dia = np.array([models_info[o]["diameter"] for o in objs.tolist()], np.float64)[inv]
+    fill = gates(et, dia, arr["pe"][arr["pair_ri"], 9:12], arr["pg"][:, 9:12])
+    vals[fill] = 1.0 if et == "vsd" else float("inf")
+  return vals, np.nonzero(~fill)[0]
+
+
+def evaluate_batch_arrays(ev, torch, p, dataset, dp_split, scene_camera, scene_id, arr, todo,
+                          models_info, depths=None):
+  """evaluate_batch on the arrays: the GPU rows [len(todo), n_values] of the
+  pairs todo (depths: the frames of their sorted images, or None)."""
+  et = p["error_type"]
+  dev = ev.device
+  ri = arr["pair_ri"][todo]
+  obj = arr["rec_obj"][ri].astype(np.int32)
+  pe, pg = arr["pe"][ri], arr["pg"][todo]
+  T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+  slots = ev.slots(obj)
+  d_pe, d_pg = T(pe, torch.float64), T(pg, torch.float64)
+  ims, inv = np.unique(arr["rec_im"][ri], return_inverse=True)  # todo_images order
+  Ks = [np.asarray(scene_camera[im]["cam_K"], np.float64).reshape(3, 3) for im in ims.tolist()]
+  if et == "vsd":
+    cam = np.array([[K[0, 0], K[1, 1], K[0, 2], K[1, 2]] for K in Ks], np.float64)
+    fidx_h = inv.astype(np.int32)
+    if depths is None:
+      depths = load_scene_depths(dp_split, scene_camera, scene_id, ims.tolist(), torch)
+    return _vsd_launch(ev, torch, p, dataset, slots, d_pe, d_pg, obj, pe, pg, fidx_h,
+                       T(fidx_h, torch.int32), cam, depths, models_info)
+  if et == "mspd":
+    K = np.stack([K.reshape(9) for K in Ks])[inv]
+    return ev.mspd(slots, d_pe, d_pg, T(K, torch.float64)).view(len(todo), 1)
+  return ev.mssd(slots, d_pe, d_pg).view(len(todo), 1)
 
 
 def _dist():
@@ -598,6 +714,8 @@ def run(p, device=0):
     sym_ids = set(dp_model["symmetric_obj_ids"] or [])
     ests_counter = 0
     rank, world = _dist()
+    arrays = (et in ARRAY_TYPES and world == 1 and ev is not None and
+              os.environ.get("BOPX_ERRORS_ARRAYS", "1") != "0")
     # VSD test depth goes to the GPU from the prepare thread on a stream of its
     # own, overlapping the current scene's kernels (the main stream only ever
     # sees frames already resident)
@@ -615,7 +733,22 @@ def run(p, device=0):
                              dp_split["scene_gt_tpath"].format(scene_id=scene_id))
       recs, n_ests = scene_records_cached(p, scene_id, scene_targets, ests_org, scene_gt)
       planned = None
-      if recs:
+      if arrays:
+        arr = scene_arrays_cached(recs)
+        vals, todo = plan_arrays(p, arr, models_info)
+        depths = None
+        if et == "vsd" and len(todo):
+          depths = load_scene_depths(dp_split, scene_camera, scene_id,
+                                     np.unique(arr["rec_im"][arr["pair_ri"][todo]]).tolist(),
+                                     torch, reuse=up is not None)
+          if up is not None and torch.is_tensor(depths):
+            with torch.cuda.stream(up[0]):
+              d = depths.to(ev.device, non_blocking=True)
+            up[0].synchronize()
+            d.record_stream(up[1])
+            depths = d
+        planned = ("arrays", arr, vals, todo, depths)
+      elif recs:
         errs, todo, mine = plan_rank(p, recs, models_info, ev.objects if ev else None,
                                      scene_camera, dp_split["im_size"], rank, world)
         depths = None
@@ -642,6 +775,26 @@ def run(p, device=0):
         log("Calculating error {} - method: {}, dataset: {}{}, scene: {}".format(
             et, method, dataset, split_type_str, scene_id))
         ests_counter += n_ests
+        if arrays:
+          _, arr, vals, todo, depths = planned
+          if len(todo):
+            rows = evaluate_batch_arrays(ev, torch, p, dataset, dp_split, scene_camera,
+                                         scene_id, arr, todo, models_info, depths)
+            vals[todo] = rows.cpu().numpy()
+          if et == "vsd":  # one file per tau (:401-415)
+            signs = [misc.get_error_signature(et, p["n_top"], vsd_delta=p["vsd_deltas"][dataset],
+                                              vsd_tau=tau) for tau in p["vsd_taus"]]
+          else:
+            signs = [misc.get_error_signature(et, p["n_top"])]
+          paths = [p["out_errors_tpath"].format(eval_path=p["eval_path"], result_name=result_name,
+                                                error_sign=sg, scene_id=scene_id) for sg in signs]
+          for path in paths:
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            log("Saving errors to: {}".format(path))
+          inout.save_errors_arrays(paths, arr["rec_im"], arr["rec_obj"], arr["rec_est"],
+                                   arr["rec_score"], arr["pair_off"], arr["pair_gt"], vals)
+          written.extend(paths)
+          continue
         errs = evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
                         models_info, sym_ids, planned=planned) if recs else []
         if errs is None or _dist()[0] != 0:  # rank 0 writes (also for a scene with no records)

@@ -6,6 +6,7 @@ read): pts, faces, normals, colors, per-vertex and per-face texture
 coordinates and the texture file name, as float64 arrays like the reference.
 """
 import json
+import os
 
 import numpy as np
 
@@ -245,6 +246,32 @@ def save_json_per_value(paths, records, n_values):
       lines.append("  " + "".join(p_ + _json_float(float(v[k])) for p_, v in zip(pre, vals)) + tail)
     with open(paths[k], "w") as f:
       f.write("[\n" + ",\n".join(lines) + ("\n]" if lines else "]"))
+
+
+def save_errors_arrays(paths, rec_im, rec_obj, rec_est, rec_score, pair_off, pair_gt, values):
+  """save_json(paths[k], [{"errors": {g: [values[q, k]] for the record's pairs q},
+  "est_id", "im_id", "obj_id", "score"} per record]) for every column k of
+  values (n_pairs x len(paths) float64), by the native writer
+  (include/bopx_score.h bopx_write_errors): the same bytes as save_json /
+  save_json_per_value of the record dicts (ids int64, scores float64, pairs in
+  ascending GT id order per record)."""
+  import ctypes as C
+  lib = _io_lib()
+  if not hasattr(lib, "_bopx_we"):
+    lib.bopx_write_errors.argtypes = [C.POINTER(C.c_char_p), C.c_int, C.c_int64] + \
+        [C.c_void_p] * 7
+    lib.bopx_write_errors.restype = C.c_int
+    lib._bopx_we = True
+  i64 = lambda a: np.ascontiguousarray(a, np.int64)
+  arrs = [i64(rec_im), i64(rec_obj), i64(rec_est), np.ascontiguousarray(rec_score, np.float64),
+          i64(pair_off), i64(pair_gt), np.ascontiguousarray(values, np.float64)]
+  n_rec = len(arrs[0])
+  if len(arrs[4]) != n_rec + 1 or arrs[6].shape != (len(arrs[5]), len(paths)):
+    raise ValueError("inconsistent errors arrays")
+  cp = (C.c_char_p * len(paths))(*[os.fsencode(x) for x in paths])
+  st = lib.bopx_write_errors(cp, len(paths), n_rec, *[a.ctypes.data for a in arrs])
+  if st != 0:
+    raise OSError("cannot write the errors files %s" % paths[0])
 
 
 def load_json(path, keys_to_int=False):

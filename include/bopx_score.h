@@ -73,6 +73,19 @@ typedef struct {
  * description of a non-OK status. */
 int bopx_score_folder(const bopx_score_args* a, char* msg, int msg_len);
 
+/* errors_{scene}.json files of one scene (scripts/eval_calc_errors.py:380-415,
+ * inout.save_json's one-record-per-line list): n_values files, file k holding
+ * for every record {"errors": {"<gt>": [values[p * n_values + k]], ...},
+ * "est_id", "im_id", "obj_id", "score"} with the record's GT pairs
+ * [pair_off[r], pair_off[r + 1]) in the given (ascending GT id) order — the
+ * per-tau VSD files (n_values = n_tau) or the one file of a point error
+ * (n_values = 1). Floats as float.__repr__, inf as Infinity. The same bytes
+ * as save_json of the record dicts. Returns 0, or BOPX_SCORE_READ when a file
+ * cannot be written. */
+int bopx_write_errors(const char* const* paths, int n_values, int64_t n_rec, const int64_t* rec_im,
+                      const int64_t* rec_obj, const int64_t* rec_est, const double* rec_score,
+                      const int64_t* pair_off, const int64_t* pair_gt, const double* values);
+
 /* float.__repr__ of v (JSON spelling for NaN / Infinity) into out (>= 32
  * bytes, NUL-terminated); returns the length. */
 int bopx_py_float_repr(double v, char* out);

@@ -181,3 +181,34 @@ def test_native_declines_what_python_handles(tmp_path):
   os.makedirs(os.path.dirname(path), exist_ok=True)
   inout.save_json(path, se)
   assert ecs.score_error_dir_native([p], folder) is None
+
+
+@pytest.mark.parametrize("n_values", [1, 10])
+def test_native_errors_writer_bytes(tmp_path, n_values):
+  """bopx_write_errors = save_json_per_value / save_json of the record dicts
+  (several GTs per record, none, fills 1.0 / inf, tiny and large values)."""
+  rnd = random.Random(n_values)
+  recs, im, ob, est, sc, off, gt, vals = [], [], [], [], [], [0], [], []
+  for _ in range(300):
+    gids = sorted(rnd.sample(range(15), rnd.choice([0, 1, 1, 2, 3, 11])))
+    errors = {g: [rnd.choice([rnd.random(), 1.0, 0.0, float("inf"), 1 / 3, 1e-20, 123456.75,
+                              rnd.random() * 1e17]) for _ in range(n_values)] for g in gids}
+    r = {"errors": errors, "est_id": rnd.randint(0, 5), "im_id": rnd.randint(0, 3000),
+         "obj_id": rnd.randint(1, 21), "score": rnd.choice([rnd.random(), 1.0, 0.5e-7])}
+    recs.append(r)
+    im.append(r["im_id"]), ob.append(r["obj_id"]), est.append(r["est_id"]), sc.append(r["score"])
+    gt += gids
+    vals += [errors[g] for g in gids]
+    off.append(len(gt))
+  want = [str(tmp_path / ("w%d.json" % k)) for k in range(n_values)]
+  got = [str(tmp_path / ("g%d.json" % k)) for k in range(n_values)]
+  if n_values == 1:
+    inout.save_json(want[0], recs)
+  else:
+    inout.save_json_per_value(want, recs, n_values)
+  inout.save_errors_arrays(got, im, ob, est, sc, off, gt,
+                           np.array(vals, np.float64).reshape(len(gt), n_values))
+  for w, g in zip(want, got):
+    assert _read(w) == _read(g)
+  inout.save_errors_arrays([got[0]], [], [], [], [], [0], [], np.zeros((0, 1)))
+  assert _read(got[0]) == "[\n]"
