@@ -54,6 +54,9 @@ def my_images(scene_gt, rank, world):
   return [im_ids[k] for k in part]
 
 
+_PINNED = [None, None]  # page-locked depth staging buffers (scene_stats)
+
+
 def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_batch=128,
                 rank=0, world=1):
   """Per image id: list of (row, masks or None) per GT instance, in GT order;
@@ -67,13 +70,20 @@ def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_ba
   dev = ev.device
   W, H = dp_split["im_size"]
 
-  def load(ims):
+  def load(ims, slot):
     # test depth in mm (float32 in place, calc_gt_info.py:99-100), decoded into
-    # one page-locked buffer while the previous batch runs
+    # a page-locked buffer while the previous batch runs; two buffers used in
+    # turn across batches and scenes (batch bi's upload has completed when
+    # bi + 2 is decoded: its rows were read back in between)
     paths = [_depth_path(dp_split, scene_id, im_id) for im_id in ims]
     scales = [scene_camera[im_id]["depth_scale"] for im_id in ims]
     if torch.cuda.is_available():
-      buf = torch.empty((len(ims), H, W), dtype=torch.float32, pin_memory=True)
+      need = len(ims) * H * W
+      if _PINNED[slot] is None or _PINNED[slot].numel() < need:
+        _PINNED[slot] = None
+        _PINNED[slot] = torch.empty(max(need, im_batch * H * W), dtype=torch.float32,
+                                    pin_memory=True)
+      buf = _PINNED[slot][:need].view(len(ims), H, W)
       try:
         inout.load_depths(paths, scales=scales, out=buf.numpy())
         return buf
@@ -84,11 +94,11 @@ def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_ba
   from concurrent.futures import ThreadPoolExecutor
   batches = [im_ids[i0:i0 + im_batch] for i0 in range(0, len(im_ids), im_batch)]
   with ThreadPoolExecutor(1) as ahead:
-    nxt = ahead.submit(load, batches[0]) if batches else None
+    nxt = ahead.submit(load, batches[0], 0) if batches else None
     for bi, ims in enumerate(batches):
       frames = nxt.result()
       if bi + 1 < len(batches):
-        nxt = ahead.submit(load, batches[bi + 1])
+        nxt = ahead.submit(load, batches[bi + 1], (bi + 1) & 1)
       cam, obj, pose, fidx, owner = [], [], [], [], []
       for k, im_id in enumerate(ims):
         K = scene_camera[im_id]["cam_K"]
