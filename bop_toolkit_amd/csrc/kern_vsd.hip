@@ -1679,7 +1679,6 @@ constexpr int kPairU = 2;
 template <int COST, int NT>
 __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {
   __shared__ double s_pX[kPairCols];
-  __shared__ float s_fA[kPairCols];  // filter: pX^2 per column
   __shared__ double s_thr[kMaxTaus];
   __shared__ uint32_t s_cnt[kPairWaves][2 + kMaxTaus];
   __shared__ double s_lin[kPairWaves][kMaxTaus];
@@ -1723,12 +1722,13 @@ __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {
   const int ux1 = ee ? Rg.z : (ge ? Re.z : max(Re.z, Rg.z));
   const int uy1 = ee ? Rg.w : (ge ? Re.w : max(Re.w, Rg.w));
   __syncthreads();
-  float thr32[NT];  // the filter's float32 thresholds (SGPRs), as in k_vsd
+  double thr[NT];  // wave-uniform (SGPRs)
 #pragma unroll
-  for (int k = 0; k < NT; ++k)
-    thr32[k] = __int_as_float(
-        __builtin_amdgcn_readfirstlane(__float_as_int(COST == 0 ? filt_thr(s_thr[k]) : 0.0f)));
-  const bool filter = COST == 0 && !divide;
+  for (int k = 0; k < NT; ++k) {
+    const double v = COST == 0 ? s_thr[k] : 0.0;
+    thr[k] = __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                              __builtin_amdgcn_readfirstlane(__double2loint(v)));
+  }
   uint32_t c_union = 0, c_inter = 0;
   uint32_t c_tau[(NT + 1) / 2];
   double lin[kMaxTaus];
@@ -1740,11 +1740,7 @@ __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {
   for (int cb = ux0; cb <= ux1; cb += kPairCols) {  // blocks of columns (wide images)
     const int cb1 = min(cb + kPairCols - 1, ux1);
     __syncthreads();  // the previous block's coefficients are consumed
-    for (int i = tid; i <= cb1 - cb; i += kPairThreads) {
-      const double pX = ((double)(cb + i) - cx) / fx;
-      s_pX[i] = pX;
-      if constexpr (COST == 0) s_fA[i] = filt_a(pX);
-    }
+    for (int i = tid; i <= cb1 - cb; i += kPairThreads) s_pX[i] = ((double)(cb + i) - cx) / fx;
     __syncthreads();
     for (int row = uy0 + wave; row <= uy1; row += kPairWaves) {
       const bool rin_e = row >= Re.y && row <= Re.w, rin_g = row >= Rg.y && row <= Rg.w;
@@ -1765,56 +1761,28 @@ __global__ __launch_bounds__(kPairThreads) void k_vsd_pair(PairArgs a) {
       // kPairU pixels per lane and step: every load of the step in flight
       // before the first use (the loop is latency-bound on the q / test-depth
       // reads otherwise); lane -> pixel map fixed (col = L + lane + 64 i)
-      const float fB = filt_b(pY);
-      // step cost: k_vsd's certified float32 filter with the exact fallback
-      auto step_exact = [&](uint32_t qe, uint32_t qg, float dtest, int col) {
-        bool vg, ve;
-        double dd;
-        vsd_exact_px(s_pX[col - cb], pY, qe, qg, dtest, a.dthr, vg, ve, dd);
-        c_union += (vg || ve);
-        if (vg && ve) {
-          ++c_inter;
-          if (divide) {
-            dd /= diam;
-            asm volatile("" : "+v"(dd));
-          }
-#pragma unroll
-          for (int k = 0; k < NT; ++k)
-            c_tau[k >> 1] += (uint32_t)(dd >= s_thr[k]) << (16 * (k & 1));
-        }
-      };
+      // the exact float64 sequence per pixel (vsd_exact_px; the float32 filter
+      // of k_vsd measured +3 % here: this loop waits on its loads, and the
+      // filter's registers cost a wave per SIMD, profiles/r04/ab_pair_filter.txt)
       auto vsd_pixel = [&](uint32_t qe, uint32_t qg, float dtest, int col) {
+        const double pX = s_pX[col - cb];
         if constexpr (COST == 0) {
-          if (!filter) {
-            step_exact(qe, qg, dtest, col);
-            return;
-          }
           bool vg, ve;
-          float lo, hi;
-          bool unc = vsd_filter_px(s_fA[col - cb] + fB, qe, qg, dtest, a.dthr, vg, ve, lo, hi);
-          const bool in = vg & ve;
-          c_union += vg | ve;
-          c_inter += in;
-#pragma unroll
-          for (int k = 0; k < NT; ++k) {
-            const bool ge_lo = in & (lo >= thr32[k]), ge_hi = in & (hi >= thr32[k]);
-            c_tau[k >> 1] += (uint32_t)ge_lo << (16 * (k & 1));
-            unc |= ge_lo != ge_hi;
-          }
-          if (__builtin_expect(__builtin_amdgcn_ballot_w64(unc) != 0, 0)) {
-            if (unc) {  // undo the float32 increments, redo the pixel exactly
-              c_union -= vg | ve;
-              c_inter -= in;
-#pragma unroll
-              for (int k = 0; k < NT; ++k)
-                c_tau[k >> 1] -= (uint32_t)(in & (lo >= thr32[k])) << (16 * (k & 1));
-              step_exact(qe, qg, dtest, col);
+          double dd;
+          vsd_exact_px(pX, pY, qe, qg, dtest, a.dthr, vg, ve, dd);
+          c_union += (vg || ve);
+          if (vg && ve) {
+            ++c_inter;
+            if (divide) {
+              dd /= diam;
+              asm volatile("" : "+v"(dd));
             }
+#pragma unroll
+            for (int k = 0; k < NT; ++k) c_tau[k >> 1] += (uint32_t)(dd >= thr[k]) << (16 * (k & 1));
           }
-        } else {  // tlinear: float64 sums, exact sequence
+        } else {  // tlinear: float64 sums
           const float de = qe ? rcp_rn(__uint_as_float(qe)) : 0.0f;
           const float dg = qg ? rcp_rn(__uint_as_float(qg)) : 0.0f;
-          const double pX = s_pX[col - cb];
           const double dist_t = dist_of(pX, pY, dtest);
           const double dist_g = qg ? dist_of(pX, pY, dg) : 0.0;
           const double dist_e = qe ? dist_of(pX, pY, de) : 0.0;
