@@ -462,8 +462,9 @@ extern "C" int bopx_score_folder(const bopx_score_args* a, char* msg_out, int ms
       for (int64_t g = g0; g < g1; ++g)
         if (std::find(objs.begin(), objs.end(), (int64_t)a->gt_obj[g]) == objs.end())
           objs.push_back(a->gt_obj[g]);
-      const auto it = by_im[fi].find(a->gt_im[g0 < g1 ? g0 : 0]);
-      if (g1 > g0 && it != by_im[fi].end()) {
+      // the image's id is its GT records' (an image without GT instances has no match)
+      const auto it = g1 > g0 ? by_im[fi].find(a->gt_im[g0]) : by_im[fi].end();
+      if (it != by_im[fi].end()) {
         for (const int64_t o : objs) {
           const int64_t s0 = (int64_t)G.order.size();
           for (const int64_t r : it->second)
