@@ -68,13 +68,14 @@ __device__ __forceinline__ void proj_mat(const double* K, const double* R, const
 #define BOPX_SYM_CHUNK 64
 #endif
 constexpr int kSymChunk = BOPX_SYM_CHUNK;  // <= 64: a unit's symmetries fit wave 0
-// Vertices staged in LDS per round (two barriers each). MSSD: large rounds keep
-// the barrier count low when a unit has few symmetries (S = 1: one d2 per
-// vertex); MSPD stages 5 values per vertex, where a smaller LDS footprint (more
-// resident blocks) measured faster (profiles/: 1024 -> 0.79 ms MSSD, 256 ->
-// 1.21 ms MSPD).
+// Vertices staged in LDS per round of the exhaustive path (two barriers each).
+// Round 4: single-symmetry units no longer stage (direct sweep), so the
+// exhaustive path only runs with pruning off or for sets > kPruneSpan, and the
+// staging's LDS mostly limited residency: MSSD 1,024 -> 256 is 30.5 -> 12 KB of
+// LDS, 5 -> 7 resident blocks per CU, -4 % (profiles/r04/ab_sym2.txt). MSPD
+// stages 5 values per vertex and was already at 256.
 #ifndef BOPX_SYM_STAGE_MSSD
-#define BOPX_SYM_STAGE_MSSD 1024
+#define BOPX_SYM_STAGE_MSSD 256
 #endif
 #ifndef BOPX_SYM_STAGE_MSPD
 #define BOPX_SYM_STAGE_MSPD 256
@@ -181,6 +182,19 @@ constexpr int kPruneSpan = 320;  // symmetry sets up to this size are pruned by 
 constexpr int kSweepU = BOPX_SYM_SWEEP_U;
 static_assert(kSweepU % 2 == 0, "pairs of maxima");
 
+// A wave-uniform double computed by VALU, moved to SGPRs (readfirstlane of
+// both halves): the sweeps' per-tuple / per-candidate matrices then take no
+// VGPRs (VALU reads one SGPR pair per instruction).
+__device__ __forceinline__ double uniform_d(double v) {
+  return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                          __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+template <int N>
+__device__ __forceinline__ void uniform_n(double* a) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) a[i] = uniform_d(a[i]);
+}
+
 // Make LDS written by other lanes of this wave visible (LDS is in order per wave).
 __device__ __forceinline__ void wave_lds_sync_pose() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -188,6 +202,9 @@ __device__ __forceinline__ void wave_lds_sync_pose() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// (round 4: forcing MSPD to 6 waves per SIMD, 77 VGPRs, was 26 % slower than
+// the free allocation's 89 / 5 waves; MSSD at 8 waves 22 % slower,
+// profiles/r04/ab_sym2.txt)
 template <int MODE>  // 0 = MSSD, 1 = MSPD
 __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __restrict__ objs,
                                                             const int32_t* __restrict__ slots,
@@ -241,6 +258,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
 #pragma unroll
       for (int i = 0; i < 9; ++i) K[i] = Km[9 * b + i];
       proj_mat(K, E, E + 9, Pe);
+      uniform_n<12>(Pe);  // per-tuple matrices in SGPRs (MSPD 125 -> 89 VGPRs)
     }
     auto d2v = [&](const double* A, int v) {  // vertex v from global memory
       const double x = px[v], y = py[v], z = pz[v];
@@ -341,6 +359,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
     {
       double A[12];
       sym_matrix<MODE>(E, K, G, syms + 12 * (int64_t)k0, A);
+      uniform_n<12>(A);
       double m = -INFINITY;
       // kSweepU vertices per thread and step, all their loads in flight
       for (int v0 = 0; v0 < nv; v0 += kSweepU * kPoseThreads) {
@@ -404,6 +423,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_sym_error(const ObjDesc* __res
       if (s_L[kk] <= best) {  // (else: the bound has passed the best by now)
         double A[12];
         sym_matrix<MODE>(E, K, G, syms + 12 * (int64_t)kk, A);
+        uniform_n<12>(A);
         double m = -INFINITY;
         uint64_t dead = 0;  // a lane's partial max exceeds a completed symmetry's max
         for (int v0 = 0; v0 < nv && dead == 0; v0 += 256) {
