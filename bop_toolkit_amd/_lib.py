@@ -77,6 +77,7 @@ SIGNATURES = {
     "bopx_depth_clear_dev": (_I, [_CTX, _P, _I64, _P]),
     "bopx_render_depth_batch_dev": (_I, [_CTX, _I64, _P, _P, _P, _P, _P, _I, _I, _P]),
     "bopx_depth_finish_dev": (_I, [_CTX, _P, _I64, _P]),
+    "bopx_png_decode_dev": (_I, [_CTX, _I64, _P, _P, _P, _I, _I, _P, _P, _I64, _P, _P, _P]),
 }
 
 _lib = None

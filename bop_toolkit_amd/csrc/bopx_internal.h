@@ -202,4 +202,11 @@ hipError_t launch_render_batch(const ObjDesc* objs, int max_nf, int64_t n, const
                                const double* pose, const int32_t* frame_idx, const double* cam,
                                float* frames, int W, int H, hipStream_t s);
 
+// kern_png.hip: 16-bit grayscale PNG decode (bopx_png_decode_dev).
+constexpr int kPngMaxWidth = 4096;  // k_png_unfilter's carry row (LDS)
+constexpr int kPngMaxRaw = 1 << 30; // inflated bytes per frame, H * (2W + 1)
+hipError_t launch_png_decode(int64_t n, const uint8_t* zdata, const int64_t* z_off,
+                             const int32_t* z_len, int H, int W, const float* scales, uint8_t* raw,
+                             int64_t raw_stride, float* frames, int32_t* status, hipStream_t s);
+
 }  // namespace bopx

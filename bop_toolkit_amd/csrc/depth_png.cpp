@@ -15,8 +15,10 @@
 #include "../../include/bopx_io.h"
 
 #include <dlfcn.h>
+#include <sys/stat.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -105,6 +107,7 @@ struct Worker {
   }
 
   int decode(const uint8_t* data, size_t n, int h, int w, float scale, float* dst);
+  int pack(const char* path, int64_t size, int h, int w, uint8_t* dst, int64_t* z_n);
 };
 
 inline uint32_t be32(const uint8_t* p) {
@@ -154,22 +157,23 @@ inline bool unfilter_row(int f, uint8_t* cur, const uint8_t* prev, int rb) {
   }
 }
 
-int Worker::decode(const uint8_t* data, size_t n, int h, int w, float scale, float* dst) {
+// Chunk walk (PNG spec 5.3-5.6, 11.2): signature, chunk lengths, CRCs, IHDR
+// (16-bit gray, no interlace, h x w), critical chunks, IEND. Calls
+// on_idat(body, len) for every IDAT payload, in order.
+template <class F>
+int walk_chunks(const Worker& wk, const uint8_t* data, size_t n, int h, int w, F&& on_idat) {
   static const uint8_t kSig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
   if (n < 8 || std::memcmp(data, kSig, 8) != 0) return BOPX_IO_CORRUPT;
   size_t pos = 8;
   bool have_hdr = false, have_end = false;
   uint32_t pw = 0, ph = 0;
-  const uint8_t* single = nullptr;  // the IDAT payload when there is one chunk
-  size_t single_n = 0;
   int n_idat = 0;
-  idat.clear();
   while (pos + 12 <= n) {
     const uint32_t len = be32(data + pos);
     if (len > n - pos - 12) return BOPX_IO_CORRUPT;
     const uint8_t* type = data + pos + 4;
     const uint8_t* body = data + pos + 8;
-    if (crc(type, (size_t)len + 4) != be32(body + len)) return BOPX_IO_CORRUPT;
+    if (wk.crc(type, (size_t)len + 4) != be32(body + len)) return BOPX_IO_CORRUPT;
     if (!have_hdr) {
       if (std::memcmp(type, "IHDR", 4) != 0 || len != 13) return BOPX_IO_CORRUPT;
       pw = be32(body);
@@ -180,10 +184,7 @@ int Worker::decode(const uint8_t* data, size_t n, int h, int w, float scale, flo
       if (pw == 0 || ph == 0) return BOPX_IO_CORRUPT;
       have_hdr = true;
     } else if (std::memcmp(type, "IDAT", 4) == 0) {
-      if (n_idat == 1) idat.assign(single, single + single_n);
-      if (n_idat >= 1) idat.insert(idat.end(), body, body + len);
-      single = body;
-      single_n = len;
+      on_idat(body, (size_t)len);
       ++n_idat;
     } else if (std::memcmp(type, "IEND", 4) == 0) {
       have_end = true;
@@ -195,6 +196,22 @@ int Worker::decode(const uint8_t* data, size_t n, int h, int w, float scale, flo
   }
   if (!have_hdr || !have_end || n_idat == 0) return BOPX_IO_CORRUPT;
   if ((int64_t)pw != w || (int64_t)ph != h) return BOPX_IO_SIZE;
+  return BOPX_IO_OK;
+}
+
+int Worker::decode(const uint8_t* data, size_t n, int h, int w, float scale, float* dst) {
+  const uint8_t* single = nullptr;  // the IDAT payload when there is one chunk
+  size_t single_n = 0;
+  int n_idat = 0;
+  idat.clear();
+  const int st = walk_chunks(*this, data, n, h, w, [&](const uint8_t* body, size_t len) {
+    if (n_idat == 1) idat.assign(single, single + single_n);
+    if (n_idat >= 1) idat.insert(idat.end(), body, body + len);
+    single = body;
+    single_n = len;
+    ++n_idat;
+  });
+  if (st != BOPX_IO_OK) return st;
 
   const size_t rb = 2 * (size_t)w;
   const size_t raw_n = (size_t)h * (rb + 1);
@@ -213,6 +230,26 @@ int Worker::decode(const uint8_t* data, size_t n, int h, int w, float scale, flo
     prev = cur;
   }
   return BOPX_IO_OK;
+}
+
+// Read a file of `size` bytes into dst, check its chunks as decode() does and
+// move the concatenated IDAT payload to dst[0, *z_n) (payloads only move
+// towards the start, over chunks already checked).
+int Worker::pack(const char* path, int64_t size, int h, int w, uint8_t* dst, int64_t* z_n) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return BOPX_IO_READ;
+  const bool ok = size >= 0 && std::fread(dst, 1, (size_t)size, f) == (size_t)size &&
+                  std::fgetc(f) == EOF;
+  std::fclose(f);
+  if (!ok) return BOPX_IO_READ;
+  size_t wp = 0;
+  const int st = walk_chunks(*this, dst, (size_t)size, h, w, [&](const uint8_t* body, size_t len) {
+    std::memmove(dst + wp, body, len);
+    wp += len;
+  });
+  *z_n = (int64_t)wp;
+  if (st == BOPX_IO_OK && wp > 0x7FFFFFFF) return BOPX_IO_UNSUPPORTED;
+  return st;
 }
 
 bool read_file(const char* path, std::vector<uint8_t>& buf) {
@@ -256,6 +293,52 @@ extern "C" int bopx_load_depth_pngs(const char* const* paths, int n, const int* 
       else
         st = wk.decode(wk.file.data(), wk.file.size(), h[k], w[k], scales ? scales[k] : 1.0f,
                        dst[k]);
+      status[k] = st;
+      if (st) failed.fetch_add(1);
+    }
+  };
+  if (nt == 1) {
+    run();
+  } else {
+    std::vector<std::thread> pool;
+    pool.reserve(nt - 1);
+    for (int i = 1; i < nt; ++i) pool.emplace_back(run);
+    run();
+    for (auto& t : pool) t.join();
+  }
+  return failed.load();
+}
+
+extern "C" int bopx_pack_depth_pngs(const char* const* paths, int n, const int* h, const int* w,
+                                    uint8_t* dst, int64_t cap, int64_t* z_off, int32_t* z_len,
+                                    int threads, int* status, int64_t* need) {
+  if (n <= 0 || !paths || !h || !w || !z_off || !z_len || !status) {
+    if (need) *need = 2048;
+    return n <= 0 ? 0 : -1;
+  }
+  std::vector<int64_t> size(n);
+  int64_t off = 0;
+  for (int k = 0; k < n; ++k) {
+    struct stat sb;
+    size[k] = stat(paths[k], &sb) == 0 ? (int64_t)sb.st_size : -1;
+    z_off[k] = off;
+    off += (std::max<int64_t>(size[k], 0) + 255) / 256 * 256;
+  }
+  if (need) *need = off + 2048;
+  if (!dst || cap < off + 2048) return -1;
+  int nt = threads > 0 ? threads : 16;
+  if (nt > n) nt = n;
+  std::atomic<int> next{0}, failed{0};
+  auto run = [&] {
+    Worker wk;
+    for (int k; (k = next.fetch_add(1)) < n;) {
+      int64_t zn = 0;
+      int st = BOPX_IO_SIZE;
+      if (size[k] < 0)
+        st = BOPX_IO_READ;
+      else if (h[k] > 0 && w[k] > 0)
+        st = wk.pack(paths[k], size[k], h[k], w[k], dst + z_off[k], &zn);
+      z_len[k] = st == BOPX_IO_OK ? (int32_t)zn : 0;
       status[k] = st;
       if (st) failed.fetch_add(1);
     }

@@ -1,0 +1,605 @@
+// kern_png.hip — 16-bit depth PNG decode on the GPU: inflate (RFC 1950/1951)
+// and row unfiltering (PNG spec 9.2-9.4) fused with the float32 depth_scale
+// multiply. The input side of the VSD pass: the reference reads every test
+// depth image with inout.load_depth (bop_toolkit_lib/inout.py:39-46, imageio)
+// and scales it in float32 (scripts/eval_calc_errors.py:242-243); the host
+// decoder (depth_png.cpp) does that in ~4 ms per 640x480 frame and core, most
+// of it in the inflate. Here the host only parses chunks (CRC, IHDR) and packs
+// the IDAT payloads; the frames are produced in HBM where k_vsd reads them.
+//
+// k_png_inflate: one wave per zlib stream. A deflate stream is sequential, so
+// the wave decodes it with wave-uniform control (bit buffer, positions and
+// table entries in SGPRs via readfirstlane) and uses its lanes where the work
+// is parallel: building the Huffman tables, back-reference copies (64 bytes a
+// round), flushing the output ring. Per wave LDS: a 1024-entry literal/length
+// table and a 256-entry distance table (16-bit entries: symbol | length << 9;
+// longer codes take a canonical slow path from SGPR limits), the symbols
+// sorted by code, the code lengths, and a 4 KB ring of the latest output.
+// The input is read 1 KB at a time into four VGPRs per lane (v_readlane per
+// 32 bits), so one load latency per KB of input is on the chain. The ring is flushed to HBM every
+// 1 KB; distances beyond the ring read the flushed bytes back from L2.
+//
+// k_png_unfilter: one wave per frame, 64 rows in flight (lane = row), lane k
+// working on pixel t - 2k at step t: the pixels a filter needs from the row
+// above (up, up-left) were produced by lane k - 1 two and three steps earlier
+// (a 4-pixel LDS ring per lane; the first row of a pass reads the last row of
+// the previous pass from a carry row). Every filter type (None, Sub, Up,
+// Average, Paeth) then runs at the same rate. The same pass computes the
+// zlib Adler-32 of the inflated bytes.
+//
+// Acceptance matches the host decoder's strictest back end: a stream is
+// accepted only if it is a valid zlib stream (header, complete Huffman codes
+// or a single length-1 code, distances inside the output, exact output size,
+// input not overrun, Adler-32), every filter byte is <= 4. Anything else gets
+// status BOPX_PNG_CORRUPT and the caller decodes that file on the host, which
+// reproduces the host path's own result or error.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bopx_internal.h"
+
+namespace bopx {
+namespace {
+
+constexpr int kInfWaves = 4;  // streams per workgroup, one wave each
+constexpr int kLitRoot = 10, kDistRoot = 8, kPreRoot = 7;
+constexpr int kRing = 4096, kRingMask = kRing - 1;
+constexpr int kFlush = 1024;       // bytes per ring flush (16 B per lane)
+constexpr int kVmcnt0 = 0x0F70;    // s_waitcnt vmcnt(0) (expcnt / lgkmcnt not waited)
+constexpr int kErr = 2;            // BOPX_PNG_CORRUPT
+constexpr uint16_t kNoCode = 0xFFFF;  // table entry: code longer than the root, or none
+
+__constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+struct InfLds {
+  uint16_t lit[1 << kLitRoot];    // also the code-length code's table (128 entries)
+  uint16_t dist[1 << kDistRoot];
+  uint16_t sorted[288 + 32];      // symbols by code: literal/length, then distance
+  uint8_t lens[288 + 32];         // code lengths: literal/length, then distance
+  alignas(16) uint8_t ring[kRing];  // the latest kRing output bytes
+};
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int popc_lt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+// Huffman table of the n code lengths lens[0..n) (LDS), with the per-length
+// quantities held lane-parallel (lane L = code length L, 1..15):
+//   lim  = (first code + count) << (15 - L): left-justified end of the length's
+//          codes (canonical codes of one length are consecutive, and the
+//          lengths' ranges follow each other), so a code's length is the
+//          smallest L with left-justified bits < lim[L];
+//   base = index in `sorted` of the length's first symbol minus its first code.
+// Writes tab (1 << ROOT entries: symbol << 4 | length, kNoCode = longer than
+// ROOT or no code; so a literal with a short code is an entry < 256 << 4) and sorted (symbols in code order). Returns 0, 1 for an empty code
+// (all lengths 0), or -1 for an over-subscribed code or an incomplete one
+// other than a single length-1 code (zlib inftrees.c; libdeflate accepts the
+// same codes).
+template <int ROOT>
+__device__ int build_code(const uint8_t* lens, int n, uint16_t* tab, uint16_t* sorted, int& lim,
+                          int& base, int lane) {
+  const bool len_lane = lane >= 1 && lane <= 15;
+  const int nch = (n + 63) >> 6;
+  int cnt = 0;
+  for (int ch = 0; ch < nch; ++ch) {
+    const int s = ch * 64 + lane;
+    const int l = s < n ? lens[s] : 0;
+#pragma unroll 1
+    for (int L = 1; L < 16; ++L) {
+      const int c = __popcll(__ballot(l == L));
+      if (lane == L) cnt += c;
+    }
+  }
+  // Kraft sum in units of 2^-15 and symbol offsets: inclusive scans over lanes
+  const int w = len_lane ? cnt << (15 - lane) : 0;
+  int ws = w, cs = len_lane ? cnt : 0;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    const int tw = __shfl_up(ws, o, 64), tc = __shfl_up(cs, o, 64);
+    if (lane >= o) {
+      ws += tw;
+      cs += tc;
+    }
+  }
+  const int kraft = __builtin_amdgcn_readlane(ws, 15), total = __builtin_amdgcn_readlane(cs, 15);
+  if (kraft > 32768) return -1;  // over-subscribed (every prefix then is too)
+  if (total == 0) return 1;
+  const uint64_t used = __ballot(len_lane && cnt > 0);
+  if (kraft < 32768 && used != 2) return -1;  // incomplete, not a single length-1 code
+  lim = ws;
+  const int first = len_lane ? (ws - w) >> (15 - lane) : 0;
+  const int offs = cs - cnt;
+  base = offs - first;
+  int run = offs;
+  for (int ch = 0; ch < nch; ++ch) {
+    const int s = ch * 64 + lane;
+    const int l = s < n ? lens[s] : 0;
+    int my = 0;
+#pragma unroll 1
+    for (int L = 1; L < 16; ++L) {
+      const uint64_t m = __ballot(l == L);
+      const int r = __builtin_amdgcn_readlane(run, L);
+      if (l == L) my = r + popc_lt(m);
+      if (lane == L) run += __popcll(m);
+    }
+    if (l) sorted[my] = (uint16_t)s;
+  }
+  wave_sync();
+#pragma unroll 1
+  for (int j = 0; j < (1 << ROOT) / 64; ++j) {
+    const int e = j * 64 + lane;
+    const int r15 = (int)(__builtin_bitreverse32((uint32_t)e) >> (32 - ROOT)) << (15 - ROOT);
+    int idx = -1, len = 0;
+#pragma unroll 1
+    for (int L = ROOT; L >= 1; --L) {  // the smallest length whose range holds the bits
+      const int lim_l = __builtin_amdgcn_readlane(lim, L);
+      const int base_l = __builtin_amdgcn_readlane(base, L);
+      if (r15 < lim_l) {
+        idx = base_l + (r15 >> (15 - L));
+        len = L;
+      }
+    }
+    tab[e] = idx >= 0 ? (uint16_t)(sorted[idx] << 4 | len) : kNoCode;
+  }
+  wave_sync();
+  return 0;
+}
+
+// A code longer than ROOT: the smallest length L > ROOT with the 15 bits
+// (first bit most significant) below lim[L]; -1 if none (no such code).
+template <int ROOT>
+__device__ __forceinline__ int slow_index(uint64_t bb, int lim, int base, int lane, int& L) {
+  const int r15 = (int)(__builtin_bitreverse32((uint32_t)bb) >> 17);
+  const uint64_t m = __ballot(lane > ROOT && lane <= 15 && r15 < lim);
+  if (m == 0) return -1;
+  L = __builtin_ctzll(m);
+  return __builtin_amdgcn_readlane(base, L) + (r15 >> (15 - L));
+}
+
+// Inflate one zlib stream (in, in_n bytes, 16-byte aligned, readable up to
+// in_n + 2048) into out (out_n bytes exactly; writable up to round_up(out_n,
+// 1024)). Returns 0 or kErr; *adler = the stream's Adler-32 field.
+__device__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t* __restrict__ out,
+                              int out_n, InfLds& S, int lane, uint32_t* adler) {
+  // input: 1 KB chunks, words [base, base + 256) with lane l holding words
+  // base + 4l .. 4l + 3, read with v_readlane. The next chunk is loaded when
+  // the current one is used up (one load latency per KB of input; a prefetch
+  // into a loop-carried register makes the compiler copy it, and the copy
+  // waits for the load anyway)
+  const uint4* in128 = reinterpret_cast<const uint4*>(in);
+  const int in_chunks = (in_n + 2048) >> 10;  // 1 KB chunks inside the readable bytes
+  uint4 c = in128[lane];
+  int base = 0;
+  int wi = 0;  // next input word
+  uint64_t bb = 0;
+  int nb = 0;
+  int p = 0, flushed = 0;
+
+  auto refill_word = [&]() -> bool {
+    if (wi - base >= 256) {
+      base += 256;
+      const int ch = min(base >> 8, max(in_chunks - 1, 0));
+      c = in128[ch * 64 + lane];
+    }
+    const int i = wi - base;
+    const int l = i >> 2;
+    uint32_t w;
+    switch (i & 3) {
+      case 0: w = (uint32_t)__builtin_amdgcn_readlane((int)c.x, l); break;
+      case 1: w = (uint32_t)__builtin_amdgcn_readlane((int)c.y, l); break;
+      case 2: w = (uint32_t)__builtin_amdgcn_readlane((int)c.z, l); break;
+      default: w = (uint32_t)__builtin_amdgcn_readlane((int)c.w, l); break;
+    }
+    bb |= (uint64_t)w << nb;
+    nb += 32;
+    ++wi;
+    return wi * 4 <= in_n + 8;
+  };
+  auto refill = [&]() -> bool { return nb > 32 || refill_word(); };
+  auto flush_block = [&](int f) {
+    wave_sync();
+    const uint4 v = reinterpret_cast<const uint4*>(S.ring)[((f & kRingMask) >> 4) + lane];
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);  // earlier flushes have landed: far reads below see them
+    reinterpret_cast<uint4*>(out)[(f >> 4) + lane] = v;
+  };
+  // one output byte (p - flushed < kFlush before and after)
+  auto put = [&](int byte) {
+    if (lane == 0) S.ring[p & kRingMask] = (uint8_t)byte;
+    ++p;
+    if ((p & (kFlush - 1)) == 0) {
+      flush_block(flushed);
+      flushed += kFlush;
+    }
+  };
+
+  refill_word();
+  {  // zlib header (RFC 1950 2.2): CM 8, CINFO <= 7, FCHECK, no preset dictionary
+    const int cmf = (int)(bb & 255), flg = (int)((bb >> 8) & 255);
+    if ((cmf & 15) != 8 || (cmf >> 4) > 7 || (cmf * 256 + flg) % 31 != 0 || (flg & 32)) return kErr;
+    bb >>= 16;
+    nb -= 16;
+  }
+  int lit_lim = 0, lit_base = 0, dist_lim = 0, dist_base = 0;  // lane L: length L (build_code)
+  bool final = false;
+  while (!final) {
+    if (!refill()) return kErr;
+    final = bb & 1;
+    const int type = (int)((bb >> 1) & 3);
+    bb >>= 3;
+    nb -= 3;
+    if (type == 0) {  // stored
+      const int drop = nb & 7;
+      bb >>= drop;
+      nb -= drop;
+      if (!refill()) return kErr;
+      const int len = (int)(bb & 0xFFFF), nlen = (int)((bb >> 16) & 0xFFFF);
+      bb >>= 32;
+      nb -= 32;
+      if (len != (~nlen & 0xFFFF) || len > out_n - p) return kErr;
+      for (int k = 0; k < len; ++k) {
+            if (nb < 8 && !refill_word()) return kErr;
+        put((int)(bb & 255));
+        bb >>= 8;
+        nb -= 8;
+      }
+      continue;
+    }
+    if (type == 3) return kErr;
+    int hlit = 288, hdist = 32;
+    if (type == 1) {  // fixed codes (RFC 1951 3.2.6)
+      for (int s = lane; s < 320; s += 64)
+        S.lens[s] = s >= 288 ? 5 : s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+      wave_sync();
+    } else {  // dynamic: the code-length code, then the two codes' lengths
+      if (!refill()) return kErr;
+      hlit = (int)(bb & 31) + 257;
+      hdist = (int)((bb >> 5) & 31) + 1;
+      const int hclen = (int)((bb >> 10) & 15) + 4;
+      bb >>= 14;
+      nb -= 14;
+      if (hlit > 286 || hdist > 30) return kErr;
+      if (lane < 19) S.lens[288 + lane] = 0;  // code-length code lengths live past the table
+      wave_sync();
+      for (int i = 0; i < hclen; ++i) {
+            if (!refill()) return kErr;
+        const int v = (int)(bb & 7);
+        bb >>= 3;
+        nb -= 3;
+        if (lane == 0) S.lens[288 + c_clorder[i]] = (uint8_t)v;
+      }
+      wave_sync();
+      int pre_lim, pre_base;
+      if (build_code<kPreRoot>(S.lens + 288, 19, S.lit, S.sorted, pre_lim, pre_base, lane) != 0)
+        return kErr;
+      const int ntot = hlit + hdist;
+      int k = 0, prev = -1;
+      while (k < ntot) {
+            if (!refill()) return kErr;
+        const int e = uni(S.lit[bb & ((1 << kPreRoot) - 1)]);
+        if (e == kNoCode) return kErr;  // every code-length code is <= 7 bits: no code
+        const int sym = e >> 4;
+        bb >>= e & 15;
+        nb -= e & 15;
+        int val, rep;
+        if (sym < 16) {
+          val = sym;
+          rep = 1;
+        } else if (sym == 16) {
+          if (prev < 0) return kErr;
+          val = prev;
+          rep = 3 + (int)(bb & 3);
+          bb >>= 2;
+          nb -= 2;
+        } else if (sym == 17) {
+          val = 0;
+          rep = 3 + (int)(bb & 7);
+          bb >>= 3;
+          nb -= 3;
+        } else {
+          val = 0;
+          rep = 11 + (int)(bb & 127);
+          bb >>= 7;
+          nb -= 7;
+        }
+        if (rep > ntot - k) return kErr;
+        // lengths k.. (literal/length codes at [0, hlit), distance codes at 288 +)
+        for (int j = lane; j < rep; j += 64) {
+          const int idx = k + j;
+          S.lens[idx < hlit ? idx : 288 + idx - hlit] = (uint8_t)val;
+        }
+        k += rep;
+        prev = val;
+      }
+      wave_sync();
+      if (uni(S.lens[256]) == 0) return kErr;  // no end-of-block code
+    }
+    if (build_code<kLitRoot>(S.lens, hlit, S.lit, S.sorted, lit_lim, lit_base, lane) != 0)
+      return kErr;
+    const int dst =
+        build_code<kDistRoot>(S.lens + 288, hdist, S.dist, S.sorted + 288, dist_lim, dist_base, lane);
+    if (dst < 0) return kErr;
+    const bool no_dist = dst == 1;
+
+    for (;;) {  // symbols of this block
+      // Literal runs, a bit-buffer window at a time: lane l looks the table up
+      // at bit offset l (one LDS gather), the chain of short literal codes
+      // through the window is followed with v_readlane (no LDS round trip per
+      // symbol), and the lanes on the chain store their bytes at once.
+        if (nb <= 32 && !refill_word()) return kErr;
+      if (nb <= 32 && !refill_word()) return kErr;  // nb in (32, 64]
+      const int lim = nb - kLitRoot;  // offsets whose lookup bits lie in the buffer
+      const int ev = S.lit[(uint32_t)(bb >> lane) & ((1 << kLitRoot) - 1)];
+      int e, off = 0;
+      uint64_t run = 0;  // bit l: a literal code starts at offset l
+      for (;;) {
+        e = __builtin_amdgcn_readlane(ev, off);
+        if (e >= 256 << 4) break;  // not a literal with a short code: below
+        run |= 1ull << off;
+        off += e & 15;
+        if (off > lim) {
+          e = -1;  // the window is used up
+          break;
+        }
+      }
+      if (run) {
+        const int nlit = __popcll(run);
+        if (nlit > out_n - p) return kErr;
+        bb = off < 64 ? bb >> off : 0;
+        nb -= off;
+        if ((run >> lane) & 1) S.ring[(p + popc_lt(run)) & kRingMask] = (uint8_t)(ev >> 4);
+        p += nlit;
+        while (p - flushed >= kFlush) {
+          flush_block(flushed);
+          flushed += kFlush;
+        }
+      }
+      if (e < 0) continue;
+      // e: the entry at the current position (a window leaves >= kLitRoot bits;
+      // a long code plus length extra bits need up to 20)
+      if (nb <= 32 && !refill_word()) return kErr;
+      int L = e & 15, sym = e >> 4;
+      if (e == kNoCode) {
+        const int idx = slow_index<kLitRoot>(bb, lit_lim, lit_base, lane, L);
+        if (idx < 0) return kErr;
+        sym = uni(S.sorted[idx]);
+      }
+      bb >>= L;
+      nb -= L;
+      if (sym < 256) {
+        if (p >= out_n) return kErr;
+        put(sym);
+        continue;
+      }
+      if (sym == 256) break;
+      if (sym > 285 || no_dist) return kErr;
+      // length: base and extra bits of RFC 1951 3.2.5 in closed form
+      const int ls = sym - 257;
+      const int lx = ls < 8 || ls == 28 ? 0 : (ls >> 2) - 1;
+      const int lbase = ls < 8 ? ls + 3 : ls == 28 ? 258 : ((4 + (ls & 3)) << lx) + 3;
+      const int len = lbase + (int)(bb & ((1u << lx) - 1));
+      bb >>= lx;
+      nb -= lx;
+      if (!refill()) return kErr;
+      e = uni(S.dist[bb & ((1 << kDistRoot) - 1)]);
+      L = e & 15;
+      int ds = e >> 4;
+      if (e == kNoCode) {
+        const int idx = slow_index<kDistRoot>(bb, dist_lim, dist_base, lane, L);
+        if (idx < 0) return kErr;
+        ds = uni(S.sorted[288 + idx]);
+      }
+      bb >>= L;
+      nb -= L;
+      if (ds >= 30) return kErr;
+      const int dx = ds < 4 ? 0 : (ds >> 1) - 1;
+      const int dbase = ds < 4 ? ds + 1 : ((2 + (ds & 1)) << dx) + 1;
+      const int dist = dbase + (int)(bb & ((1u << dx) - 1));
+      bb >>= dx;
+      nb -= dx;
+      if (dist > p || len > out_n - p) return kErr;
+      // copy: byte i of the match = out[p - dist + i % dist]; sources all lie
+      // before p, so each 64-byte round reads, then writes (the ring cannot
+      // wrap onto a later round's source: rounds span < 520 bytes).
+      const bool overlap = dist < len;
+      const float rd = 1.0f / (float)dist;
+      for (int r0 = 0; r0 < len; r0 += 64) {
+        const int i = r0 + lane;
+        int j = i;
+        if (overlap) {
+          j = i - (int)((float)i * rd) * dist;
+          if (j >= dist) j -= dist;
+          if (j < 0) j += dist;
+        }
+        const int q = p - dist + j;
+        int b = 0;
+        if (i < len) {
+          if (dist - j <= kRing) {
+            b = S.ring[q & kRingMask];
+          } else {  // flushed at least one flush before the last (see flush_block)
+            const uint32_t w = __hip_atomic_load(
+                reinterpret_cast<uint32_t*>(out + (q & ~3)), __ATOMIC_RELAXED,
+                __HIP_MEMORY_SCOPE_AGENT);
+            b = (int)((w >> ((q & 3) * 8)) & 255);
+          }
+        }
+        wave_sync();
+        if (i < len) S.ring[(p + i) & kRingMask] = (uint8_t)b;
+      }
+      p += len;
+      while (p - flushed >= kFlush) {
+        flush_block(flushed);
+        flushed += kFlush;
+      }
+    }
+  }
+  if (p != out_n) return kErr;
+  if (p > flushed) flush_block(flushed);  // the tail (the buffer is padded to 1 KB)
+  {
+    const int drop = nb & 7;
+    bb >>= drop;
+    nb -= drop;
+    if (!refill()) return kErr;
+    *adler = __builtin_bswap32((uint32_t)bb);
+    nb -= 32;
+    if (wi * 4 - nb / 8 > in_n) return kErr;  // the stream ran past its bytes
+  }
+  return 0;
+}
+
+__global__ __launch_bounds__(64 * kInfWaves) void k_png_inflate(
+    const uint8_t* __restrict__ zdata, const int64_t* __restrict__ z_off,
+    const int32_t* __restrict__ z_len, int64_t n, int out_n, int64_t raw_stride,
+    uint8_t* __restrict__ raw, int32_t* __restrict__ status) {
+  __shared__ InfLds s_inf[kInfWaves];
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  const int64_t k = (int64_t)blockIdx.x * kInfWaves + wave;
+  if (k >= n) return;
+  const int64_t off = z_off[k];
+  const int len = z_len[k];
+  uint32_t adler = 0;
+  int st = kErr;
+  if ((off & 255) == 0 && len >= 7)
+    st = inflate_stream(zdata + off, len, raw + k * raw_stride, out_n, s_inf[wave], lane, &adler);
+  if (lane == 0) {
+    status[2 * k] = st;
+    status[2 * k + 1] = (int32_t)adler;
+  }
+}
+
+constexpr int kUnfWaves = 4;
+
+__device__ __forceinline__ uint32_t unfilter_byte(int f, uint32_t x, uint32_t a, uint32_t b,
+                                                  uint32_t c) {
+  switch (f) {
+    case 1:
+      return (x + a) & 255;
+    case 2:
+      return (x + b) & 255;
+    case 3:
+      return (x + ((a + b) >> 1)) & 255;
+    case 4: {
+      const int pp = (int)a + (int)b - (int)c;
+      const int pa = abs(pp - (int)a), pb = abs(pp - (int)b), pc = abs(pp - (int)c);
+      return (x + (pa <= pb && pa <= pc ? a : pb <= pc ? b : c)) & 255;
+    }
+    default:
+      return x;
+  }
+}
+
+__global__ __launch_bounds__(64 * kUnfWaves) void k_png_unfilter(
+    const uint8_t* __restrict__ raw, int64_t raw_stride, int64_t n, int H, int W,
+    const float* __restrict__ scales, float* __restrict__ frames, int32_t* __restrict__ status) {
+  __shared__ uint16_t s_carry[kUnfWaves][kPngMaxWidth];
+  __shared__ uint16_t s_slot[kUnfWaves][64][4];
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  const int64_t k = (int64_t)blockIdx.x * kUnfWaves + wave;
+  if (k >= n) return;
+  if (uni(status[2 * k]) != 0) return;
+  const uint8_t* fr = raw + k * raw_stride;
+  const uint32_t* fr32 = reinterpret_cast<const uint32_t*>(fr);
+  const int64_t last_word = raw_stride / 4 - 5;  // a group's 5 words stay inside the frame
+  const int rowb = 2 * W + 1;
+  const uint64_t N = (uint64_t)H * rowb;
+  const float scale = scales ? scales[k] : 1.0f;
+  float* out = frames + k * (int64_t)H * W;
+  uint16_t* carry = s_carry[wave];
+  uint16_t(*slot)[4] = s_slot[wave];
+  uint64_t A = 0, B = 0;
+  bool bad = false;
+  for (int r0 = 0; r0 < H; r0 += 64) {
+    const int row = r0 + lane;
+    const bool act = row < H;
+    const int64_t rb = (int64_t)(act ? row : H - 1) * rowb;
+    int f = 0;
+    if (act) {
+      f = fr[rb];
+      A += f;
+      B += (N - rb) * f;
+      bad |= f > 4;
+    }
+    // lane k works on pixel c = t - 2k at step t; steps go in groups of 8, whose
+    // 16 bytes start at rb + 1 + 16 g - 4 k (the same alignment for every group)
+    const int64_t g0 = rb + 1 - 4 * lane;
+    const int sh = (int)(g0 & 3);
+    const int64_t d0 = (g0 - sh) >> 2;
+    auto load = [&](uint32_t(&w)[5], int g) {
+      const int64_t d = min(max(d0 + 4 * (int64_t)g, (int64_t)0), last_word);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) w[i] = fr32[d + i];
+    };
+    uint32_t left = 0, upl = 0;  // this row's previous pixel, the row above's previous pixel
+    auto step = [&](uint32_t x, int c) {
+      if (act && c >= 0 && c < W) {
+        const uint32_t xh = x & 255, xl = (x >> 8) & 255;
+        const uint32_t up = row == 0 ? 0u : lane == 0 ? carry[c] : slot[lane - 1][c & 3];
+        const uint32_t hi = unfilter_byte(f, xh, left >> 8, up >> 8, upl >> 8);
+        const uint32_t lo = unfilter_byte(f, xl, left & 255, up & 255, upl & 255);
+        const uint32_t px = hi << 8 | lo;
+        slot[lane][c & 3] = (uint16_t)px;
+        if (lane == 63) carry[c] = (uint16_t)px;
+        out[(int64_t)row * W + c] = (float)px * scale;
+        const uint64_t bi = (uint64_t)(rb + 1 + 2 * c);
+        A += xh + xl;
+        B += (N - bi) * xh + (N - bi - 1) * xl;
+        left = px;
+        upl = up;
+      }
+      wave_sync();
+    };
+    auto group = [&](const uint32_t(&w)[5], int g) {
+      uint32_t pl[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pl[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) step(pl[u >> 1] >> (16 * (u & 1)), 8 * g + u - 2 * lane);
+    };
+    const int nsteps = W + 2 * min(63, H - 1 - r0);
+    const int ng = (nsteps + 7) >> 3;
+    uint32_t wa[5], wb[5];  // groups in flight: even groups in wa, odd ones in wb
+    load(wa, 0);
+    for (int g = 0; g < ng; g += 2) {
+      load(wb, g + 1);
+      group(wa, g);
+      if (g + 1 >= ng) break;
+      load(wa, g + 2);
+      group(wb, g + 1);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    A += __shfl_xor((unsigned long long)A, o, 64);
+    B += __shfl_xor((unsigned long long)B, o, 64);
+  }
+  const uint32_t a = (uint32_t)((1 + A) % 65521u), b = (uint32_t)((N + B) % 65521u);
+  const bool ok = !__any(bad) && (b << 16 | a) == (uint32_t)status[2 * k + 1];
+  if (lane == 0 && !ok) status[2 * k] = kErr;
+}
+
+}  // namespace
+
+hipError_t launch_png_decode(int64_t n, const uint8_t* zdata, const int64_t* z_off,
+                             const int32_t* z_len, int H, int W, const float* scales, uint8_t* raw,
+                             int64_t raw_stride, float* frames, int32_t* status, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int out_n = H * (2 * W + 1);
+  const unsigned gi = (unsigned)((n + kInfWaves - 1) / kInfWaves);
+  hipLaunchKernelGGL(k_png_inflate, dim3(gi), dim3(64 * kInfWaves), 0, s, zdata, z_off, z_len, n,
+                     out_n, raw_stride, raw, status);
+  if (hipError_t e = hipGetLastError()) return e;
+  const unsigned gu = (unsigned)((n + kUnfWaves - 1) / kUnfWaves);
+  hipLaunchKernelGGL(k_png_unfilter, dim3(gu), dim3(64 * kUnfWaves), 0, s, raw, raw_stride, n, H,
+                     W, scales, frames, status);
+  return hipGetLastError();
+}
+
+}  // namespace bopx

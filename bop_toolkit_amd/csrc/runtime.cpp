@@ -1589,6 +1589,29 @@ int bopx_depth_finish_dev(bopx_ctx* c, float* frames, int64_t n_pixels, void* st
   return BOPX_OK;
 }
 
+int bopx_png_decode_dev(bopx_ctx* c, int64_t n, const uint8_t* zdata, const int64_t* z_off,
+                        const int32_t* z_len, int height, int width, const float* scales,
+                        uint8_t* raw, int64_t raw_stride, float* frames, int32_t* status,
+                        void* stream) {
+  if (!c) return BOPX_E_INVALID;
+  if (n < 0) return fail(c, BOPX_E_INVALID, "n = %lld", (long long)n);
+  if (width <= 0 || height <= 0 || width > bopx::kPngMaxWidth ||
+      (int64_t)height * (2 * (int64_t)width + 1) > bopx::kPngMaxRaw)
+    return fail(c, BOPX_E_INVALID, "png size %d x %d outside the device decoder's range", width,
+                height);
+  const int64_t need = ((int64_t)height * (2 * width + 1) + 64 + 1023) / 1024 * 1024;
+  if (raw_stride < need)
+    return fail(c, BOPX_E_INVALID, "raw_stride %lld < %lld", (long long)raw_stride,
+                (long long)need);
+  if (n == 0) return BOPX_OK;
+  if (!zdata || !z_off || !z_len || !raw || !frames || !status)
+    return fail(c, BOPX_E_INVALID, "null device pointer");
+  if (int r = set_dev(c)) return r;
+  HIPCHK(c, bopx::launch_png_decode(n, zdata, z_off, z_len, height, width, scales, raw, raw_stride,
+                                    frames, status, pick_stream(c, stream)));
+  return BOPX_OK;
+}
+
 int bopx_render_depth_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pose,
                                 const int32_t* frame_idx, const double* cam, float* frames,
                                 int width, int height, void* stream) {

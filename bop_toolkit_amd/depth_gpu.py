@@ -1,0 +1,140 @@
+"""Test depth decoded on the GPU: the device side of inout.load_depths.
+
+The reference reads every test depth image with inout.load_depth
+(bop_toolkit_lib/inout.py:39-46, imageio) and scales it in float32
+(scripts/eval_calc_errors.py:242-243, calc_gt_info.py:106-107). On the host
+that is ~4 ms per 640x480 frame and core, most of it zlib inflate. Here the
+host only reads the files and checks their chunks (libbopx_io.so
+bopx_pack_depth_pngs: signature, CRCs, IHDR), concatenating the IDAT payloads
+of a whole batch into one page-locked buffer; one DMA moves the compressed
+bytes, and kern_png.hip inflates, unfilters and scales them straight into the
+(n, H, W) float32 frames the VSD kernels read (bopx_png_decode_dev).
+
+Exactness: PNG is lossless and both decoders compute sample * (float)scale in
+float32, so the frames are bit-identical to the host decoder's
+(tests/test_gpu_png.py). Files the device decoder does not take — another
+format or size, or any defect it detects (it accepts only what the host's
+libdeflate accepts, with the same bytes) — are decoded by inout.load_depths on
+the host, which gives the host path's own result or raises its own error.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib, inout
+
+RAW_ALIGN = 1024      # bopx_png_decode_dev's raw_stride granule
+MAX_WIDTH = 4096      # kern_png.hip's carry row (bopx_internal.h kPngMaxWidth)
+MAX_RAW = 1 << 30     # inflated bytes per frame
+
+
+def enabled():
+  """BOPX_DEPTH_GPU=0 keeps the test depth on the host decoder."""
+  return os.environ.get("BOPX_DEPTH_GPU", "1") != "0"
+
+
+def _io():
+  L = inout._io_lib()
+  if not getattr(L, "_pack_sig", False):
+    L.bopx_pack_depth_pngs.argtypes = [
+        ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+        ctypes.POINTER(ctypes.c_int), ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
+    L.bopx_pack_depth_pngs.restype = ctypes.c_int
+    L._pack_sig = True
+  return L
+
+
+def pack(paths, H, W, buf_for, workers=None):
+  """Read and pack the files (bopx_pack_depth_pngs). buf_for(nbytes) returns
+  a writable uint8 buffer (numpy array or a page-locked torch tensor) of at
+  least nbytes. Returns (buf, need, z_off, z_len, status)."""
+  n = len(paths)
+  L = _io()
+  cp = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])
+  hh = (ctypes.c_int * n)(*([int(H)] * n))
+  ww = (ctypes.c_int * n)(*([int(W)] * n))
+  z_off = np.zeros(n, np.int64)
+  z_len = np.zeros(n, np.int32)
+  st = np.zeros(n, np.int32)
+  need = ctypes.c_int64(0)
+  L.bopx_pack_depth_pngs(cp, n, hh, ww, None, 0, z_off.ctypes.data, z_len.ctypes.data, 0,
+                         st.ctypes.data, ctypes.byref(need))
+  buf = buf_for(need.value)
+  addr = buf.ctypes.data if isinstance(buf, np.ndarray) else buf.data_ptr()
+  cap = buf.nbytes if isinstance(buf, np.ndarray) else buf.numel() * buf.element_size()
+  rc = L.bopx_pack_depth_pngs(cp, n, hh, ww, addr, cap, z_off.ctypes.data, z_len.ctypes.data,
+                              int(workers or min(16, os.cpu_count() or 1)), st.ctypes.data,
+                              ctypes.byref(need))
+  if rc < 0:
+    raise RuntimeError("bopx_pack_depth_pngs: %d bytes needed, %d given" % (need.value, cap))
+  return buf, need.value, z_off, z_len, st
+
+
+class DepthDecoder:
+  """Decodes batches of 16-bit depth PNGs of one size into device frames.
+
+  Owns a libbopx context (one per thread, include/bopx.h) and a page-locked
+  staging buffer reused across calls; load() enqueues on torch's current
+  stream of the device and returns once the frames are final (it reads the
+  per-frame status back)."""
+
+  def __init__(self, device=0):
+    self.ctx = _lib.Context(device)
+    self.device = int(device)
+    self._pinned = None
+
+  def _staging(self, torch, nbytes):
+    if self._pinned is None or self._pinned.numel() < nbytes:
+      self._pinned = None
+      self._pinned = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, pin_memory=True)
+    return self._pinned
+
+  def load(self, paths, scales, H, W, torch, workers=None):
+    """(n, H, W) float32 frames on the device: sample * (float32)scales[k]
+    (scales None: 1). Raises ValueError like inout.load_depths when a file
+    that the device decoder cannot take has another size."""
+    n = len(paths)
+    dev = torch.device("cuda", self.device)
+    frames = torch.empty((n, H, W), dtype=torch.float32, device=dev)
+    if n == 0:
+      return frames
+    if W > MAX_WIDTH or H * (2 * W + 1) > MAX_RAW:  # outside the kernel's range: host decoder
+      frames.copy_(torch.from_numpy(_host_frames(paths, scales, H, W, workers)))
+      self.last_host = n
+      return frames
+    sc = np.ones(n, np.float32) if scales is None else np.asarray(
+        [np.float32(float(s)) for s in scales], np.float32)
+    buf, need, z_off, z_len, st = pack(paths, H, W, lambda nb: self._staging(torch, nb), workers)
+    stream = torch.cuda.current_stream(dev)
+    z_d = buf[:need].to(dev, non_blocking=True)
+    off_d = torch.from_numpy(z_off).to(dev)
+    len_d = torch.from_numpy(z_len).to(dev)
+    sc_d = torch.from_numpy(sc).to(dev)
+    raw_stride = raw_stride_of(H, W)
+    raw = torch.empty(n * raw_stride, dtype=torch.uint8, device=dev)
+    status = torch.empty(2 * n, dtype=torch.int32, device=dev)
+    self.ctx.call("bopx_png_decode_dev", n, z_d.data_ptr(), off_d.data_ptr(), len_d.data_ptr(),
+                  int(H), int(W), sc_d.data_ptr(), raw.data_ptr(), raw_stride, frames.data_ptr(),
+                  status.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+    gst = status.view(n, 2)[:, 0].cpu().numpy()  # synchronises: staging reusable after this
+    del raw, z_d
+    host = np.nonzero((st != 0) | (gst != 0))[0]
+    if len(host):
+      arr = _host_frames([paths[k] for k in host], None if scales is None else
+                         [float(sc[k]) for k in host], H, W, workers)
+      frames[torch.from_numpy(host).to(dev)] = torch.from_numpy(arr).to(dev)
+    self.last_host = len(host)
+    return frames
+
+
+def raw_stride_of(H, W):
+  """bopx_png_decode_dev's per-frame scratch: the inflated rows + 64, in KiB."""
+  return (H * (2 * W + 1) + 64 + RAW_ALIGN - 1) // RAW_ALIGN * RAW_ALIGN
+
+
+def _host_frames(paths, scales, H, W, workers):
+  arr = np.empty((len(paths), H, W), np.float32)
+  inout.load_depths(paths, scales=scales, out=arr, workers=workers)
+  return arr

@@ -30,7 +30,7 @@ import time
 
 import numpy as np
 
-from . import dataset_params, inout, misc, pose_error
+from . import dataset_params, depth_gpu, inout, misc, pose_error
 
 DEFAULTS = {
     "n_top": 1,
@@ -372,6 +372,12 @@ def todo_images(recs, todo):
 _PINNED = [None]  # the page-locked staging buffer reused by load_scene_depths(reuse=True)
 
 
+def scene_depth_paths(dp_split, scene_camera, scene_id, ims):
+  """Depth PNG paths and depth_scale values of the images ims (:240-243)."""
+  paths = [dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id) for im_id in ims]
+  return paths, [scene_camera[im_id]["depth_scale"] for im_id in ims]
+
+
 def load_scene_depths(dp_split, scene_camera, scene_id, ims, torch=None, reuse=False):
   """Test depth of the images ims in mm, float32 (eval_calc_errors.py:240-243),
   decoded straight into one (n, H, W) array — page-locked when torch is given,
@@ -379,8 +385,7 @@ def load_scene_depths(dp_split, scene_camera, scene_id, ims, torch=None, reuse=F
   reuse: the frames land in one page-locked buffer kept across calls (grown
   when needed; page-locking a scene's 1-2 GB anew per scene is slow), valid
   until the next such call — the caller uploads and synchronises first."""
-  paths = [dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id) for im_id in ims]
-  scales = [scene_camera[im_id]["depth_scale"] for im_id in ims]  # float32 in place, :242-243
+  paths, scales = scene_depth_paths(dp_split, scene_camera, scene_id, ims)  # float32, :242-243
   W, H = dp_split["im_size"]
   if torch is not None and torch.cuda.is_available() and os.environ.get("BOPX_PIN", "1") != "0":
     if reuse:
@@ -723,6 +728,34 @@ def run(p, device=0):
     if et == "vsd" and ev is not None and torch.cuda.is_available():
       up = (torch.cuda.Stream(ev.device), torch.cuda.current_stream(ev.device))
 
+    decoder = [None]  # depth_gpu.DepthDecoder, used by the prefetch thread only
+
+    def prefetch_depths(ims, scene_id, scene_camera):
+      # the scene's test depth, resident on the device when the GPU runs the
+      # VSD: PNGs decoded by kern_png.hip (depth_gpu; BOPX_DEPTH_GPU=0: host
+      # decoder + one upload), on the upload stream
+      if up is not None and depth_gpu.enabled():
+        paths, scales = scene_depth_paths(dp_split, scene_camera, scene_id, ims)
+        W, H = dp_split["im_size"]
+        if decoder[0] is None:
+          decoder[0] = depth_gpu.DepthDecoder(ev.device.index or 0)
+        try:
+          with torch.cuda.stream(up[0]):
+            d = decoder[0].load(paths, scales, H, W, torch)
+          d.record_stream(up[1])  # freed behind the main stream's use
+          return d
+        except ValueError:
+          pass  # a frame of another size: the host path below
+      depths = load_scene_depths(dp_split, scene_camera, scene_id, ims, torch,
+                                 reuse=up is not None)
+      if up is not None and torch.is_tensor(depths):
+        with torch.cuda.stream(up[0]):
+          d = depths.to(ev.device, non_blocking=True)
+        up[0].synchronize()
+        d.record_stream(up[1])  # freed behind the main stream's use
+        depths = d
+      return depths
+
     def prepare(scene_id, scene_targets):
       # host side of one scene: annotations, records, gates, this rank's share
       # of the tuples and (VSD) its test-depth PNGs, decoded while the previous
@@ -738,29 +771,16 @@ def run(p, device=0):
         vals, todo = plan_arrays(p, arr, models_info)
         depths = None
         if et == "vsd" and len(todo):
-          depths = load_scene_depths(dp_split, scene_camera, scene_id,
-                                     np.unique(arr["rec_im"][arr["pair_ri"][todo]]).tolist(),
-                                     torch, reuse=up is not None)
-          if up is not None and torch.is_tensor(depths):
-            with torch.cuda.stream(up[0]):
-              d = depths.to(ev.device, non_blocking=True)
-            up[0].synchronize()
-            d.record_stream(up[1])
-            depths = d
+          depths = prefetch_depths(
+              np.unique(arr["rec_im"][arr["pair_ri"][todo]]).tolist(), scene_id, scene_camera)
         planned = ("arrays", arr, vals, todo, depths)
       elif recs:
         errs, todo, mine = plan_rank(p, recs, models_info, ev.objects if ev else None,
                                      scene_camera, dp_split["im_size"], rank, world)
         depths = None
         if et == "vsd" and len(mine):
-          depths = load_scene_depths(dp_split, scene_camera, scene_id,
-                                     todo_images(recs, [todo[i] for i in mine]), torch)
-          if up is not None and torch.is_tensor(depths):
-            with torch.cuda.stream(up[0]):
-              d = depths.to(ev.device, non_blocking=True)
-            up[0].synchronize()
-            d.record_stream(up[1])  # freed behind the main stream's use
-            depths = d
+          depths = prefetch_depths(todo_images(recs, [todo[i] for i in mine]), scene_id,
+                                   scene_camera)
         planned = (errs, todo, mine, depths)
       return scene_camera, recs, n_ests, planned
 

@@ -58,10 +58,12 @@ _PINNED = [None, None]  # page-locked depth staging buffers (scene_stats)
 
 
 def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_batch=128,
-                rank=0, world=1):
+                rank=0, world=1, frames_all=None):
   """Per image id: list of (row, masks or None) per GT instance, in GT order;
   images are evaluated in batches of im_batch frames. With world > 1 only this
-  rank's images (my_images) are evaluated."""
+  rank's images (my_images) are evaluated. frames_all: the test depth of those
+  images already on the device (SceneDepthPrefetch), else it is decoded here
+  on the host, a batch ahead."""
   from . import runtime
   scene_camera = inout.load_scene_camera(dp_split["scene_camera_tpath"].format(scene_id=scene_id))
   scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
@@ -93,12 +95,19 @@ def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_ba
 
   from concurrent.futures import ThreadPoolExecutor
   batches = [im_ids[i0:i0 + im_batch] for i0 in range(0, len(im_ids), im_batch)]
+  if frames_all is not None and len(frames_all) != len(im_ids):
+    raise ValueError("frames_all holds %d frames for %d images" % (len(frames_all), len(im_ids)))
   with ThreadPoolExecutor(1) as ahead:
-    nxt = ahead.submit(load, batches[0], 0) if batches else None
+    nxt = None
+    if batches and frames_all is None:
+      nxt = ahead.submit(load, batches[0], 0)
     for bi, ims in enumerate(batches):
-      frames = nxt.result()
-      if bi + 1 < len(batches):
-        nxt = ahead.submit(load, batches[bi + 1], (bi + 1) & 1)
+      if frames_all is not None:
+        frames = frames_all[bi * im_batch:bi * im_batch + len(ims)]
+      else:
+        frames = nxt.result()
+        if bi + 1 < len(batches):
+          nxt = ahead.submit(load, batches[bi + 1], (bi + 1) & 1)
       cam, obj, pose, fidx, owner = [], [], [], [], []
       for k, im_id in enumerate(ims):
         K = scene_camera[im_id]["cam_K"]
@@ -167,6 +176,56 @@ def _gather_info(torch, ev, stats, scene_gt, rank, world):
   return {im: [table[pos[im] + g] for g in range(len(scene_gt[im]))] for im in ims}
 
 
+class SceneDepthPrefetch:
+  """The next scene's test depth decoded on the GPU (depth_gpu, kern_png.hip)
+  while the current scene runs: the frames of this rank's images (my_images
+  order) land on the device from an upload stream. None for a scene (host
+  decoding in scene_stats) without a GPU, with BOPX_DEPTH_GPU=0, or when a
+  frame has another size."""
+
+  def __init__(self, ev, torch, dp_split, rank, world):
+    from concurrent.futures import ThreadPoolExecutor
+    from . import depth_gpu
+    self.on = torch.cuda.is_available() and depth_gpu.enabled()
+    self.ev, self.torch, self.dp_split, self.rank, self.world = ev, torch, dp_split, rank, world
+    self.pool = ThreadPoolExecutor(1)
+    self.dec = None
+    self.up = None
+    self.pending = {}
+
+  def _load(self, scene_id):
+    from . import depth_gpu
+    torch, dp = self.torch, self.dp_split
+    path_gt = dp["scene_gt_tpath"].format(scene_id=scene_id)
+    if not os.path.exists(path_gt):
+      return None
+    scene_camera = inout.load_scene_camera(dp["scene_camera_tpath"].format(scene_id=scene_id))
+    im_ids = my_images(inout.load_scene_gt(path_gt), self.rank, self.world)
+    W, H = dp["im_size"]
+    if self.dec is None:
+      self.dec = depth_gpu.DepthDecoder(self.ev.device.index or 0)
+      self.up = torch.cuda.Stream(self.ev.device)
+    try:
+      with torch.cuda.stream(self.up):
+        d = self.dec.load([_depth_path(dp, scene_id, i) for i in im_ids],
+                          [scene_camera[i]["depth_scale"] for i in im_ids], H, W, torch)
+    except ValueError:
+      return None
+    d.record_stream(torch.cuda.current_stream(self.ev.device))
+    return d
+
+  def submit(self, scene_id):
+    if self.on:
+      self.pending[scene_id] = self.pool.submit(self._load, scene_id)
+
+  def take(self, scene_id):
+    f = self.pending.pop(scene_id, None)
+    return f.result() if f is not None else None
+
+  def close(self):
+    self.pool.shutdown()
+
+
 def calc_gt_info(p):
   """scene_gt_info.json of every scene (calc_gt_info.py:75-175); returns paths.
   Under torchrun the images of each scene are split over the GPUs and rank 0
@@ -175,11 +234,17 @@ def calc_gt_info(p):
   rank, world, _ = shard.init_from_env()
   torch, ev, dp_split, scene_ids = _setup(p)
   written = []
-  for scene_id in scene_ids:
+  ahead = SceneDepthPrefetch(ev, torch, dp_split, rank, world)
+  if scene_ids:
+    ahead.submit(scene_ids[0])
+  for k, scene_id in enumerate(scene_ids):
     misc.log("Calculating GT info - dataset: {} ({}, {}), scene: {}".format(
         p["dataset"], p["dataset_split"], p["dataset_split_type"], scene_id))
+    frames = ahead.take(scene_id)
+    if k + 1 < len(scene_ids):
+      ahead.submit(scene_ids[k + 1])
     stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 3, False, rank=rank,
-                        world=world)
+                        world=world, frames_all=frames)
     scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
     rows = _gather_info(torch, ev, stats, scene_gt, rank, world)
     if rows is None:
@@ -189,6 +254,7 @@ def calc_gt_info(p):
     os.makedirs(os.path.dirname(path), exist_ok=True)
     inout.save_json(path, info)
     written.append(path)
+  ahead.close()
   return written
 
 
@@ -200,14 +266,20 @@ def calc_gt_masks(p):
   rank, world, _ = shard.init_from_env()
   torch, ev, dp_split, scene_ids = _setup(p)
   written = []
-  for scene_id in scene_ids:
+  ahead = SceneDepthPrefetch(ev, torch, dp_split, rank, world)
+  if scene_ids:
+    ahead.submit(scene_ids[0])
+  for k, scene_id in enumerate(scene_ids):
+    frames = ahead.take(scene_id)
+    if k + 1 < len(scene_ids):
+      ahead.submit(scene_ids[k + 1])
     if not os.path.exists(dp_split["scene_gt_tpath"].format(scene_id=scene_id)):
       print("Skip scene {} (GT file not found).".format(scene_id))
       continue
     misc.log("Calculating masks - dataset: {} ({}, {}), scene: {}".format(
         p["dataset"], p["dataset_split"], p["dataset_split_type"], scene_id))
     stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 1, True, rank=rank,
-                        world=world)
+                        world=world, frames_all=frames)
     for im_id, lst in stats.items():
       for gt_id, (_, mk) in enumerate(lst):
         for plane, key in enumerate(("mask_tpath", "mask_visib_tpath")):
@@ -215,6 +287,7 @@ def calc_gt_masks(p):
           os.makedirs(os.path.dirname(path), exist_ok=True)
           Image.fromarray(mk[plane]).save(path)
           written.append(path)
+  ahead.close()
   return written
 
 

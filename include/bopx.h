@@ -259,6 +259,30 @@ int bopx_render_depth_batch_dev(bopx_ctx* ctx, int64_t n, const int32_t* slots,
                                 void* stream);
 int bopx_depth_finish_dev(bopx_ctx* ctx, float* frames, int64_t n_pixels, void* stream);
 
+/* Depth PNG decode on the device (kern_png.hip), the GPU side of
+ * inout.load_depth (bop_toolkit_lib/inout.py:39-46) + the float32
+ * `depth *= depth_scale` (scripts/eval_calc_errors.py:242-243): n zlib
+ * streams — the concatenated IDAT payloads of n 16-bit grayscale,
+ * non-interlaced PNGs of height x width, as bopx_pack_depth_pngs
+ * (include/bopx_io.h) lays them out — are inflated, unfiltered and scaled
+ * into frames (n x height x width float32, dst = sample * scales[k], scales
+ * NULL = 1). Device pointers:
+ *   zdata   stream k at zdata + z_off[k] (a multiple of 256), z_len[k] bytes;
+ *           readable for 2048 bytes past every stream's end;
+ *   raw     scratch, n x raw_stride bytes, raw_stride >= round_up(height *
+ *           (2 width + 1) + 64, 1024);
+ *   status  2n int32: status[2k] = BOPX_PNG_OK or BOPX_PNG_CORRUPT (any
+ *           defect: zlib header, Huffman code, distance, size, Adler-32, filter
+ *           type); status[2k + 1] is scratch. A corrupt frame's pixels are
+ *           undefined; decode that file on the host (bopx_load_depth_pngs),
+ *           which reports the host path's own result or error.
+ * width <= 4096, height * (2 width + 1) <= 2^30. */
+enum { BOPX_PNG_OK = 0, BOPX_PNG_CORRUPT = 2 };
+int bopx_png_decode_dev(bopx_ctx* ctx, int64_t n, const uint8_t* zdata, const int64_t* z_off,
+                        const int32_t* z_len, int height, int width, const float* scales,
+                        uint8_t* raw, int64_t raw_stride, float* frames, int32_t* status,
+                        void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -44,6 +44,19 @@ int bopx_load_depth_pngs(const char* const* paths, int n, const int* h, const in
                          const float* scales, float* const* dst, int threads,
                          int* status);
 
+/* Host half of the GPU decoder (bopx_png_decode_dev, include/bopx.h): file k
+ * is read to dst + z_off[k], its chunks are checked as bopx_load_depth_pngs
+ * checks them (signature, lengths, CRCs, IHDR = h[k] x w[k], 16-bit gray, no
+ * interlace, critical chunks, IEND) and its IDAT payloads are concatenated in
+ * place: the zlib stream, z_len[k] bytes at dst + z_off[k]. z_off[k] = the
+ * sum of the sizes of files 0..k-1, each rounded up to 256 bytes; *need (may
+ * be NULL) = z_off[n] + 2048, the bytes dst must hold. With dst NULL or cap <
+ * *need nothing is read and -1 is returned; else the number of files with
+ * status[k] != BOPX_IO_OK (decode those with bopx_load_depth_pngs). */
+int bopx_pack_depth_pngs(const char* const* paths, int n, const int* h, const int* w,
+                         uint8_t* dst, int64_t cap, int64_t* z_off, int32_t* z_len,
+                         int threads, int* status, int64_t* need);
+
 /* 1 when the libdeflate inflater is in use, 0 for zlib. */
 int bopx_io_backend(void);
 

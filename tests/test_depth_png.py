@@ -52,9 +52,16 @@ def _filter_rows(img, filters):
   return b"".join(out)
 
 
-def write_png16(path, img, filters=(0, 1, 2, 3, 4), idat_split=None, extra=b""):
+def write_png16(path, img, filters=(0, 1, 2, 3, 4), idat_split=None, extra=b"", compress=None):
+  """compress: raw scanlines -> zlib stream (default zlib.compress level 6)."""
   h, w = img.shape
-  data = zlib.compress(_filter_rows(img, filters), 6)
+  raw = _filter_rows(img, filters)
+  data = compress(raw) if compress else zlib.compress(raw, 6)
+  png_from_zlib(path, w, h, data, idat_split, extra)
+
+
+def png_from_zlib(path, w, h, data, idat_split=None, extra=b""):
+  """A 16-bit gray PNG around the zlib stream `data` (valid chunk CRCs)."""
   parts = [data] if not idat_split else [data[i:i + idat_split]
                                          for i in range(0, len(data), idat_split)]
   ihdr = struct.pack(">IIBBBBB", w, h, 16, 0, 0, 0, 0)
@@ -185,3 +192,41 @@ def test_scale_is_one_float32_multiply(tmp_path):
     got = inout.load_depths([p], scales=[s])[0]
     want = img.astype(np.float32) * np.float32(s)
     assert got.dtype == np.float32 and np.array_equal(got, want), s
+
+
+def test_pack_for_the_device_decoder(tmp_path):
+  """bopx_pack_depth_pngs (the host half of the GPU decoder): offsets on
+  256-byte boundaries from the file sizes, each file's IDAT payloads
+  concatenated in place (= the zlib stream), the same per-file checks and
+  status codes as the host decoder."""
+  from bop_toolkit_amd import depth_gpu
+  rng = np.random.default_rng(21)
+  paths, streams = [], []
+  for i in range(5):
+    img = _depth(rng, 30, 40)
+    p = str(tmp_path / ("%d.png" % i))
+    z = zlib.compress(_filter_rows(img, (i % 5,)), i)
+    png_from_zlib(p, 40, 30, z, idat_split=[None, 7, 100, 1, 50][i],
+                  extra=_chunk(b"tEXt", b"k\x00v") if i == 2 else b"")
+    paths.append(p)
+    streams.append(z)
+  Image.fromarray(_depth(rng, 30, 40)).save(str(tmp_path / "pil.png"))
+  paths.append(str(tmp_path / "pil.png"))
+  raw = bytearray(open(paths[0], "rb").read())
+  raw[raw.index(b"IDAT") + 9] ^= 1  # CRC mismatch
+  open(str(tmp_path / "crc.png"), "wb").write(bytes(raw))
+  Image.fromarray((_depth(rng, 30, 40) % 256).astype(np.uint8)).save(str(tmp_path / "g8.png"))
+  write_png16(str(tmp_path / "size.png"), _depth(rng, 31, 40))
+  paths += [str(tmp_path / n) for n in ("crc.png", "g8.png", "size.png", "missing.png")]
+  buf, need, off, ln, st = depth_gpu.pack(paths, 30, 40, lambda nb: np.zeros(nb, np.uint8))
+  sizes = [os.path.getsize(p) if os.path.exists(p) else 0 for p in paths]
+  want_off = np.concatenate([[0], np.cumsum([(s + 255) // 256 * 256 for s in sizes])])
+  assert list(off) == list(want_off[:-1]) and need == want_off[-1] + 2048
+  assert list(st) == [0] * 6 + [2, 1, 3, 4]
+  for k in range(5):
+    assert bytes(buf[off[k]:off[k] + ln[k]]) == streams[k]
+  pil = zlib.decompress(bytes(buf[off[5]:off[5] + ln[5]]))
+  assert len(pil) == 30 * 81
+  # too small a buffer: nothing read
+  with pytest.raises(RuntimeError):
+    depth_gpu.pack(paths, 30, 40, lambda nb: np.zeros(nb - 1, np.uint8))

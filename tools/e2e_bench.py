@@ -149,6 +149,9 @@ def main():
   ap.add_argument("--profile", action="store_true")
   ap.add_argument("--instances", type=int, default=1,
                   help="instances (and estimates) per object and image; > 1: multi-instance")
+  ap.add_argument("--ab-depth", action="store_true",
+                  help="evaluate twice: test depth decoded on the GPU, then on the host "
+                       "(BOPX_DEPTH_GPU=0); both timings and identical scores reported")
   a = ap.parse_args()
   import torch
   if os.path.exists(a.root):
@@ -191,7 +194,8 @@ def main():
   ece.run = run_wrap
   ecs.score_error_dir = timed("scores", score0)
   # host steps of the error passes (the prepare thread's included)
-  from bop_toolkit_amd import inout
+  from bop_toolkit_amd import depth_gpu, inout
+  depth_gpu.DepthDecoder.load = timed("host:gpu_depth_load", depth_gpu.DepthDecoder.load)
   for mod, name in ((ece, "scene_records"), (ece, "plan_rank"), (ece, "load_scene_depths"),
                     (ece, "evaluate_batch"), (ece, "evaluate"), (ece, "Models"), (inout, "save_json"), (inout, "save_json_per_value")):
     setattr(mod, name, timed("host:" + name, getattr(mod, name)))
@@ -217,6 +221,30 @@ def main():
     with open(os.path.join(REPO, "gpurun_out", "e2e_profile.txt"), "w") as f:
       f.write(s.getvalue())
   scores = final[os.path.splitext(result)[0]]
+  ab = None
+  if a.ab_depth:  # warm runs (annotation caches filled by the first): host decoder, then GPU
+    first_phases, first_err = dict(phases), dict(err_t)
+    ab = {}
+    for name, env in (("host_decode_warm", "0"), ("gpu_decode_warm", "1")):
+      for k in list(phases):
+        if k.startswith("host:"):
+          phases[k] = 0.0
+      err_t.clear()
+      os.environ["BOPX_DEPTH_GPU"] = env
+      t0 = time.perf_counter()
+      fin = eval_bop19_pose.evaluate(p)
+      t_run = time.perf_counter() - t0
+      ab[name] = {"eval_bop19_s": round(t_run, 2),
+                  "errors_s": {k: round(v, 2) for k, v in err_t.items()},
+                  "host_s": {k[5:]: round(v, 3) for k, v in phases.items()
+                             if k.startswith("host:") and v},
+                  "eval_tuples_per_s": n / t_run,
+                  "identical_scores": fin[os.path.splitext(result)[0]] == scores}
+    os.environ.pop("BOPX_DEPTH_GPU")
+    phases.clear()
+    phases.update(first_phases)
+    err_t.clear()
+    err_t.update(first_err)
   print(json.dumps({
       "what": "end-to-end BOP19 evaluation (calc_gt_info + eval_bop19_pose), synthetic YCB-V "
               "layout, 21 objs V=5002, 640x480 PNG depth, 1 GPU",
@@ -227,6 +255,7 @@ def main():
       "scores_s": round(phases.get("scores", 0.0), 2), "eval_bop19_s": round(t_eval, 2),
       "host_s": {k[5:]: round(v, 3) for k, v in phases.items() if k.startswith("host:")},
       "eval_tuples_per_s": n / t_eval,
+      "depth_decoder": "gpu" if depth_gpu.enabled() else "host", "ab_depth": ab,
       "ar": {k: round(float(v), 4) for k, v in scores.items()}}))
 
 

@@ -14,10 +14,11 @@ for env in "BOPX_VSD_CULL=0" "BOPX_VSD_CULL=3" "BOPX_VSD_CULL=1" "BOPX_VSD_QORDE
       || { echo "$env FAILED"; tail -20 gpurun_out/sw.log; exit 1; }
   echo "$env: $(tail -1 gpurun_out/sw.log)"
 done
-# host-side switches of the callers (round 4): the record-dict error path and
-# the Python scorer, against the reference scripts' files
-for env in "BOPX_ERRORS_ARRAYS=0" "BOPX_SCORE_NATIVE=0"; do
+# host-side switches of the callers (round 4): the record-dict error path, the
+# Python scorer and the host depth decoder, against the reference scripts' files
+for env in "BOPX_ERRORS_ARRAYS=0" "BOPX_SCORE_NATIVE=0" "BOPX_DEPTH_GPU=0"; do
   env $env timeout -k 10 300 python -u -m pytest tests/test_e2e_errors.py tests/test_scores.py \
+      tests/test_gt_side.py \
       -m gpu -q -x --timeout 240 --timeout-method thread > gpurun_out/sw.log 2>&1 \
       || { echo "$env FAILED"; tail -20 gpurun_out/sw.log; exit 1; }
   echo "$env: $(tail -1 gpurun_out/sw.log)"
