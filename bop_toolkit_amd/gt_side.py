@@ -235,26 +235,28 @@ def calc_gt_info(p):
   torch, ev, dp_split, scene_ids = _setup(p)
   written = []
   ahead = SceneDepthPrefetch(ev, torch, dp_split, rank, world)
-  if scene_ids:
-    ahead.submit(scene_ids[0])
-  for k, scene_id in enumerate(scene_ids):
-    misc.log("Calculating GT info - dataset: {} ({}, {}), scene: {}".format(
-        p["dataset"], p["dataset_split"], p["dataset_split_type"], scene_id))
-    frames = ahead.take(scene_id)
-    if k + 1 < len(scene_ids):
-      ahead.submit(scene_ids[k + 1])
-    stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 3, False, rank=rank,
-                        world=world, frames_all=frames)
-    scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
-    rows = _gather_info(torch, ev, stats, scene_gt, rank, world)
-    if rows is None:
-      continue
-    info = {im_id: [info_from_row(r) for r in lst] for im_id, lst in rows.items()}
-    path = dp_split["scene_gt_info_tpath"].format(scene_id=scene_id)
-    os.makedirs(os.path.dirname(path), exist_ok=True)
-    inout.save_json(path, info)
-    written.append(path)
-  ahead.close()
+  try:
+    if scene_ids:
+      ahead.submit(scene_ids[0])
+    for k, scene_id in enumerate(scene_ids):
+      misc.log("Calculating GT info - dataset: {} ({}, {}), scene: {}".format(
+          p["dataset"], p["dataset_split"], p["dataset_split_type"], scene_id))
+      frames = ahead.take(scene_id)
+      if k + 1 < len(scene_ids):
+        ahead.submit(scene_ids[k + 1])
+      stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 3, False, rank=rank,
+                          world=world, frames_all=frames)
+      scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+      rows = _gather_info(torch, ev, stats, scene_gt, rank, world)
+      if rows is None:
+        continue
+      info = {im_id: [info_from_row(r) for r in lst] for im_id, lst in rows.items()}
+      path = dp_split["scene_gt_info_tpath"].format(scene_id=scene_id)
+      os.makedirs(os.path.dirname(path), exist_ok=True)
+      inout.save_json(path, info)
+      written.append(path)
+  finally:
+    ahead.close()
   return written
 
 
@@ -267,27 +269,29 @@ def calc_gt_masks(p):
   torch, ev, dp_split, scene_ids = _setup(p)
   written = []
   ahead = SceneDepthPrefetch(ev, torch, dp_split, rank, world)
-  if scene_ids:
-    ahead.submit(scene_ids[0])
-  for k, scene_id in enumerate(scene_ids):
-    frames = ahead.take(scene_id)
-    if k + 1 < len(scene_ids):
-      ahead.submit(scene_ids[k + 1])
-    if not os.path.exists(dp_split["scene_gt_tpath"].format(scene_id=scene_id)):
-      print("Skip scene {} (GT file not found).".format(scene_id))
-      continue
-    misc.log("Calculating masks - dataset: {} ({}, {}), scene: {}".format(
-        p["dataset"], p["dataset_split"], p["dataset_split_type"], scene_id))
-    stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 1, True, rank=rank,
-                        world=world, frames_all=frames)
-    for im_id, lst in stats.items():
-      for gt_id, (_, mk) in enumerate(lst):
-        for plane, key in enumerate(("mask_tpath", "mask_visib_tpath")):
-          path = dp_split[key].format(scene_id=scene_id, im_id=im_id, gt_id=gt_id)
-          os.makedirs(os.path.dirname(path), exist_ok=True)
-          Image.fromarray(mk[plane]).save(path)
-          written.append(path)
-  ahead.close()
+  try:
+    if scene_ids:
+      ahead.submit(scene_ids[0])
+    for k, scene_id in enumerate(scene_ids):
+      frames = ahead.take(scene_id)
+      if k + 1 < len(scene_ids):
+        ahead.submit(scene_ids[k + 1])
+      if not os.path.exists(dp_split["scene_gt_tpath"].format(scene_id=scene_id)):
+        print("Skip scene {} (GT file not found).".format(scene_id))
+        continue
+      misc.log("Calculating masks - dataset: {} ({}, {}), scene: {}".format(
+          p["dataset"], p["dataset_split"], p["dataset_split_type"], scene_id))
+      stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 1, True, rank=rank,
+                          world=world, frames_all=frames)
+      for im_id, lst in stats.items():
+        for gt_id, (_, mk) in enumerate(lst):
+          for plane, key in enumerate(("mask_tpath", "mask_visib_tpath")):
+            path = dp_split[key].format(scene_id=scene_id, im_id=im_id, gt_id=gt_id)
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            Image.fromarray(mk[plane]).save(path)
+            written.append(path)
+  finally:
+    ahead.close()
   return written
 
 
