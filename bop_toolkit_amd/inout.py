@@ -375,24 +375,65 @@ def load_scene_gt(path):
 
 def load_bop_results(path, version="bop19"):
   """BOP19 CSV results: scene_id,im_id,obj_id,score,R,t,time; a first line
-  containing the header is skipped (inout.py:221-261)."""
+  containing the header is skipped (inout.py:221-261). Files in the plain
+  form every writer produces are read natively (bopx_read_bop_results: the
+  same int() / float() values; R and t are views into one (n, 3, 3) / (n, 3,
+  1) array); anything else by the line reader below, which raises the
+  reference's error for the first bad line."""
   if version != "bop19":
     raise ValueError("Unknown version of BOP results.")
+  res = _bop_results_native(path)
+  if res is not None:
+    return res
   header = "scene_id,im_id,obj_id,score,R,t,time"
-  results = []
   with open(path, "r") as f:
-    for line_no, line in enumerate(f, 1):
-      if line_no == 1 and header in line:
-        continue
-      e = line.split(",")
-      if len(e) != 7:
-        raise ValueError("A line does not have 7 comma-sep. elements: {}".format(line))
-      results.append({
-          "scene_id": int(e[0]), "im_id": int(e[1]), "obj_id": int(e[2]),
-          "score": float(e[3]),
-          "R": np.array([float(x) for x in e[4].split()], np.float64).reshape((3, 3)),
-          "t": np.array([float(x) for x in e[5].split()], np.float64).reshape((3, 1)),
-          "time": float(e[6])})
+    lines = f.readlines()
+  return _bop_results_lines(lines[1:] if lines and header in lines[0] else lines)
+
+
+def _bop_results_native(path):
+  """The rows of a results file through libbopx_io.so, or None when the file
+  is not in the native reader's strict form (or cannot be read)."""
+  import ctypes
+  L = _io_lib()
+  if not getattr(L, "_res_sig", False):
+    L.bopx_read_bop_results.argtypes = [ctypes.c_char_p, ctypes.c_int64] + [ctypes.c_void_p] * 5 + [
+        ctypes.POINTER(ctypes.c_int64)]
+    L.bopx_read_bop_results.restype = ctypes.c_int64
+    L._res_sig = True
+  p = os.fsencode(path)
+  need = ctypes.c_int64(0)
+  rc = L.bopx_read_bop_results(p, 0, None, None, None, None, None, ctypes.byref(need))
+  if rc == 0:
+    return []
+  if rc != -3:  # BOPX_RES_CAP: n lines to convert; READ / OTHER: the Python reader
+    return None
+  n = need.value
+  ids = np.empty((n, 3), np.int64)
+  score, tm = np.empty(n), np.empty(n)
+  R, t = np.empty((n, 3, 3)), np.empty((n, 3, 1))
+  rc = L.bopx_read_bop_results(p, n, ids.ctypes.data, score.ctypes.data, R.ctypes.data,
+                               t.ctypes.data, tm.ctypes.data, ctypes.byref(need))
+  if rc != n:
+    return None
+  sc, im, ob = ids.T.tolist()
+  score, tm = score.tolist(), tm.tolist()
+  return [{"scene_id": sc[k], "im_id": im[k], "obj_id": ob[k], "score": score[k], "R": R[k],
+           "t": t[k], "time": tm[k]} for k in range(n)]
+
+
+def _bop_results_lines(body):
+  results = []
+  for line in body:
+    e = line.split(",")
+    if len(e) != 7:
+      raise ValueError("A line does not have 7 comma-sep. elements: {}".format(line))
+    results.append({
+        "scene_id": int(e[0]), "im_id": int(e[1]), "obj_id": int(e[2]),
+        "score": float(e[3]),
+        "R": np.array([float(x) for x in e[4].split()], np.float64).reshape((3, 3)),
+        "t": np.array([float(x) for x in e[5].split()], np.float64).reshape((3, 1)),
+        "time": float(e[6])})
   return results
 
 

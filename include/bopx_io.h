@@ -57,6 +57,18 @@ int bopx_pack_depth_pngs(const char* const* paths, int n, const int* h, const in
                          uint8_t* dst, int64_t cap, int64_t* z_off, int32_t* z_len,
                          int threads, int* status, int64_t* need);
 
+/* BOP19 results CSV (bop_toolkit_lib/inout.py:221-261: an optional header line
+ * "scene_id,im_id,obj_id,score,R,t,time", then one estimate per line) into
+ * arrays: ids n x 3 (scene, im, obj), score n, R n x 9 (row-major), t n x 3,
+ * time n; numbers converted as Python's int() / float() convert them. Only a
+ * strict form is read ('\n' line ends, ASCII, 7 fields, blanks ' ' / '\t',
+ * decimal numbers, 9 + 3 pose numbers); otherwise BOPX_RES_OTHER and the
+ * caller uses the Python reader. *need = n; with cap < n nothing is converted
+ * (BOPX_RES_CAP). Returns n or a negative BOPX_RES_* code. */
+enum { BOPX_RES_READ = -1, BOPX_RES_OTHER = -2, BOPX_RES_CAP = -3 };
+int64_t bopx_read_bop_results(const char* path, int64_t cap, int64_t* ids, double* score,
+                              double* R, double* t, double* time, int64_t* need);
+
 /* 1 when the libdeflate inflater is in use, 0 for zlib. */
 int bopx_io_backend(void);
 

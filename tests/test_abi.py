@@ -60,7 +60,7 @@ def test_io_library_exports_every_declared_symbol():
   src = re.sub(r"/\*.*?\*/", "", open(IO_HEADER).read(), flags=re.S)
   syms = sorted(set(re.findall(r"\b(bopx_[a-z0-9_]+)\s*\(", src)))
   assert syms == ["bopx_decode_depth_png", "bopx_io_backend", "bopx_load_depth_pngs",
-                  "bopx_pack_depth_pngs"]
+                  "bopx_pack_depth_pngs", "bopx_read_bop_results"]
   assert os.path.exists(IO_LIB), "libbopx_io.so not built (make -C bop_toolkit_amd/csrc)"
   L = ctypes.CDLL(IO_LIB)
   assert not [s for s in syms if not hasattr(L, s)]

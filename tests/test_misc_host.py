@@ -88,3 +88,78 @@ def test_vsd_result_types():
   assert e == [0.25, 1.0] and all(type(x) is np.float64 for x in e)
   e = _vsd_result(np.array([1.0, 1.0, 1.0]), 0.0)
   assert e == [1.0] * 3 and all(type(x) is float for x in e)
+
+
+def _same_results(a, b):
+  assert len(a) == len(b)
+  for x, y in zip(a, b):
+    assert x.keys() == y.keys()
+    for key in ("scene_id", "im_id", "obj_id", "score", "time"):
+      assert type(x[key]) is type(y[key])
+      assert x[key] == y[key] or (x[key] != x[key] and y[key] != y[key])  # nan == nan
+    for key, shape in (("R", (3, 3)), ("t", (3, 1))):
+      assert x[key].shape == y[key].shape == shape and x[key].dtype == y[key].dtype
+      assert np.array_equal(x[key].view(np.uint64), y[key].view(np.uint64))
+
+
+def test_bop_results_native_reader_matches_the_line_reader(tmp_path):
+  """inout.load_bop_results (native bopx_read_bop_results for the plain form)
+  returns the reference reader's values bit for bit (inout.py:221-261: int()
+  of the ids, float() of every number), and files outside the plain form go
+  through the line reader: the same values, or the reference's error for the
+  first bad line."""
+  from bop_toolkit_amd import inout
+  rng = np.random.default_rng(3)
+  nums = ["%.17g", "%.8f", "%.3e", "%r"]
+  special = ["5.", ".5", "+1.25", "-0.0", "0", "1e400", "-1e400", "1e-400", "4.9e-324",
+             "0.1234567890123456789012345", "123456789012345678901234567890", "1E5", "-7E-3"]
+  header = "scene_id,im_id,obj_id,score,R,t,time\n"
+
+  def row(k):
+    f = lambda v: nums[k % 4].replace("%r", "%s") % (repr(float(v)) if nums[k % 4] == "%r" else v)
+    R = [f(v) for v in rng.normal(size=9)]
+    t = [f(v) for v in rng.normal(size=3) * 1000]
+    if k % 5 == 0:
+      R[k % 9] = special[k % len(special)]
+    sep = "\t" if k % 7 == 0 else " "
+    ids = ["%d" % (k % 7), " %d " % k if k % 11 == 0 else "%d" % k, "%03d" % (1 + k % 21)]
+    return ",".join(ids + [f(rng.random()), sep.join(R), sep.join(t), "-1" if k % 2 else "0.25"])
+
+  rows = [row(k) for k in range(400)]
+  p = str(tmp_path / "r.csv")
+  for text in (header + "\n".join(rows) + "\n", "\n".join(rows), header, "", header + rows[0]):
+    open(p, "w").write(text)
+    lines = text.splitlines(keepends=True)
+    want = inout._bop_results_lines(lines[1:] if lines and header.strip() in lines[0] else lines)
+    assert inout._bop_results_native(p) is not None
+    _same_results(inout.load_bop_results(p), want)
+  # outside the plain form: the line reader decides (values or its error)
+  body = rows[:30]
+  cases = {
+      "crlf": "\r\n".join(body) + "\r\n",
+      "inf_nan": "\n".join(body[:3] + [body[3].replace(body[3].split(",")[4].split()[0], "nan", 1),
+                                       body[4].replace(",0.25", ",inf")]),
+      "underscore": "\n".join(body[:2] + [body[2].replace(",", ",1_0", 1)]),
+      "non_ascii": header.replace("time", "timé") + "\n".join(body),
+      "fields": "\n".join(body[:5] + ["1,2,3"] + body[5:]),
+      "bad_float": "\n".join(body[:7] + [body[7].replace(".", "x", 1)]),
+      "short_R": "\n".join(body[:4] + [",".join(body[4].split(",")[:4] + ["1 2 3"] +
+                                               body[4].split(",")[5:])]),
+      "blank_line": "\n".join(body[:3] + [""] + body[3:]),
+      "vtab": "\n".join(body[:2] + [body[2].replace(" ", "\v", 1)]),
+  }
+  for name, text in cases.items():
+    open(p, "w", newline="").write(text)
+    assert inout._bop_results_native(p) is None, name
+    with open(p, "r") as f:
+      lines = f.readlines()
+    try:
+      want = inout._bop_results_lines(lines[1:] if lines and header.strip() in lines[0] else lines)
+    except Exception as e:  # noqa: BLE001
+      with pytest.raises(type(e)) as got:
+        inout.load_bop_results(p)
+      assert str(got.value) == str(e), name
+    else:
+      _same_results(inout.load_bop_results(p), want)
+  with pytest.raises(OSError):
+    inout.load_bop_results(str(tmp_path / "missing.csv"))
