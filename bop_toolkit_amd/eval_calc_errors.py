@@ -524,6 +524,76 @@ def scene_arrays(recs):
           "pe": pe, "pair_off": pair_off, "pair_ri": pair_ri, "pair_gt": pair_gt, "pg": pg}
 
 
+def scene_arrays_direct(p, scene_id, scene_targets, ests_org, scene_gt):
+  """scene_arrays(scene_records(...)) without the per-record dicts (the arrays
+  path keeps no records): the same traversal, ranking, n_top rule, errors and
+  GT pairs (eval_calc_errors.py:238-290), straight into lists. Returns
+  (arrays, n_ests)."""
+  n_top_p, skip = p["n_top"], p["skip_missing"]
+  se = ests_org.get(scene_id, {})
+  rec_im, rec_obj, rec_est, rec_score, est_R, est_t, cnt = [], [], [], [], [], [], []
+  pair_gt, gt_R, gt_t = [], [], []
+  for im_id, im_targets in scene_targets.items():
+    ie = se.get(im_id, {})
+    for obj_id, target in im_targets.items():
+      if n_top_p == 0:
+        n_top = None
+      elif n_top_p == -1:
+        n_top = target["inst_count"]
+      else:
+        n_top = n_top_p
+      obj_ests = ie.get(obj_id, [])
+      if not skip and len(obj_ests) < n_top:
+        raise ValueError(
+            "Not enough estimates for scene: {}, im: {}, obj: {} (provided: {}, expected: {})"
+            .format(scene_id, im_id, obj_id, len(obj_ests), n_top))
+      ranked = sorted(enumerate(obj_ests), key=lambda x: x[1]["score"], reverse=True)
+      ranked = ranked[slice(0, n_top)]
+      gts = [(gt_id, gt) for gt_id, gt in enumerate(scene_gt[im_id]) if gt["obj_id"] == obj_id]
+      for est_id, est in ranked:
+        rec_im.append(im_id)
+        rec_obj.append(obj_id)
+        rec_est.append(est_id)
+        rec_score.append(est["score"])
+        est_R.append(est["R"])
+        est_t.append(est["t"])
+        cnt.append(len(gts))
+        for gt_id, gt in gts:
+          pair_gt.append(gt_id)
+          gt_R.append(gt["cam_R_m2c"])
+          gt_t.append(gt["cam_t_m2c"])
+  n, m = len(rec_im), len(pair_gt)
+  cnt = np.array(cnt, np.int64).reshape(n)
+  pair_off = np.zeros(n + 1, np.int64)
+  np.cumsum(cnt, out=pair_off[1:])
+  arr = {"rec_im": np.array(rec_im, np.int64).reshape(n),
+         "rec_obj": np.array(rec_obj, np.int64).reshape(n),
+         "rec_est": np.array(rec_est, np.int64).reshape(n),
+         "rec_score": np.array(rec_score, np.float64).reshape(n),
+         "pe": _poses12(est_R, est_t) if n else np.zeros((0, 12)), "pair_off": pair_off,
+         "pair_ri": np.repeat(np.arange(n, dtype=np.int64), cnt),
+         "pair_gt": np.array(pair_gt, np.int64).reshape(m),
+         "pg": _poses12(gt_R, gt_t) if m else np.zeros((0, 12))}
+  return arr, n
+
+
+_DIRECT_CACHE = {}
+
+
+def scene_arrays_direct_cached(p, scene_id, scene_targets, ests_org, scene_gt):
+  """scene_arrays_direct shared by the error types of one BOP19 run (keyed like
+  scene_records_cached; callers treat the arrays as read-only)."""
+  key = (scene_id, id(scene_targets), id(ests_org), id(scene_gt), p["n_top"], p["skip_missing"])
+  hit = _DIRECT_CACHE.get(key)
+  if hit is not None and hit[0] is scene_targets and hit[1] is ests_org and hit[2] is scene_gt:
+    return hit[3]
+  out = scene_arrays_direct(p, scene_id, scene_targets, ests_org, scene_gt)
+  if len(_DIRECT_CACHE) >= 4096:
+    _DIRECT_CACHE.clear()
+  _DIRECT_CACHE[key] = (scene_targets, ests_org, scene_gt, out)
+  return out
+
+
 _ARR_CACHE = {}
 
 
@@ -764,17 +834,19 @@ def run(p, device=0):
                                  dp_split["scene_camera_tpath"].format(scene_id=scene_id))
       scene_gt = cached_load(inout.load_scene_gt,
                              dp_split["scene_gt_tpath"].format(scene_id=scene_id))
-      recs, n_ests = scene_records_cached(p, scene_id, scene_targets, ests_org, scene_gt)
       planned = None
       if arrays:
-        arr = scene_arrays_cached(recs)
+        arr, n_ests = scene_arrays_direct_cached(p, scene_id, scene_targets, ests_org, scene_gt)
+        recs = None
         vals, todo = plan_arrays(p, arr, models_info)
         depths = None
         if et == "vsd" and len(todo):
           depths = prefetch_depths(
               np.unique(arr["rec_im"][arr["pair_ri"][todo]]).tolist(), scene_id, scene_camera)
         planned = ("arrays", arr, vals, todo, depths)
-      elif recs:
+        return scene_camera, recs, n_ests, planned
+      recs, n_ests = scene_records_cached(p, scene_id, scene_targets, ests_org, scene_gt)
+      if recs:
         errs, todo, mine = plan_rank(p, recs, models_info, ev.objects if ev else None,
                                      scene_camera, dp_split["im_size"], rank, world)
         depths = None

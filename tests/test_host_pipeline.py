@@ -188,3 +188,64 @@ def test_save_json_list_bytes(tmp_path):
     inout.save_json(str(path), c)
     want = "[\n" + ",\n".join("  " + json.dumps(e, sort_keys=True) for e in c) + "\n]" if c else "[\n]"
     assert path.read_text() == want, k
+
+
+def _rand_scene(rng, n_im, n_obj, max_ests, max_inst, tie_scores):
+  """targets / ests / scene_gt of one scene in the reference's shapes."""
+  scene_gt, targets, ests = {}, {}, []
+  for im in range(n_im):
+    objs = rng.choice(np.arange(1, 30), n_obj, replace=False).tolist()
+    gts = []
+    for o in objs:
+      for _ in range(int(rng.integers(1, max_inst + 1))):
+        gts.append({"obj_id": o, "cam_R_m2c": rng.normal(size=(3, 3)),
+                    "cam_t_m2c": rng.normal(size=(3, 1))})
+    rng.shuffle(gts)
+    scene_gt[im] = gts
+    for o in objs:
+      targets.setdefault(im, {})[o] = {"scene_id": 5, "im_id": im, "obj_id": o,
+                                       "inst_count": int(rng.integers(1, max_inst + 1))}
+      for _ in range(int(rng.integers(0, max_ests + 1))):
+        ests.append({"scene_id": 5, "im_id": im, "obj_id": o,
+                     "score": float(rng.integers(0, 3)) if tie_scores else float(rng.random()),
+                     "R": rng.normal(size=(3, 3)), "t": rng.normal(size=(3, 1)), "time": -1.0})
+  rng.shuffle(ests)
+  return targets, ests, scene_gt
+
+
+def test_scene_arrays_direct_equals_records_then_arrays():
+  """The arrays path builds a scene's arrays without record dicts
+  (scene_arrays_direct); they equal scene_arrays(scene_records(...)) for every
+  n_top rule, ties, missing estimates, and raise the same errors."""
+  rng = np.random.default_rng(17)
+  for trial in range(60):
+    targets, ests, scene_gt = _rand_scene(rng, int(rng.integers(0, 12)), int(rng.integers(1, 5)),
+                                          int(rng.integers(0, 4)), int(rng.integers(1, 3)),
+                                          trial % 2 == 0)
+    _, ests_org = ece._organize([], ests)
+    for n_top in (0, -1, 1, 2, 5):
+      for skip in (True, False):
+        p = {"n_top": n_top, "skip_missing": skip}
+        try:
+          recs, n_want = ece.scene_records(p, 5, targets, ests_org, scene_gt)
+          want = ece.scene_arrays(recs)
+        except Exception as e:  # noqa: BLE001
+          with pytest.raises(type(e)) as got_e:
+            ece.scene_arrays_direct(p, 5, targets, ests_org, scene_gt)
+          assert str(got_e.value) == str(e)
+          continue
+        got, n_got = ece.scene_arrays_direct(p, 5, targets, ests_org, scene_gt)
+        assert n_got == n_want
+        assert got.keys() == want.keys()
+        for k in want:
+          assert got[k].dtype == want[k].dtype and got[k].shape == want[k].shape, k
+          assert np.array_equal(got[k], want[k]), k
+  # an image of the targets without GT annotations: the same KeyError
+  targets, ests, scene_gt = _rand_scene(rng, 3, 2, 2, 1, False)
+  del scene_gt[1]
+  _, ests_org = ece._organize([], ests)
+  p = {"n_top": -1, "skip_missing": True}
+  with pytest.raises(KeyError):
+    ece.scene_records(p, 5, targets, ests_org, scene_gt)
+  with pytest.raises(KeyError):
+    ece.scene_arrays_direct(p, 5, targets, ests_org, scene_gt)

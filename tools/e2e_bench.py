@@ -196,7 +196,8 @@ def main():
   # host steps of the error passes (the prepare thread's included)
   from bop_toolkit_amd import depth_gpu, inout
   depth_gpu.DepthDecoder.load = timed("host:gpu_depth_load", depth_gpu.DepthDecoder.load)
-  for mod, name in ((ece, "scene_records"), (ece, "plan_rank"), (ece, "load_scene_depths"),
+  for mod, name in ((ece, "scene_records"), (ece, "scene_arrays_direct"), (ece, "plan_rank"),
+                    (ece, "load_scene_depths"),
                     (ece, "evaluate_batch"), (ece, "evaluate"), (ece, "Models"), (inout, "save_json"), (inout, "save_json_per_value")):
     setattr(mod, name, timed("host:" + name, getattr(mod, name)))
   p = eval_bop19_pose.parse_args([
