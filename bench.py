@@ -14,6 +14,11 @@ images are split over the ranks by LPT on the SURVEY.md §8d cost model
 
     python bench.py [--gpus N --steps K --warmup W --config C --tuples T]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+`python bench.py --gpus N` (no torchrun) starts the N rank processes itself
+(launch_ranks: one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as
+torchrun sets them) and exits with their status; under torchrun WORLD_SIZE
+must equal N.
 """
 import argparse
 import json
@@ -322,12 +327,87 @@ def algorithmic_cost(objs, host, n, K):
           "mspd": (mspd_bytes, 0.0, mspd_f64), "roi_mean": float(roi.mean())}
 
 
+def free_port():
+  import socket
+  s = socket.socket()
+  s.bind(("127.0.0.1", 0))
+  port = s.getsockname()[1]
+  s.close()
+  return port
+
+
+def rank_envs(n, port, base=None):
+  """The environment of each of n rank processes on this node (what
+  torch.distributed.run exports), rendezvous on 127.0.0.1."""
+  base = dict(os.environ if base is None else base)
+  return [dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+          for r in range(n)]
+
+
+def launch_ranks(cmd, n, base_env=None, poll=0.2):
+  """Run cmd as n rank processes (rank_envs) and wait for them. If one fails,
+  the others are terminated (their own pids, then killed after 30 s). Returns
+  0 or the first failing rank's exit status. The caller must not have touched
+  the GPU (the children initialise it)."""
+  import subprocess
+  envs = rank_envs(n, free_port(), base_env)
+  procs = [subprocess.Popen(cmd, env=e) for e in envs]
+  rc = 0
+  try:
+    live = list(procs)
+    while live:
+      time.sleep(poll)
+      for p in list(live):
+        r = p.poll()
+        if r is None:
+          continue
+        live.remove(p)
+        if r != 0 and rc == 0:
+          rc = r if r > 0 else 128 - r
+          for q in live:
+            q.terminate()
+  finally:
+    for p in procs:
+      try:
+        p.wait(timeout=30)
+      except subprocess.TimeoutExpired:
+        p.kill()
+        p.wait()
+  return rc
+
+
+def world_of(args, environ=None):
+  """(rank, world, local_rank) of this process; None when this is the
+  launcher of --gpus N > 1 rank processes (no WORLD_SIZE in the
+  environment). Under torchrun WORLD_SIZE must equal --gpus."""
+  env = os.environ if environ is None else environ
+  if "WORLD_SIZE" not in env:
+    if args.gpus > 1:
+      return None
+    return 0, 1, 0
+  world = int(env["WORLD_SIZE"])
+  if world != args.gpus:
+    raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+  return int(env.get("RANK", 0)), world, int(env.get("LOCAL_RANK", 0))
+
+
 def lib_digest():
   """sha256 of the loaded libbopx.so: ties a PMC summary to the build it measured."""
   import hashlib
   from bop_toolkit_amd import _lib
   with open(_lib.LIB_PATH, "rb") as f:
     return hashlib.sha256(f.read()).hexdigest()
+
+
+def code_digests():
+  """sha256 of the gfx950 code objects holding the measured kernels
+  (_lib.code_object_digests): ties a PMC summary to the machine code it
+  counted, not to the whole library (host code and other kernels' code
+  objects may change without changing these)."""
+  from bop_toolkit_amd import _lib
+  d = _lib.code_object_digests()
+  return {k: d.get(k) for k in ("k_vsd", "k_sym_error", "k_mean_error", "k_adi")}
 
 
 def workload_key(args, n):
@@ -338,12 +418,15 @@ def workload_key(args, n):
 def load_traffic(dom, args, n):
   """HBM bytes per launch of kernel `dom` from the committed rocprofv3 PMC
   summaries (profiles/*_pmc.json, written by tools/pmc_summary.py), or None.
-  A summary counts only if it records this library build (`lib_sha256`) and
-  this launch's workload (`workload`): otherwise it measured something else."""
+  A summary counts only if it records the code object of the measured kernel
+  (`code_sha256`, or a whole-library `lib_sha256` equal to this one) and this
+  launch's workload (`workload`): otherwise it measured something else."""
   import glob
   name = {"vsd": "k_vsd", "mssd": "k_sym_error<MSSD>", "mspd": "k_sym_error<MSPD>"}.get(dom)
   if name is None:
     return None
+  family = name.split("<")[0]
+  code = code_digests().get(family)
   digest, key = lib_digest(), workload_key(args, n)
   best = None
   for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json"))):
@@ -353,7 +436,8 @@ def load_traffic(dom, args, n):
     except (OSError, ValueError):
       continue
     meta = j.get("_meta", {})
-    if meta.get("lib_sha256") == digest and meta.get("workload") == key:
+    same_code = code is not None and meta.get("code_sha256", {}).get(family) == code
+    if (same_code or meta.get("lib_sha256") == digest) and meta.get("workload") == key:
       best = j.get(name, {}).get("hbm_bytes_per_launch", best)
   return best
 
@@ -427,12 +511,17 @@ def main():
   import torch
   import torch.distributed as dist
 
-  rank = int(os.environ.get("RANK", 0))
-  world = int(os.environ.get("WORLD_SIZE", 1))
-  local = int(os.environ.get("LOCAL_RANK", 0))
   # BOPX_DIST_BACKEND=gloo: rehearsal of the multi-rank flow with several ranks
   # on one GPU (host collectives); the measured configuration is RCCL, one GPU per rank.
   backend = os.environ.get("BOPX_DIST_BACKEND", "nccl")
+  rw = world_of(args)
+  if rw is None:  # --gpus N without torchrun: this process only launches the ranks
+    # (device_count() does not initialise the GPU on this image)
+    if backend == "nccl" and torch.cuda.device_count() < args.gpus:
+      raise SystemExit("bench.py --gpus %d: only %d GPUs visible (RCCL needs one per rank)" %
+                       (args.gpus, torch.cuda.device_count()))
+    sys.exit(launch_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
+  rank, world, local = rw
   if backend == "gloo":
     local %= torch.cuda.device_count()
   torch.cuda.set_device(local)
@@ -450,7 +539,8 @@ def main():
   meta = os.environ.get("BOPX_BENCH_META")  # tools/pmc.sh: what the counters measured
   if meta and rank == 0:
     with open(meta, "w") as f:
-      json.dump({"lib_sha256": lib_digest(), "workload": workload_key(args, n)}, f)
+      json.dump({"lib_sha256": lib_digest(), "code_sha256": code_digests(),
+                 "workload": workload_key(args, n)}, f)
 
   out_vsd = torch.empty((n, N_TAU), dtype=torch.float64, device=ev.device)
   out_mssd = torch.empty(n, dtype=torch.float64, device=ev.device)

@@ -200,3 +200,47 @@ class Context:
   def set_symmetries(self, obj_id, syms12):
     syms12 = np.ascontiguousarray(syms12, np.float64).reshape(-1, 12)
     self.call("bopx_set_symmetries", int(obj_id), ptr(syms12, _d), len(syms12))
+
+
+def code_object_digests(path=None):
+  """sha256 of each gfx950 code object in libbopx.so's .hip_fatbin section,
+  keyed by the kernels it defines ("k_vsd", "k_sym_error", "k_png_inflate",
+  ...: each translation unit's kernels share one code object). Ties a
+  rocprofv3 PMC summary to the machine code it measured, independently of
+  host code or other translation units linked into the same library
+  (bench.py load_traffic, tools/pmc.sh). Reads the file only (no GPU)."""
+  import hashlib
+  import re
+  import struct
+  with open(path or LIB_PATH, "rb") as f:
+    so = f.read()
+  # ELF64 section headers: find .hip_fatbin
+  shoff, = struct.unpack_from("<Q", so, 0x28)
+  shentsize, shnum, shstrndx = struct.unpack_from("<HHH", so, 0x3A)
+  sec = [struct.unpack_from("<IIQQQQ", so, shoff + i * shentsize) for i in range(shnum)]
+  stroff = sec[shstrndx][4]
+  fat = None
+  for name, _typ, _flags, _addr, off, size in sec:
+    end = so.index(b"\0", stroff + name)
+    if so[stroff + name:end] == b".hip_fatbin":
+      fat = so[off:off + size]
+  if fat is None:
+    raise ValueError("%s has no .hip_fatbin section" % (path or LIB_PATH))
+  magic = b"__CLANG_OFFLOAD_BUNDLE__"
+  out = {}
+  for m in re.finditer(re.escape(magic), fat):
+    b = m.start()
+    nent, = struct.unpack_from("<Q", fat, b + len(magic))
+    p = b + len(magic) + 8
+    for _ in range(nent):
+      off, size, tlen = struct.unpack_from("<QQQ", fat, p)
+      triple = fat[p + 24:p + 24 + tlen].decode(errors="replace")
+      p += 24 + tlen
+      if "gfx950" not in triple or size == 0:
+        continue
+      co = fat[b + off:b + off + size]
+      digest = hashlib.sha256(co).hexdigest()
+      # kernel descriptors are named "<mangled kernel>.kd" in the symbol table
+      for k in set(re.findall(rb"(k_[a-z0-9_]+)[A-Za-z0-9_]*\.kd\0", co)):
+        out[k.decode()] = digest
+  return out

@@ -204,7 +204,8 @@ hipError_t launch_render_batch(const ObjDesc* objs, int max_nf, int64_t n, const
 
 // kern_png.hip: 16-bit grayscale PNG decode (bopx_png_decode_dev).
 constexpr int kPngMaxWidth = 4096;  // k_png_unfilter's carry row (LDS)
-constexpr int kPngMaxRaw = 1 << 30; // inflated bytes per frame, H * (2W + 1)
+constexpr int kPngMaxRaw = 1 << 28; // inflated bytes per frame, H * (2W + 1); the Adler-32
+                                     // B sum (<= 255 N^2 / 2) fits in 64 bits up to here
 hipError_t launch_png_decode(int64_t n, const uint8_t* zdata, const int64_t* z_off,
                              const int32_t* z_len, int H, int W, const float* scales, uint8_t* raw,
                              int64_t raw_stride, float* frames, int32_t* status, hipStream_t s);

@@ -406,8 +406,10 @@ __device__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t*
       nb -= dx;
       if (dist > p || len > out_n - p) return kErr;
       // copy: byte i of the match = out[p - dist + i % dist]; sources all lie
-      // before p, so each 64-byte round reads, then writes (the ring cannot
-      // wrap onto a later round's source: rounds span < 520 bytes).
+      // before p, so each 64-byte round reads, then writes. Rounds before r0
+      // wrote ring slots p .. p + r0 - 1, which hold the sources q with
+      // kRing - r0 < p - q <= kRing: those are read from the flushed output
+      // (p - q > kRing - 256 lies more than two flushes back).
       const bool overlap = dist < len;
       const float rd = 1.0f / (float)dist;
       for (int r0 = 0; r0 < len; r0 += 64) {
@@ -421,7 +423,7 @@ __device__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t*
         const int q = p - dist + j;
         int b = 0;
         if (i < len) {
-          if (dist - j <= kRing) {
+          if (dist - j <= kRing - r0) {
             b = S.ring[q & kRingMask];
           } else {  // flushed at least one flush before the last (see flush_block)
             const uint32_t w = __hip_atomic_load(

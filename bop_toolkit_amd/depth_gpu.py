@@ -26,7 +26,7 @@ from . import _lib, inout
 
 RAW_ALIGN = 1024      # bopx_png_decode_dev's raw_stride granule
 MAX_WIDTH = 4096      # kern_png.hip's carry row (bopx_internal.h kPngMaxWidth)
-MAX_RAW = 1 << 30     # inflated bytes per frame
+MAX_RAW = 1 << 28     # inflated bytes per frame (bopx_internal.h kPngMaxRaw)
 
 
 def enabled():
@@ -102,6 +102,7 @@ class DepthDecoder:
       return frames
     if W > MAX_WIDTH or H * (2 * W + 1) > MAX_RAW:  # outside the kernel's range: host decoder
       frames.copy_(torch.from_numpy(_host_frames(paths, scales, H, W, workers)))
+      torch.cuda.current_stream(dev).synchronize()
       self.last_host = n
       return frames
     sc = np.ones(n, np.float32) if scales is None else np.asarray(
@@ -125,6 +126,9 @@ class DepthDecoder:
       arr = _host_frames([paths[k] for k in host], None if scales is None else
                          [float(sc[k]) for k in host], H, W, workers)
       frames[torch.from_numpy(host).to(dev)] = torch.from_numpy(arr).to(dev)
+      # the index_put is queued on `stream`; callers consume the frames on other
+      # streams (the scene prefetch threads), so the frames are final on return
+      stream.synchronize()
     self.last_host = len(host)
     return frames
 

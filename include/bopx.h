@@ -276,7 +276,8 @@ int bopx_depth_finish_dev(bopx_ctx* ctx, float* frames, int64_t n_pixels, void* 
  *           type); status[2k + 1] is scratch. A corrupt frame's pixels are
  *           undefined; decode that file on the host (bopx_load_depth_pngs),
  *           which reports the host path's own result or error.
- * width <= 4096, height * (2 width + 1) <= 2^30. */
+ * width <= 4096, height * (2 width + 1) <= 2^28
+ * (the Adler-32 sums of k_png_unfilter stay inside 64 bits). */
 enum { BOPX_PNG_OK = 0, BOPX_PNG_CORRUPT = 2 };
 int bopx_png_decode_dev(bopx_ctx* ctx, int64_t n, const uint8_t* zdata, const int64_t* z_off,
                         const int32_t* z_len, int height, int width, const float* scales,

@@ -230,3 +230,119 @@ def test_pack_for_the_device_decoder(tmp_path):
   # too small a buffer: nothing read
   with pytest.raises(RuntimeError):
     depth_gpu.pack(paths, 30, 40, lambda nb: np.zeros(nb - 1, np.uint8))
+
+
+def deflate_matches(z):
+  """(output bytes, [(length, distance), ...]) of a zlib stream: a small
+  RFC 1951 decoder that records every back-reference (test helper; the
+  device decoder's ring / flushed-output split depends on the distances)."""
+  pos = [16]  # bit position (after the 2-byte zlib header)
+  def bits(n):
+    v = 0
+    for i in range(n):
+      p = pos[0] + i
+      v |= ((z[p >> 3] >> (p & 7)) & 1) << i
+    pos[0] += n
+    return v
+  def code(lens):
+    cnt = [0] * 16
+    for l in lens:
+      cnt[l] += 1
+    cnt[0] = 0
+    nxt, c = [0] * 16, 0
+    for L in range(1, 16):
+      c = (c + cnt[L - 1]) << 1
+      nxt[L] = c
+    tab = {}
+    for s, l in enumerate(lens):
+      if l:
+        tab[(l, nxt[l])] = s
+        nxt[l] += 1
+    return tab
+  def sym(tab):
+    c = L = 0
+    while True:
+      c = (c << 1) | bits(1)
+      L += 1
+      if (L, c) in tab:
+        return tab[(L, c)]
+  LB = [3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115,
+        131, 163, 195, 227, 258]
+  LX = [0] * 8 + [1] * 4 + [2] * 4 + [3] * 4 + [4] * 4 + [5] * 4 + [0]
+  DB = [1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769, 1025, 1537,
+        2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577]
+  DX = [0, 0, 0, 0] + [i // 2 for i in range(2, 28)]
+  out, matches = bytearray(), []
+  final = 0
+  while not final:
+    final, typ = bits(1), bits(2)
+    if typ == 0:
+      pos[0] = (pos[0] + 7) & ~7
+      n = bits(16)
+      bits(16)
+      out += z[pos[0] >> 3:(pos[0] >> 3) + n]
+      pos[0] += 8 * n
+      continue
+    if typ == 1:
+      lt = code([8] * 144 + [9] * 112 + [7] * 24 + [8] * 8)
+      dt = code([5] * 30)
+    else:
+      hlit, hdist, hclen = bits(5) + 257, bits(5) + 1, bits(4) + 4
+      order = [16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15]
+      cl = [0] * 19
+      for i in range(hclen):
+        cl[order[i]] = bits(3)
+      ct = code(cl)
+      lens = []
+      while len(lens) < hlit + hdist:
+        s = sym(ct)
+        if s < 16:
+          lens.append(s)
+        elif s == 16:
+          lens += [lens[-1]] * (3 + bits(2))
+        elif s == 17:
+          lens += [0] * (3 + bits(3))
+        else:
+          lens += [0] * (11 + bits(7))
+      lt, dt = code(lens[:hlit]), code(lens[hlit:])
+    while True:
+      s = sym(lt)
+      if s < 256:
+        out.append(s)
+      elif s == 256:
+        break
+      else:
+        n = LB[s - 257] + bits(LX[s - 257])
+        ds = sym(dt)
+        d = DB[ds] + bits(DX[ds])
+        matches.append((n, d))
+        for _ in range(n):
+          out.append(out[-d])
+  return bytes(out), matches
+
+
+def far_match_stream(rng, period, h, w):
+  """Filtered scanlines (filter 0) whose bytes repeat with the given period,
+  compressed at level 9: long matches (up to 258 bytes) at distance `period`.
+  Returns (zlib stream, raw bytes)."""
+  rowb = 2 * w + 1
+  base = rng.integers(0, 256, period, dtype=np.uint8)
+  raw = np.resize(base, h * rowb)
+  raw[::rowb] = 0
+  raw = raw.tobytes()
+  return zlib.compress(raw, 9), raw
+
+
+def test_far_match_streams_hold_matches_past_the_ring():
+  """The streams of test_gpu_png.py::test_gpu_decode_far_matches: 258-byte
+  matches at distances just past the device decoder's 4 KB ring (4096 <
+  dist <= 4096 + 257), where a 64-byte copy round would read a slot an
+  earlier round of the same copy rewrote; the tracer itself is checked
+  against zlib."""
+  rng = np.random.default_rng(17)
+  for period in (4100, 4166, 4323, 4350):
+    z, raw = far_match_stream(rng, period, 24, 720)
+    out, matches = deflate_matches(z)
+    assert out == raw == zlib.decompress(z)
+    far = [m for m in matches if 4096 < m[1] <= 4096 + 257 and m[0] > 64]
+    assert len(far) >= 20, (period, len(far))

@@ -121,3 +121,21 @@ def test_bench_two_ranks_multi_instance():
   n = line["config"]["global_batch"]
   assert line["n_gpus"] == 2 and n > 1000 and 0 < line["config"]["tuples_rank0"] < n  # ~1,500 (random k)
   assert line["value"] > 0 and line["kernels"]["vsd"]["ms"] > 0
+
+
+def test_bench_gpus_flag_launches_ranks():
+  """`python bench.py --gpus 2` without torchrun (the driver's command form):
+  bench.py starts the two rank processes itself (gloo rehearsal on the one
+  GPU), the line reports n_gpus 2 and the unchanged whole job."""
+  import json
+  env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+  env["BOPX_DIST_BACKEND"] = "gloo"
+  cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--tuples", "1000",
+         "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+  r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=300)
+  assert r.returncode == 0, r.stderr[-3000:]
+  lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+  assert len(lines) == 1  # rank 0 only
+  line = json.loads(lines[0])
+  assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 1002
+  assert 0 < line["config"]["tuples_rank0"] < 1002 and line["value"] > 0

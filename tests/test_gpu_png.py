@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 from PIL import Image
 
-from test_depth_png import _depth, _filter_rows, png_from_zlib, write_png16
+from test_depth_png import _depth, _filter_rows, far_match_stream, png_from_zlib, write_png16
 
 pytestmark = pytest.mark.gpu
 
@@ -111,6 +111,50 @@ def test_gpu_decode_full_frames(tmp_path, dec):
   assert dec.last_host == 0
   assert np.array_equal(got.cpu().numpy().view(np.uint32),
                         _host(paths, scales, 480, 640).view(np.uint32))
+
+
+def test_gpu_decode_far_matches(tmp_path, dec):
+  """258-byte matches at distances 4100-4350 (a T-LESS 720-px row is 1,441
+  bytes, so a 3-row distance is 4,323): past the 4 KB ring by less than a
+  copy's length, so later copy rounds must read the flushed output, not ring
+  slots the same copy already rewrote. Decoded on the device (no host
+  fallback) and equal to the host decoder."""
+  rng = np.random.default_rng(17)
+  h, w = 24, 720
+  paths = []
+  for period in (4100, 4166, 4323, 4350):
+    z, _ = far_match_stream(rng, period, h, w)
+    p = str(tmp_path / ("far%d.png" % period))
+    png_from_zlib(p, w, h, z)
+    paths.append(p)
+  got = dec.load(paths, None, h, w, torch).cpu().numpy()
+  assert dec.last_host == 0
+  assert np.array_equal(got.view(np.uint32), _host(paths, None, h, w).view(np.uint32))
+
+
+def test_gpu_decode_host_rows_final_for_other_streams(tmp_path, dec):
+  """A batch with a file only the host decodes (8-bit) and clean ones: the
+  frames load() returns are final for a consumer on another stream (the
+  scene prefetch hands them to the error kernels' stream)."""
+  rng = np.random.default_rng(21)
+  h, w = 480, 640
+  paths = []
+  for k in range(6):
+    p = str(tmp_path / ("c%d.png" % k))
+    write_png16(p, _image(rng, k % 6, h, w))
+    paths.append(p)
+  p8 = str(tmp_path / "g8.png")
+  Image.fromarray((_image(rng, 0, h, w) % 256).astype(np.uint8)).save(p8)
+  paths.insert(3, p8)
+  side = torch.cuda.Stream()
+  with torch.cuda.stream(side):
+    got = dec.load(paths, [0.1] * len(paths), h, w, torch)
+  consumer = torch.cuda.Stream()
+  with torch.cuda.stream(consumer):
+    snap = got.clone()
+  consumer.synchronize()
+  assert dec.last_host == 1
+  assert np.array_equal(snap.cpu().numpy(), _host(paths, [0.1] * len(paths), h, w))
 
 
 def test_gpu_decode_rejects_what_the_host_rejects(tmp_path, dec):
