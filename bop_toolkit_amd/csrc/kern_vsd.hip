@@ -49,12 +49,29 @@ __device__ unsigned long long g_vsd_stats[16];
 // [4] pixel work, [5] pixel barrier wait, [6] pre-loop, [7] epilogue; raster work
 // split: [8] vertex staging, [9] bbox test + compaction, [10] set-up, [11] walk.
 __device__ unsigned long long g_vsd_time[16];
+// Wave-level loop trip counts for the instruction census (bit 2; tools/isa_census.py):
+// [0] claim-loop iterations, [1] set-up chunks, [2] row-item windows, [3] walk passes,
+// [4] walk column-pair iterations (per pass: the widest row of its lanes),
+// [5] pixel compaction rows, [6] pixel-loop iterations, [7] exact-path ballots,
+// [8] slow-raster column iterations (widest lane), [9] slow-raster rows (widest lane),
+// [10] list_tile calls, [11] tile iterations, [12] set-up chunks with a slow triangle
+__device__ unsigned long long g_vsd_wave[16];
 // Diagnostics are compiled in only with -DBOPX_VSD_DIAG=1 (tools/vsd_stats.py
 // loads such a variant); the product kernel carries none of their state.
 #ifndef BOPX_VSD_DIAG
 #define BOPX_VSD_DIAG 0
 #endif
 #define VSD_DIAG(bit) (BOPX_VSD_DIAG && (a.ablate & (bit)))
+// lane 0 adds v (wave-uniform) to wave-level counter k (diag builds only; the
+// product build has no trace of it, not even a captured variable)
+#if BOPX_VSD_DIAG
+#define VSD_WAVE(k, v)                                                             \
+  do {                                                                             \
+    if (VSD_DIAG(4) && lane == 0) atomicAdd(&g_vsd_wave[k], (unsigned long long)(v)); \
+  } while (0)
+#else
+#define VSD_WAVE(k, v) ((void)0)
+#endif
 #define VSD_STAMP(k)                                              \
   do {                                                            \
     if (VSD_DIAG(8)) {                                            \
@@ -383,6 +400,12 @@ __device__ __forceinline__ bool region_covered(const uint32_t* dep, const Region
   for (int b = b0; b < g.nb; b += 8)
     if (__builtin_amdgcn_ballot_w64(region_min8(dep, g, b, lane) < qb) != 0) return false;
   return true;
+}
+
+// Max over the lanes of a non-negative int (diagnostics only: not optimised)
+__device__ __forceinline__ int diag_wave_max(int v) {
+  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+  return v;
 }
 
 // Inclusive prefix sum over the 64 lanes (full exec), all in DPP: row_shr 1, 2,
@@ -773,6 +796,7 @@ void k_vsd(VsdArgs a) {
     // q tiles are already zero, see the pixel pass): each thread its kR
     // rectangles (kStream: round e0, recomputed)
     auto list_tile = [&](int tt, int qb, int e0) {
+      VSD_WAVE(10, 1);
       const int lx0 = rx0 + (tt % ntx) * kTileW, ly0 = ry0 + (tt / ntx) * kTileH;
       const int lx1 = min(lx0 + kTileW - 1, rx1), ly1 = min(ly0 + kTileH - 1, ry1);
 #pragma unroll
@@ -818,6 +842,7 @@ void k_vsd(VsdArgs a) {
       const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
       const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
       const int qb = kAhead ? (it & 1) : 0;  // this tile's queue
+      VSD_WAVE(11, 1);
       ListT* const s_list = s_lists[qb];
       int* const p_nlist = &s_nlists[qb];
       int* const p_nsmall = &s_nsmalls[qb];
@@ -858,6 +883,7 @@ void k_vsd(VsdArgs a) {
           base = __builtin_amdgcn_readfirstlane(base);
         }
         VSD_STAMP(12);
+        VSD_WAVE(0, 1);
         if (base >= nl) break;
         if (base + kGroup * kVsdWaves >= nl) __builtin_amdgcn_s_setprio(kVsdPrio);
         f32x3 v[kGroup];
@@ -987,6 +1013,7 @@ void k_vsd(VsdArgs a) {
         if (VSD_DIAG(4) && lane == 0) atomicAdd(&g_vsd_stats[1], (unsigned long long)kGroup);
         VSD_STAMP(9);
         for (int c0 = 0; c0 < (VSD_DIAG(64) ? 0 : cnt); c0 += 64) {
+          VSD_WAVE(1, 1);
           // Set-up, one triangle per lane.
           RTri T;
           bool ok = false;
@@ -1024,6 +1051,14 @@ void k_vsd(VsdArgs a) {
             }
             if (lane == 0 && __builtin_amdgcn_ballot_w64(ok && !fast) != 0)
               atomicAdd(&g_vsd_stats[12], 1ull);
+#if BOPX_VSD_DIAG
+            const bool slow = ok && !fast;
+            const int sr = diag_wave_max(slow ? rr1 - rr0 + 1 : 0);
+            const int sc = diag_wave_max(slow ? (rr1 - rr0 + 1) * (cc1 - cc0 + 1) : 0);
+            VSD_WAVE(8, sc);
+            VSD_WAVE(9, sr);
+            VSD_WAVE(12, sr > 0);
+#endif
           }
           if (ok && !fast) {
             uint32_t* dep = s_dep[r];
@@ -1047,6 +1082,7 @@ void k_vsd(VsdArgs a) {
                            (uint32_t)(rbal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rbal, 0u))]);
           int rec_base = 0;  // records started before the current pass
           for (int wb = 0; wb < (VSD_DIAG(32) ? 0 : nrow); wb += kRowWin) {
+            VSD_WAVE(2, 1);
             wave_lds_sync();  // records written / previous window's owners consumed
             // one start flag per record instead of one owner byte per row item
             reinterpret_cast<uint32_t*>(&s_own[wave][0])[lane] = 0u;
@@ -1069,6 +1105,13 @@ void k_vsd(VsdArgs a) {
                                 (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
               rec_base += __popcll(M);
+              VSD_WAVE(3, 1);
+#if BOPX_VSD_DIAG
+              if VSD_DIAG(4) {
+                const int wl = valid ? (int)((s_rec[wave][owner].meta >> 12) & 63u) + 1 : 0;
+                VSD_WAVE(4, diag_wave_max((wl + 1) >> 1));
+              }
+#endif
               if (valid) {
                 // the 48-B record as three 16-B LDS reads
                 RRow rec;
@@ -1157,6 +1200,7 @@ void k_vsd(VsdArgs a) {
         // column right of a tile cut by the ROI: the row walk may have written
         // it (r_walk_row_max); cleared here (wave-private rows, raster done)
         const int cut = tx1 - tx0 + 1;
+        VSD_WAVE(5, nrow > wave ? (nrow - wave + kVsdWaves - 1) / kVsdWaves : 0);
         for (int r = wave; r < nrow; r += kVsdWaves) {
           if (cut < kTileW && lane < 2) s_dep[lane][r * kTileStride + cut] = 0u;
           const int ps = r * kTileStride + lane;
@@ -1218,6 +1262,7 @@ void k_vsd(VsdArgs a) {
             unc |= ge_lo != ge_hi;
           }
           if (__builtin_expect(__builtin_amdgcn_ballot_w64(unc) != 0, 0)) {
+            VSD_WAVE(7, 1);
             if (unc) {  // undo the float32 increments, redo the pixel exactly
               if VSD_DIAG(4) atomicAdd(&g_vsd_stats[14], 1ull);
               c_union -= vg | ve;
@@ -1254,6 +1299,7 @@ void k_vsd(VsdArgs a) {
           }
         }
       };
+      VSD_WAVE(6, (npix + 63) / 64);
       for (int i = lane; i < npix; i += 64) {
         const int p = pix[i];
         const int row = ty0 + p / kTileW, col = tx0 + p % kTileW;
@@ -1425,10 +1471,13 @@ hipError_t read_vsd_stats(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vsd_stats), sizeof(g_vsd_stats));
   if (e == hipSuccess)
     e = hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(g_vsd_time), sizeof(g_vsd_time));
+  if (e == hipSuccess)
+    e = hipMemcpyFromSymbol(out + 32, HIP_SYMBOL(g_vsd_wave), sizeof(g_vsd_wave));
   if (e != hipSuccess || !reset) return e;
   unsigned long long z[16] = {};
   e = hipMemcpyToSymbol(HIP_SYMBOL(g_vsd_stats), z, sizeof(g_vsd_stats));
-  return e == hipSuccess ? hipMemcpyToSymbol(HIP_SYMBOL(g_vsd_time), z, sizeof(z)) : e;
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_vsd_time), z, sizeof(z));
+  return e == hipSuccess ? hipMemcpyToSymbol(HIP_SYMBOL(g_vsd_wave), z, sizeof(z)) : e;
 }
 
 constexpr int kBopTaus = 10;  // eval_calc_errors.py:47, np.arange(0.05, 0.51, 0.05)

@@ -1710,7 +1710,8 @@ int bopx_visib_mask(bopx_ctx* c, int64_t n, const double* d_test, const double* 
 // Diagnostics (not in include/bopx.h): out[0..15] = k_vsd workload counters
 // (BOPX_VSD_ABLATE bit 2: tiles, meshlet entries, triangle set-ups, bbox
 // pixels, row items, fragments, covered pixels, row passes, sum of per-pass
-// widest rows), out[16..31] = phase clocks (bit 3). out holds 32 values.
+// widest rows), out[16..31] = phase clocks (bit 3), out[32..47] = wave-level
+// loop trip counts (bit 2, tools/isa_census.py). out holds 48 values.
 int bopx_debug_vsd_stats(bopx_ctx* c, unsigned long long* out, int reset) {
   if (!c || !out) return BOPX_E_INVALID;
   if (int r = set_dev(c)) return r;

@@ -34,7 +34,7 @@ def main():
   n, d = bench.build_workload(ev, objs, args, 0, 1, torch)
   fn = ev.ctx.lib.bopx_debug_vsd_stats
   fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-  st = (ctypes.c_ulonglong * 32)()
+  st = (ctypes.c_ulonglong * 48)()
   fn(ev.ctx.h, st, 1)
   ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"], d["frames"], d["cam"],
          bench.DELTA, bench.TAUS, d["diameters"])
@@ -56,6 +56,20 @@ def main():
                          bench.synth_K() if hasattr(bench, "synth_K") else __import__(
                              "bop_toolkit_amd.synth", fromlist=["YCBV_K"]).YCBV_K)
   print("bbox-corner ROI mean px %.0f" % np.mean(roi))
+  wave = ["claim_iters", "setup_chunks", "row_windows", "walk_passes", "walk_col_iters",
+          "pix_compact_rows", "pix_iters", "exact_ballots", "slow_col_iters", "slow_rows",
+          "list_calls", "tile_iters", "slow_chunks"]
+  for i, k in enumerate(wave):
+    print("wave %-18s total %14d  per tuple %12.2f" % (k, st[32 + i], st[32 + i] / n))
+  out = os.environ.get("BOPX_VSD_STATS_JSON")
+  if out:
+    import json
+    with open(out, "w") as f:
+      json.dump({"tuples": n, "workload": bench.workload_key(args, n),
+                 "stats": {k: st[i] / n for i, k in enumerate(names)},
+                 "wave": {k: st[32 + i] / n for i, k in enumerate(wave)},
+                 "phase_cycles_per_wave_tuple": {k: st[16 + i] / n / 8 for i, k in enumerate(ph)}},
+                f, indent=1)
 
 
 if __name__ == "__main__":
