@@ -31,41 +31,112 @@ KERNEL = "_ZN4bopx5k_vsdILi0ELi1ELi10EEEvNS_7VsdArgsE"  # k_vsd<0,1,10>: the ben
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-fast-math", "--cuda-device-only", "-S"]
 
-# Source ranges -> phase (file, first line, last line, phase); first match wins.
-PHASES = [
-    ("raster.h", 357, 406, "walk"),               # r_walk_row_max
-    ("kern_vsd.hip", 1049, 1092, "walk"),         # windows, passes, owner lookup, record reads
-    ("raster.h", 324, 341, "setup"),              # r_make_row
-    ("raster.h", 182, 231, "setup"),              # r_setup_touching
-    ("raster.h", 40, 46, "rcp"),                  # rcp_rn (set-up, staging, pixel pass)
-    ("raster.h", 254, 305, "slow_raster"),        # r_raster (large / irregular triangles)
-    ("kern_vsd.hip", 989, 1048, "setup"),         # chunk loop, row numbering, records
-    ("raster.h", 62, 78, "staging"),              # r_vertex
-    ("raster.h", 235, 241, "compaction"),         # r_touches
-    ("kern_vsd.hip", 971, 988, "compaction"),
-    ("kern_vsd.hip", 341, 386, "cull"),           # occlusion-test regions (cull modes)     # bbox test + ballot compaction
-    ("kern_vsd.hip", 854, 970, "staging"),        # claim, queue words, loads, transform, cull
-    ("kern_vsd.hip", 1093, 1098, "setup"),
-    ("kern_vsd.hip", 1099, 1103, "list"),         # list-ahead
-    ("kern_vsd.hip", 775, 816, "list"),           # list_tile
-    ("kern_vsd.hip", 1104, 1144, "coeffs_touch"),  # touch loads, coefficients, barrier
-    ("kern_vsd.hip", 1145, 1178, "pixel_compaction"),
-    ("kern_vsd.hip", 86, 106, "pixel"),           # dist_of / visib
-    ("kern_vsd.hip", 72, 84, "pixel"),            # sqrt_depth
-    ("kern_vsd.hip", 138, 190, "pixel"),          # filter
-    ("kern_vsd.hip", 1179, 1316, "pixel"),
-    ("kern_vsd.hip", 817, 853, "tile_loop"),
-    ("kern_vsd.hip", 1317, 1422, "epilogue"),
-    ("kern_vsd.hip", 496, 774, "prologue"),       # rectangles, ROI, thresholds, clears
-    ("kern_vsd.hip", 200, 340, "prologue"),       # step_threshold, meshlet_rect, wave max
+# Phases by source anchors (resolved against the current sources, so the
+# table survives edits): functions by name (raster.h / kern_vsd.hip device
+# functions), and regions of k_vsd from the first line matching `start` to the
+# line before the first later line matching `stop`. First match wins.
+FUNCS = {  # device function -> phase
+    "rcp_rn": "rcp", "r_vertex": "staging", "r_setup_touching": "setup", "r_touches": "compaction",
+    "r_raster": "slow_raster", "r_q": "slow_raster", "r_make_row": "setup",
+    "r_walk_row_max": "walk", "vsd_exact_px": "exact", "sqrt_depth": "pixel", "dist_of": "pixel",
+    "visib19t": "pixel", "vsd_filter_px": "pixel", "filt_a": "coeffs_touch",
+    "filt_b": "coeffs_touch", "filt_thr": "prologue", "step_threshold": "prologue",
+    "meshlet_rect": "prologue", "wave_max_nonneg_f32": "prologue", "region_min8": "cull",
+    "region_covered": "cull", "make_region": "cull", "wave_incl_scan": "setup",
+    "wave_sum_u32": "epilogue", "wave_sum_f64": "epilogue",
+}
+REGIONS = [  # (start, stop, phase) inside k_vsd
+    ("auto step_exact = [&]", "auto vsd_px = [&]", "exact"),
+    ("if (unc) {  // undo", "} else {  // tlinear", "exact"),
+    ("for (int wb = 0; wb <", "VSD_STAMP(11);", "walk"),
+    ("for (int c0 = 0; c0 <", "for (int wb = 0; wb <", "setup"),
+    ("VSD_STAMP(11);", "}  // rounds (kStream)", "setup"),
+    ("int cnt = 0;", "VSD_STAMP(9);", "compaction"),
+    ("for (int claimed = 0;; claimed = 1)", "int cnt = 0;", "staging"),
+    ("auto list_tile = [&]", "for (int t = sp, it = 0;", "list"),
+    ("}  // rounds (kStream)", "// Touch the test-depth lines", "list"),
+    ("for (int t = sp, it = 0;", "for (int claimed = 0;; claimed = 1)", "tile_loop"),
+    ("// Touch the test-depth lines", "// 3. per-pixel distances", "coeffs_touch"),
+    ("// 3. per-pixel distances", "// step cost: the certified", "pixel_compaction"),
+    ("// step cost: the certified", "// 4. workgroup reduction", "pixel"),
+    ("// 4. workgroup reduction", "hipError_t read_vsd_stats", "epilogue"),
+    ("void k_vsd(VsdArgs a) {", "// 2a. list the (pose, meshlet)", "prologue"),
 ]
+# Loops: the region (or function) holding the loop's header block -> the diag
+# counter of its wave-level trip count (tools/vsd_stats.py "wave" keys, per
+# tuple and summed over the 8 waves).
+LOOP_REGIONS = [
+    ("func", "r_walk_row_max", "walk_col_iters"),
+    ("for (int p0 = 0; p0 < wn", "VSD_STAMP(11);", "walk_passes"),
+    ("for (int wb = 0; wb <", "for (int p0 = 0; p0 < wn", "row_windows"),
+    ("for (int c0 = 0; c0 <", "for (int wb = 0; wb <", "setup_chunks"),
+    ("for (int claimed = 0;; claimed = 1)", "int cnt = 0;", "claim_iters"),
+    ("for (int t = sp, it = 0;", "for (int claimed = 0;; claimed = 1)", "tile_iters"),
+    ("// 3. per-pixel distances", "// step cost: the certified", "pix_compact_rows"),
+    ("for (int i = lane; i < npix; i += 64)", "VSD_STAMP(4);", "pix_iters"),
+    ("func", "r_raster", "slow"),
+    ("func", "region_min8", "zero"),
+    ("func", "region_covered", "zero"),
+]
+# Blocks outside their loop's usual path: their own counters
+BLOCK_COUNTERS = {"exact": "exact_ballots", "cull": "zero", "slow_raster": "slow_chunks"}
+_RANGES = {}
+
+
+def _lines(path):
+  with open(path) as f:
+    return f.read().split("\n")
+
+
+def _func_range(lines, name):
+  """[first, last] 1-based lines of device function `name` (its signature line
+  to the first later line that is a lone closing brace)."""
+  pat = re.compile(r"^(?:template <.*>\s*)?(?:__device__|__global__).*[ *]%s\(" % re.escape(name))
+  for i, l in enumerate(lines):
+    if pat.search(l) or (l.startswith("__device__") and (" %s(" % name) in l):
+      for j in range(i, len(lines)):
+        if lines[j] == "}":
+          return i + 1, j + 1
+  return None
+
+
+def _region(lines, start, stop):
+  a = next(i for i, l in enumerate(lines) if start in l)
+  b = next(i for i in range(a + 1, len(lines)) if stop in lines[i])
+  return a + 1, b  # [start line, line before stop]
+
+
+def ranges():
+  if _RANGES:
+    return _RANGES
+  src = {os.path.basename(p): _lines(p) for p in (SRC, os.path.join(os.path.dirname(SRC),
+                                                                      "raster.h"))}
+  ph, lp = [], []
+  for fname, lines in src.items():
+    for name, phase in FUNCS.items():
+      r = _func_range(lines, name)
+      if r:
+        ph.append((fname, r[0], r[1], phase))
+  k = src["kern_vsd.hip"]
+  reg = [("kern_vsd.hip",) + _region(k, a, b) + (p,) for a, b, p in REGIONS]
+  _RANGES["phases"] = reg + ph  # k_vsd regions first (lambdas inside k_vsd), then functions
+  for a, b, name in LOOP_REGIONS:
+    if a == "func":
+      for fname, lines in src.items():
+        r = _func_range(lines, b)
+        if r:
+          lp.append((fname, r[0], r[1], name))
+    else:
+      lp.append(("kern_vsd.hip",) + _region(k, a, b) + (name,))
+  _RANGES["loops"] = lp
+  return _RANGES
 
 
 def phase_of(loc):
   if loc is None:
     return "?"
   f, line = loc
-  for pf, a, b, name in PHASES:
+  for pf, a, b, name in ranges()["phases"]:
     if f == pf and a <= line <= b:
       return name
   if f.startswith("amd_") or f.startswith("__clang"):
@@ -156,6 +227,70 @@ def parse(path, kernel):
   return blocks
 
 
+# Small prologue / epilogue loops: fixed trips per tuple (anchor region, trips)
+CONST_LOOPS = [
+    ("for (int k = 0; k < a.n_tau; ++k) fast", "divide = a.normalized && !fast;", 8 * 10.0),
+    ("for (int i = tid; i < 2 * kTileStride * kTileH", "__syncthreads();", 8 * 17.0),
+    ("// 4. workgroup reduction", "hipError_t read_vsd_stats", 10.0),  # tid 0: n_tau
+]
+CONST_FUNCS = {"step_threshold": 4.0}  # wave 0: the ulp walk
+
+
+def _votes(b):
+  """The LOOP_REGIONS entry holding most of block b's instruction lines."""
+  votes = collections.Counter()
+  for _, loc in b["insts"]:
+    if not loc:
+      continue
+    for f, a0, a1, name in ranges()["loops"]:
+      if loc[0] == f and a0 <= loc[1] <= a1:
+        votes[name] += 1
+        break
+  return votes.most_common(1)[0][0] if votes else None
+
+
+def loop_counter(blocks, header):
+  """Counter of a loop: the LOOP_REGIONS entry of its header block (r_raster
+  loops: rows when the enclosing loop is the set-up chunk loop, columns
+  otherwise), a fixed trip count (float) for the small prologue / epilogue
+  loops, or None."""
+  by = {b["label"]: b for b in blocks}
+  b = by.get(header)
+  if b is None:
+    return None
+  name = _votes(b)
+  par = b["parents"][-1] if b["parents"] else None
+  if name is None:
+    src = _lines(SRC)
+    for a0, z, trips in CONST_LOOPS:
+      r0, r1 = _region(src, a0, z)
+      if any(loc and loc[0] == "kern_vsd.hip" and r0 <= loc[1] <= r1 for _, loc in b["insts"]):
+        return trips
+    for fn, trips in CONST_FUNCS.items():
+      r = _func_range(src, fn)
+      if r and any(loc and loc[0] == "kern_vsd.hip" and r[0] <= loc[1] <= r[1]
+                   for _, loc in b["insts"]):
+        return trips
+    if any(loc and loc[0].startswith("amd_hip_atomic") for _, loc in b["insts"]):
+      return 8.0  # the CAS loop of a lane-0 atomic: once per wave
+    # a header without lines of its own (r_raster's small-triangle row loop)
+    if par in by and _votes(by[par]) == "setup_chunks":
+      kids = [c for c in blocks if c["loop"] == c["label"] and c["parents"] and
+              c["parents"][-1] == header]
+      if any(_votes(c) == "slow" for c in kids):
+        return "slow_rows"
+    return None
+  if name == "slow":
+    name = "slow_rows" if par in by and _votes(by[par]) == "setup_chunks" else "slow_col_iters"
+  return name
+
+
+def block_rare(b):
+  """Blocks of the IEEE division fall-back of rcp_rn (inputs outside the
+  normal range) and the diag-free error paths: not executed on the bench."""
+  return any(op.startswith(("v_div_fmas", "v_div_scale", "v_div_fixup")) for op, _ in b["insts"])
+
+
 def loop_phase(blocks, header):
   """Majority phase of the instructions of a loop's own blocks."""
   cnt = collections.Counter()
@@ -200,8 +335,32 @@ def main():
   print("kernel %s: %d blocks, %d instructions (%s)" % (
       a.kernel, len(blocks), sum(total.values()),
       ", ".join("%s %d" % kv for kv in sorted(total.items()))))
-  counts = json.load(open(a.counts)) if a.counts else {}
+  counts = {}
+  if a.counts:
+    cj = json.load(open(a.counts))
+    counts = dict(cj["wave"])
+    counts["zero"] = 0.0
+    counts["<top>"] = 8.0  # once per wave
+  loop_ctr = {key: loop_counter(blocks, key) for key in loops if key != "<top>"}
+  loop_ctr["<top>"] = "<top>"
   dyn = collections.defaultdict(collections.Counter)
+  if counts:
+    for b in blocks:
+      key = b["loop"] or "<top>"
+      ph_b = collections.Counter(phase_of(loc) for _, loc in b["insts"])
+      name = loop_ctr.get(key)
+      major = ph_b.most_common(1)[0][0] if ph_b else None
+      if block_rare(b):
+        name = "zero"
+      elif major in BLOCK_COUNTERS and not (major == "slow_raster" and str(name).startswith("slow")):
+        name = BLOCK_COUNTERS[major]
+      trip = name if isinstance(name, float) else counts.get(name)
+      if trip is None:
+        print("  no counter for block %s (loop %s, %s): %d instructions" % (
+            b["label"], key, name, len(b["insts"])))
+        continue
+      for op, loc in b["insts"]:
+        dyn[phase_of(loc)][iclass(op)] += trip
   rows = []
   for key, info in sorted(loops.items(), key=lambda kv: (kv[1]["depth"], kv[0])):
     c = per_loop[key]
@@ -209,17 +368,15 @@ def main():
     v = sum(n for (p, cl), n in c.items() if cl == "VALU")
     s = sum(n for (p, cl), n in c.items() if cl == "SALU")
     l = sum(n for (p, cl), n in c.items() if cl == "LDS")
-    trip = counts.get(key)
+    lc = loop_ctr.get(key)
+    trip = (lc if isinstance(lc, float) else counts.get(lc)) if counts else None
     rows.append({"loop": key, "depth": info["depth"], "parents": info["parents"], "phase": ph,
                  "blocks": info["blocks"], "valu": v, "salu": s, "lds": l, "trip_per_tuple": trip})
-    print("%-10s d%d %-18s blocks %3d  VALU %4d SALU %4d LDS %3d  parents %s%s" % (
-        key, info["depth"], ph, info["blocks"], v, s, l, ",".join(info["parents"]),
+    print("%-10s d%d %-18s blocks %3d  VALU %4d SALU %4d LDS %3d  %-16s%s" % (
+        key, info["depth"], ph, info["blocks"], v, s, l, loop_ctr.get(key),
         "" if trip is None else "  trips/tuple %.1f" % trip))
-    if trip is not None:
-      for (p, cl), n in c.items():
-        dyn[p][cl] += n * trip
   if counts:
-    print("\ndynamic estimate per tuple (static body x wave-level trips):")
+    print("\ndynamic estimate per tuple (each block's static count x its loop's wave-level trips):")
     tot = collections.Counter()
     for p, c in sorted(dyn.items(), key=lambda kv: -kv[1]["VALU"]):
       tot.update(c)
