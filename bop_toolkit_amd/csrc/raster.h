@@ -67,7 +67,7 @@ __device__ __forceinline__ RVtx r_vertex(const float* __restrict__ Rf, const Cam
   const float Z = ((Rf[6] * x + Rf[7] * y) + Rf[8] * z) + Rf[11];
   // Branch-free: every lane computes the projection, invalid ones are
   // replaced by the sentinel afterwards (same values as an early return).
-  const float iz = rcp_rn(Z);  // the one IEEE division per vertex (spec v4)
+  const float iz = rcp_rn(Z);  // the one IEEE division per vertex (spec v5)
   const float u = (c.fx * X) * iz + c.cx;
   const float v = (c.fy * Y) * iz + c.cy;
   const bool ok = (int)(Z > 0.0f) & (int)(fabsf(u) <= kGuardBand) & (int)(fabsf(v) <= kGuardBand);

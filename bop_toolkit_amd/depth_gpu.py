@@ -133,6 +133,119 @@ class DepthDecoder:
     return frames
 
 
+class GroupPrefetch:
+  """Test depth of consecutive scenes decoded in shared launches, ahead of use.
+
+  A scene's frames alone leave most of the chip idle during k_png_inflate (one
+  wave per stream: a launch takes one stream's latency, ~70 ms for 640x480
+  frames, whether it holds 100 or 5,000 streams). A worker thread walks the
+  scenes in order, collects their PNG paths (items: (key, thunk), thunk() ->
+  (paths, scales), run in the worker) until a group holds max_frames frames,
+  and decodes the group with one DepthDecoder.load on `stream`; each scene
+  gets its slice of the group's frames. At most max_groups decoded groups wait
+  for their consumer (device memory bound). get(key) blocks until the scene's
+  frames are final and returns them (None: no images; raises the decoder's
+  ValueError for a group it could not take, e.g. a frame of another size).
+  """
+
+  def __init__(self, device, items, H, W, torch, stream, consumer, max_frames=4096, max_groups=2):
+    import concurrent.futures as cf
+    import threading
+    self._torch = torch
+    self._items = list(items)
+    self._fut = {k: cf.Future() for k, _ in self._items}
+    self._left = {}  # group id -> keys not yet taken
+    self._group_of = {}
+    self._sem = threading.Semaphore(max_groups)
+    self._lock = threading.Lock()
+    self._stop = False
+    self.H, self.W, self.max_frames = int(H), int(W), int(max_frames)
+    self.stream, self.consumer, self.device = stream, consumer, device
+    self.groups = 0
+    self._thread = threading.Thread(target=self._run, name="bopx-depth-groups", daemon=True)
+    self._thread.start()
+
+  def _run(self):
+    dec = None
+    pending, n = [], 0
+    try:
+      for key, thunk in self._items:
+        if self._stop:
+          break
+        try:
+          paths, scales = thunk()
+        except BaseException as e:  # noqa: BLE001 - the consumer re-raises it
+          self._fut[key].set_exception(e)
+          continue
+        if not paths:
+          self._fut[key].set_result(None)
+          continue
+        pending.append((key, paths, scales))
+        n += len(paths)
+        if n >= self.max_frames:
+          dec = self._flush(pending, dec)
+          pending, n = [], 0
+      if pending and not self._stop:
+        self._flush(pending, dec)
+    finally:
+      for f in self._fut.values():
+        if not f.done():
+          f.set_exception(RuntimeError("depth prefetch stopped"))
+
+  def _flush(self, pending, dec):
+    torch = self._torch
+    self._sem.acquire()
+    if self._stop:
+      return dec
+    if dec is None:
+      dec = DepthDecoder(self.device)
+    paths = [q for _, ps, _ in pending for q in ps]
+    scales = [c for _, _, cs in pending for c in cs]
+    gid = self.groups
+    self.groups += 1
+    with self._lock:
+      self._left[gid] = len(pending)
+      for key, _, _ in pending:
+        self._group_of[key] = gid
+    try:
+      with torch.cuda.stream(self.stream):
+        frames = dec.load(paths, scales, self.H, self.W, torch)
+      frames.record_stream(self.consumer)  # freed behind the consumer's use
+    except BaseException as e:  # noqa: BLE001
+      for key, _, _ in pending:
+        self._fut[key].set_exception(e)
+      return dec
+    o = 0
+    for key, ps, _ in pending:
+      self._fut[key].set_result(frames[o:o + len(ps)])
+      o += len(ps)
+    return dec
+
+  def get(self, key):
+    try:
+      return self._fut[key].result()
+    finally:
+      with self._lock:
+        gid = self._group_of.pop(key, None)
+        if gid is not None:
+          self._left[gid] -= 1
+          if self._left[gid] == 0:
+            del self._left[gid]
+            self._sem.release()
+
+  def close(self):
+    self._stop = True
+    self._sem.release()
+    self._thread.join(timeout=60)
+
+  def __enter__(self):
+    return self
+
+  def __exit__(self, *exc):
+    self.close()
+    return False
+
+
 def raw_stride_of(H, W):
   """bopx_png_decode_dev's per-frame scratch: the inflated rows + 64, in KiB."""
   return (H * (2 * W + 1) + 64 + RAW_ALIGN - 1) // RAW_ALIGN * RAW_ALIGN

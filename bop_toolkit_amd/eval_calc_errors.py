@@ -26,6 +26,7 @@ reference. The HIP rasteriser replaces the OpenGL renderer, whatever
 import argparse
 import copy
 import os
+import threading
 import time
 
 import numpy as np
@@ -56,6 +57,9 @@ POINT_ERRORS = ("ad", "add", "adi", "mssd", "mspd", "proj")
 # the shared-render path (batch.BatchEvaluator.vsd_shared); one instance per
 # object (2 renders per tuple) keeps the fused per-tuple kernel
 SHARED_RENDER_RATIO = float(os.environ.get("BOPX_SHARED_RENDER_RATIO", "1.5"))
+# VSD test depth of consecutive scenes decoded in shared k_png_inflate launches
+# of about this many frames (depth_gpu.GroupPrefetch; 0: one launch per scene)
+DEPTH_GROUP_FRAMES = int(os.environ.get("BOPX_DEPTH_GROUP_FRAMES", "4096"))
 ERROR_TYPES = ("vsd", "mssd", "mspd", "ad", "add", "adi", "cus", "proj", "rete", "re", "te")
 
 
@@ -107,6 +111,21 @@ def log(s):
 # returned objects as read-only.
 _FILE_CACHE = {}
 _FILE_CACHE_MAX = 512
+_KEY_LOCKS = {}
+_KEY_LOCKS_LOCK = threading.Lock()
+
+
+def _key_lock(key):
+  """One lock per cache key: a file (or a scene's arrays) requested by two
+  threads at once (the scene prefetch and the depth-group thread) is parsed
+  once and both get the same object (the identity-keyed caches rely on it)."""
+  with _KEY_LOCKS_LOCK:
+    lk = _KEY_LOCKS.get(key)
+    if lk is None:
+      if len(_KEY_LOCKS) >= 8192:
+        _KEY_LOCKS.clear()
+      lk = _KEY_LOCKS[key] = threading.Lock()
+    return lk
 
 
 def cached_load(loader, path, **kw):
@@ -115,9 +134,12 @@ def cached_load(loader, path, **kw):
          tuple(sorted(kw.items())))
   hit = _FILE_CACHE.get(key)
   if hit is None:
-    if len(_FILE_CACHE) >= _FILE_CACHE_MAX:
-      _FILE_CACHE.pop(next(iter(_FILE_CACHE)))
-    hit = _FILE_CACHE[key] = loader(path, **kw)
+    with _key_lock(key):
+      hit = _FILE_CACHE.get(key)
+      if hit is None:
+        if len(_FILE_CACHE) >= _FILE_CACHE_MAX:
+          _FILE_CACHE.pop(next(iter(_FILE_CACHE)))
+        hit = _FILE_CACHE[key] = loader(path, **kw)
   return hit
 
 
@@ -584,14 +606,15 @@ def scene_arrays_direct_cached(p, scene_id, scene_targets, ests_org, scene_gt):
   """scene_arrays_direct shared by the error types of one BOP19 run (keyed like
   scene_records_cached; callers treat the arrays as read-only)."""
   key = (scene_id, id(scene_targets), id(ests_org), id(scene_gt), p["n_top"], p["skip_missing"])
-  hit = _DIRECT_CACHE.get(key)
-  if hit is not None and hit[0] is scene_targets and hit[1] is ests_org and hit[2] is scene_gt:
-    return hit[3]
-  out = scene_arrays_direct(p, scene_id, scene_targets, ests_org, scene_gt)
-  if len(_DIRECT_CACHE) >= 4096:
-    _DIRECT_CACHE.clear()
-  _DIRECT_CACHE[key] = (scene_targets, ests_org, scene_gt, out)
-  return out
+  with _key_lock(("direct",) + key):
+    hit = _DIRECT_CACHE.get(key)
+    if hit is not None and hit[0] is scene_targets and hit[1] is ests_org and hit[2] is scene_gt:
+      return hit[3]
+    out = scene_arrays_direct(p, scene_id, scene_targets, ests_org, scene_gt)
+    if len(_DIRECT_CACHE) >= 4096:
+      _DIRECT_CACHE.clear()
+    _DIRECT_CACHE[key] = (scene_targets, ests_org, scene_gt, out)
+    return out
 
 
 _ARR_CACHE = {}
@@ -826,6 +849,27 @@ def run(p, device=0):
         depths = d
       return depths
 
+    scenes = list(targets_org.items())
+    groups = None
+    if arrays and et == "vsd" and up is not None and depth_gpu.enabled() and DEPTH_GROUP_FRAMES > 0:
+      def scene_images(scene_id, scene_targets):
+        # the images prepare() will ask for (the same cached arrays and plan)
+        scene_camera = cached_load(inout.load_scene_camera,
+                                   dp_split["scene_camera_tpath"].format(scene_id=scene_id))
+        scene_gt = cached_load(inout.load_scene_gt,
+                               dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+        arr, _ = scene_arrays_direct_cached(p, scene_id, scene_targets, ests_org, scene_gt)
+        _, todo = plan_arrays(p, arr, models_info)
+        if not len(todo):
+          return [], []
+        ims = np.unique(arr["rec_im"][arr["pair_ri"][todo]]).tolist()
+        return scene_depth_paths(dp_split, scene_camera, scene_id, ims)
+      W_, H_ = dp_split["im_size"]
+      groups = depth_gpu.GroupPrefetch(
+          ev.device.index or 0,
+          [(sid, (lambda sid=sid, st=st: scene_images(sid, st))) for sid, st in scenes],
+          H_, W_, torch, up[0], up[1], max_frames=DEPTH_GROUP_FRAMES)
+
     def prepare(scene_id, scene_targets):
       # host side of one scene: annotations, records, gates, this rank's share
       # of the tuples and (VSD) its test-depth PNGs, decoded while the previous
@@ -841,8 +885,14 @@ def run(p, device=0):
         vals, todo = plan_arrays(p, arr, models_info)
         depths = None
         if et == "vsd" and len(todo):
-          depths = prefetch_depths(
-              np.unique(arr["rec_im"][arr["pair_ri"][todo]]).tolist(), scene_id, scene_camera)
+          if groups is not None:
+            try:
+              depths = groups.get(scene_id)
+            except ValueError:
+              depths = None  # a frame of another size in the group: per-scene path
+          if depths is None:
+            depths = prefetch_depths(
+                np.unique(arr["rec_im"][arr["pair_ri"][todo]]).tolist(), scene_id, scene_camera)
         planned = ("arrays", arr, vals, todo, depths)
         return scene_camera, recs, n_ests, planned
       recs, n_ests = scene_records_cached(p, scene_id, scene_targets, ests_org, scene_gt)
@@ -856,9 +906,9 @@ def run(p, device=0):
         planned = (errs, todo, mine, depths)
       return scene_camera, recs, n_ests, planned
 
+    import contextlib
     from concurrent.futures import ThreadPoolExecutor
-    scenes = list(targets_org.items())
-    with ThreadPoolExecutor(1) as ahead:
+    with ThreadPoolExecutor(1) as ahead, (groups or contextlib.nullcontext()):
       nxt = ahead.submit(prepare, *scenes[0]) if scenes else None
       for k, (scene_id, scene_targets) in enumerate(scenes):
         scene_camera, recs, n_ests, planned = nxt.result()

@@ -1,0 +1,105 @@
+"""depth_gpu.GroupPrefetch (CPU, a stand-in decoder): scenes' frames decoded
+in shared groups of about max_frames, each scene gets exactly its slice in
+order, scenes without images get None, a failing group raises for its scenes
+only, and at most max_groups decoded groups wait for their consumer."""
+import contextlib
+import threading
+import time
+import types
+
+import numpy as np
+import pytest
+
+from bop_toolkit_amd import depth_gpu
+
+
+class _Frames:
+  def __init__(self, arr):
+    self.arr = arr
+
+  def __getitem__(self, sl):
+    return _Frames(self.arr[sl])
+
+  def __len__(self):
+    return len(self.arr)
+
+  def record_stream(self, s):
+    pass
+
+
+def _fake_torch():
+  return types.SimpleNamespace(cuda=types.SimpleNamespace(stream=lambda s: contextlib.nullcontext()))
+
+
+@pytest.fixture
+def fake_decoder(monkeypatch):
+  calls = []
+
+  class Dec:
+    def __init__(self, device):
+      pass
+
+    def load(self, paths, scales, H, W, torch):
+      if any(p.startswith("bad") for p in paths):
+        raise ValueError("frame of another size")
+      calls.append(list(paths))
+      arr = np.array([[int(p.split(":")[1])] for p in paths])  # one value per frame
+      return _Frames(arr)
+  monkeypatch.setattr(depth_gpu, "DepthDecoder", Dec)
+  return calls
+
+
+def _scene(k, n):
+  return (k, lambda: (["s%d:%d" % (k, 100 * k + i) for i in range(n)], [0.1] * n))
+
+
+def test_groups_and_slices(fake_decoder):
+  sizes = [3, 0, 5, 2, 7, 1]
+  g = depth_gpu.GroupPrefetch(0, [_scene(k, n) for k, n in enumerate(sizes)], 4, 4,
+                              _fake_torch(), None, None, max_frames=6, max_groups=2)
+  with g:
+    for k, n in enumerate(sizes):
+      f = g.get(k)
+      if n == 0:
+        assert f is None
+      else:
+        assert [int(v) for v in f.arr[:, 0]] == [100 * k + i for i in range(n)]
+  # groups close once they hold >= 6 frames: [3, 5] -> 8, [2, 7] -> 9, [1]
+  assert [len(c) for c in fake_decoder] == [8, 9, 1]
+
+
+def test_failing_group_raises_for_its_scenes_only(fake_decoder):
+  items = [_scene(0, 4), (1, lambda: (["bad:0"], [1.0])), _scene(2, 5), _scene(3, 2)]
+  with depth_gpu.GroupPrefetch(0, items, 4, 4, _fake_torch(), None, None, max_frames=5) as g:
+    with pytest.raises(ValueError):
+      g.get(0)
+    with pytest.raises(ValueError):
+      g.get(1)
+    assert len(g.get(2)) == 5
+    assert len(g.get(3)) == 2
+
+
+def test_thunk_error_reaches_the_consumer(fake_decoder):
+  def boom():
+    raise KeyError("scene_gt")
+  with depth_gpu.GroupPrefetch(0, [_scene(0, 2), (1, boom), _scene(2, 2)], 4, 4, _fake_torch(),
+                               None, None, max_frames=2) as g:
+    assert len(g.get(0)) == 2
+    with pytest.raises(KeyError):
+      g.get(1)
+    assert len(g.get(2)) == 2
+
+
+def test_at_most_max_groups_wait(fake_decoder):
+  items = [_scene(k, 4) for k in range(8)]
+  g = depth_gpu.GroupPrefetch(0, items, 4, 4, _fake_torch(), None, None, max_frames=4,
+                              max_groups=2)
+  try:
+    time.sleep(0.3)
+    assert len(fake_decoder) == 2  # nothing taken yet: two groups decoded, the worker waits
+    g.get(0)
+    time.sleep(0.3)
+    assert len(fake_decoder) == 3
+  finally:
+    g.close()
+  assert not g._thread.is_alive()
