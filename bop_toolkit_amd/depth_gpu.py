@@ -19,6 +19,8 @@ the host, which gives the host path's own result or raises its own error.
 """
 import ctypes
 import os
+import threading
+import time
 
 import numpy as np
 
@@ -27,6 +29,20 @@ from . import _lib, inout
 RAW_ALIGN = 1024      # bopx_png_decode_dev's raw_stride granule
 MAX_WIDTH = 4096      # kern_png.hip's carry row (bopx_internal.h kPngMaxWidth)
 MAX_RAW = 1 << 28     # inflated bytes per frame (bopx_internal.h kPngMaxRaw)
+
+
+# Cumulative wall time of DepthDecoder.load's steps over all decoders
+# (diagnostics for tools/e2e_bench.py): pack = reading and checking the files
+# on host threads; decode = upload + kernels + status readback; host = frames
+# the device did not take.
+STATS = {"calls": 0, "frames": 0, "pack_s": 0.0, "decode_s": 0.0, "host_s": 0.0}
+_STATS_LOCK = threading.Lock()
+
+
+def _stat(**kw):
+  with _STATS_LOCK:
+    for k, v in kw.items():
+      STATS[k] += v
 
 
 def enabled():
@@ -107,7 +123,9 @@ class DepthDecoder:
       return frames
     sc = np.ones(n, np.float32) if scales is None else np.asarray(
         [np.float32(float(s)) for s in scales], np.float32)
+    t0 = time.perf_counter()
     buf, need, z_off, z_len, st = pack(paths, H, W, lambda nb: self._staging(torch, nb), workers)
+    t1 = time.perf_counter()
     stream = torch.cuda.current_stream(dev)
     z_d = buf[:need].to(dev, non_blocking=True)
     off_d = torch.from_numpy(z_off).to(dev)
@@ -121,6 +139,7 @@ class DepthDecoder:
                   status.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
     gst = status.view(n, 2)[:, 0].cpu().numpy()  # synchronises: staging reusable after this
     del raw, z_d
+    t2 = time.perf_counter()
     host = np.nonzero((st != 0) | (gst != 0))[0]
     if len(host):
       arr = _host_frames([paths[k] for k in host], None if scales is None else
@@ -130,6 +149,7 @@ class DepthDecoder:
       # streams (the scene prefetch threads), so the frames are final on return
       stream.synchronize()
     self.last_host = len(host)
+    _stat(calls=1, frames=n, pack_s=t1 - t0, decode_s=t2 - t1, host_s=time.perf_counter() - t2)
     return frames
 
 

@@ -57,9 +57,13 @@ POINT_ERRORS = ("ad", "add", "adi", "mssd", "mspd", "proj")
 # the shared-render path (batch.BatchEvaluator.vsd_shared); one instance per
 # object (2 renders per tuple) keeps the fused per-tuple kernel
 SHARED_RENDER_RATIO = float(os.environ.get("BOPX_SHARED_RENDER_RATIO", "1.5"))
-# VSD test depth of consecutive scenes decoded in shared k_png_inflate launches
-# of about this many frames (depth_gpu.GroupPrefetch; 0: one launch per scene)
-DEPTH_GROUP_FRAMES = int(os.environ.get("BOPX_DEPTH_GROUP_FRAMES", "4096"))
+
+
+def depth_group_frames():
+  """VSD test depth of consecutive scenes is decoded in shared k_png_inflate
+  launches of about this many frames (depth_gpu.GroupPrefetch;
+  BOPX_DEPTH_GROUP_FRAMES=0: one launch per scene, from the scene prefetch)."""
+  return int(os.environ.get("BOPX_DEPTH_GROUP_FRAMES", "4096"))
 ERROR_TYPES = ("vsd", "mssd", "mspd", "ad", "add", "adi", "cus", "proj", "rete", "re", "te")
 
 
@@ -851,7 +855,7 @@ def run(p, device=0):
 
     scenes = list(targets_org.items())
     groups = None
-    if arrays and et == "vsd" and up is not None and depth_gpu.enabled() and DEPTH_GROUP_FRAMES > 0:
+    if arrays and et == "vsd" and up is not None and depth_gpu.enabled() and depth_group_frames() > 0:
       def scene_images(scene_id, scene_targets):
         # the images prepare() will ask for (the same cached arrays and plan)
         scene_camera = cached_load(inout.load_scene_camera,
@@ -868,7 +872,7 @@ def run(p, device=0):
       groups = depth_gpu.GroupPrefetch(
           ev.device.index or 0,
           [(sid, (lambda sid=sid, st=st: scene_images(sid, st))) for sid, st in scenes],
-          H_, W_, torch, up[0], up[1], max_frames=DEPTH_GROUP_FRAMES)
+          H_, W_, torch, up[0], up[1], max_frames=depth_group_frames())
 
     def prepare(scene_id, scene_targets):
       # host side of one scene: annotations, records, gates, this rank's share

@@ -149,6 +149,8 @@ def main():
   ap.add_argument("--profile", action="store_true")
   ap.add_argument("--instances", type=int, default=1,
                   help="instances (and estimates) per object and image; > 1: multi-instance")
+  ap.add_argument("--ab-group", action="store_true",
+                  help="with --ab-depth: warm runs with per-scene and grouped GPU decode launches")
   ap.add_argument("--ab-depth", action="store_true",
                   help="evaluate twice: test depth decoded on the GPU, then on the host "
                        "(BOPX_DEPTH_GPU=0); both timings and identical scores reported")
@@ -222,26 +224,40 @@ def main():
     with open(os.path.join(REPO, "gpurun_out", "e2e_profile.txt"), "w") as f:
       f.write(s.getvalue())
   scores = final[os.path.splitext(result)[0]]
+  first_stats = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in depth_gpu.STATS.items()}
   ab = None
   if a.ab_depth:  # warm runs (annotation caches filled by the first): host decoder, then GPU
     first_phases, first_err = dict(phases), dict(err_t)
     ab = {}
-    for name, env in (("host_decode_warm", "0"), ("gpu_decode_warm", "1")):
+    runs = (("host_decode_warm", "0", None), ("gpu_decode_warm", "1", None))
+    if a.ab_group:  # per-scene decode launches vs shared launches of ~4,096 frames
+      runs = (("gpu_decode_per_scene_warm", "1", "0"), ("gpu_decode_grouped_warm", "1", "4096"),
+              ("gpu_decode_per_scene_warm2", "1", "0"), ("gpu_decode_grouped_warm2", "1", "4096"))
+    for name, env, grp in runs:
+      if grp is None:
+        os.environ.pop("BOPX_DEPTH_GROUP_FRAMES", None)
+      else:
+        os.environ["BOPX_DEPTH_GROUP_FRAMES"] = grp
       for k in list(phases):
         if k.startswith("host:"):
           phases[k] = 0.0
       err_t.clear()
+      for k in depth_gpu.STATS:
+        depth_gpu.STATS[k] = 0 if k in ("calls", "frames") else 0.0
       os.environ["BOPX_DEPTH_GPU"] = env
       t0 = time.perf_counter()
       fin = eval_bop19_pose.evaluate(p)
       t_run = time.perf_counter() - t0
       ab[name] = {"eval_bop19_s": round(t_run, 2),
+                  "depth_decoder": {k: (round(v, 3) if isinstance(v, float) else v)
+                                    for k, v in depth_gpu.STATS.items()},
                   "errors_s": {k: round(v, 2) for k, v in err_t.items()},
                   "host_s": {k[5:]: round(v, 3) for k, v in phases.items()
                              if k.startswith("host:") and v},
                   "eval_tuples_per_s": n / t_run,
                   "identical_scores": fin[os.path.splitext(result)[0]] == scores}
     os.environ.pop("BOPX_DEPTH_GPU")
+    os.environ.pop("BOPX_DEPTH_GROUP_FRAMES", None)
     phases.clear()
     phases.update(first_phases)
     err_t.clear()
@@ -257,6 +273,7 @@ def main():
       "host_s": {k[5:]: round(v, 3) for k, v in phases.items() if k.startswith("host:")},
       "eval_tuples_per_s": n / t_eval,
       "depth_decoder": "gpu" if depth_gpu.enabled() else "host", "ab_depth": ab,
+      "depth_decoder_first_run": first_stats,
       "ar": {k: round(float(v), 4) for k, v in scores.items()}}))
 
 
