@@ -655,9 +655,10 @@ def plan_arrays(p, arr, models_info):
 
 
 def evaluate_batch_arrays(ev, torch, p, dataset, dp_split, scene_camera, scene_id, arr, todo,
-                          models_info, depths=None):
+                          models_info, depths=None, depth_ims=None):
   """evaluate_batch on the arrays: the GPU rows [len(todo), n_values] of the
-  pairs todo (depths: the frames of their sorted images, or None)."""
+  pairs todo (depths: the frames of their sorted images, or None; with
+  depth_ims, the frames of those sorted image ids, a superset)."""
   et = p["error_type"]
   dev = ev.device
   ri = arr["pair_ri"][todo]
@@ -669,6 +670,14 @@ def evaluate_batch_arrays(ev, torch, p, dataset, dp_split, scene_camera, scene_i
   ims, inv = np.unique(arr["rec_im"][ri], return_inverse=True)  # todo_images order
   Ks = [np.asarray(scene_camera[im]["cam_K"], np.float64).reshape(3, 3) for im in ims.tolist()]
   if et == "vsd":
+    if depths is not None and depth_ims is not None:
+      depth_ims = np.asarray(depth_ims, np.int64)
+      pos = np.searchsorted(depth_ims, ims)
+      if len(ims) and (pos.max() >= len(depth_ims) or not np.array_equal(depth_ims[pos], ims)):
+        raise ValueError("depth frames do not cover the batch's images")
+      Ks = [np.asarray(scene_camera[im]["cam_K"], np.float64).reshape(3, 3)
+            for im in depth_ims.tolist()]
+      inv = pos[inv]
     cam = np.array([[K[0, 0], K[1, 1], K[0, 2], K[1, 2]] for K in Ks], np.float64)
     fidx_h = inv.astype(np.int32)
     if depths is None:
@@ -857,18 +866,18 @@ def run(p, device=0):
     groups = None
     if arrays and et == "vsd" and up is not None and depth_gpu.enabled() and depth_group_frames() > 0:
       def scene_images(scene_id, scene_targets):
-        # the images prepare() will ask for (the same cached arrays and plan)
+        # every target image of the scene that has estimates (a superset of the
+        # images of the scene's VSD batch: gated pairs may leave some out; the
+        # batch maps its tuples to these frames, evaluate_batch_arrays)
         scene_camera = cached_load(inout.load_scene_camera,
                                    dp_split["scene_camera_tpath"].format(scene_id=scene_id))
-        scene_gt = cached_load(inout.load_scene_gt,
-                               dp_split["scene_gt_tpath"].format(scene_id=scene_id))
-        arr, _ = scene_arrays_direct_cached(p, scene_id, scene_targets, ests_org, scene_gt)
-        _, todo = plan_arrays(p, arr, models_info)
-        if not len(todo):
-          return [], []
-        ims = np.unique(arr["rec_im"][arr["pair_ri"][todo]]).tolist()
+        se = ests_org.get(scene_id, {})
+        ims = sorted(im for im, tg in scene_targets.items()
+                     if any(se.get(im, {}).get(o) for o in tg))
+        group_ims[scene_id] = ims
         return scene_depth_paths(dp_split, scene_camera, scene_id, ims)
       W_, H_ = dp_split["im_size"]
+      group_ims = {}
       groups = depth_gpu.GroupPrefetch(
           ev.device.index or 0,
           [(sid, (lambda sid=sid, st=st: scene_images(sid, st))) for sid, st in scenes],
@@ -887,17 +896,19 @@ def run(p, device=0):
         arr, n_ests = scene_arrays_direct_cached(p, scene_id, scene_targets, ests_org, scene_gt)
         recs = None
         vals, todo = plan_arrays(p, arr, models_info)
-        depths = None
+        depths = depth_ims = None
         if et == "vsd" and len(todo):
           if groups is not None:
             try:
               depths = groups.get(scene_id)
+              depth_ims = group_ims.get(scene_id)
             except ValueError:
               depths = None  # a frame of another size in the group: per-scene path
           if depths is None:
+            depth_ims = None
             depths = prefetch_depths(
                 np.unique(arr["rec_im"][arr["pair_ri"][todo]]).tolist(), scene_id, scene_camera)
-        planned = ("arrays", arr, vals, todo, depths)
+        planned = ("arrays", arr, vals, todo, (depths, depth_ims))
         return scene_camera, recs, n_ests, planned
       recs, n_ests = scene_records_cached(p, scene_id, scene_targets, ests_org, scene_gt)
       if recs:
@@ -922,10 +933,10 @@ def run(p, device=0):
             et, method, dataset, split_type_str, scene_id))
         ests_counter += n_ests
         if arrays:
-          _, arr, vals, todo, depths = planned
+          _, arr, vals, todo, (depths, depth_ims) = planned
           if len(todo):
             rows = evaluate_batch_arrays(ev, torch, p, dataset, dp_split, scene_camera,
-                                         scene_id, arr, todo, models_info, depths)
+                                         scene_id, arr, todo, models_info, depths, depth_ims)
             vals[todo] = rows.cpu().numpy()
           if et == "vsd":  # one file per tau (:401-415)
             signs = [misc.get_error_signature(et, p["n_top"], vsd_delta=p["vsd_deltas"][dataset],
