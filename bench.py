@@ -92,6 +92,9 @@ def parse():
   ap.add_argument("--cpu-seconds", type=float, default=10.0,
                   help="target wall time of the CPU-baseline sample")
   ap.add_argument("--no-cpu-baseline", action="store_true")
+  ap.add_argument("--e2e-images", type=int, default=None,
+                  help="images of the end-to-end drop-in run after the timed region (default "
+                       "4,002 for configs[3] at N=1, else 0 = none)")
   ap.add_argument("--seed", type=int, default=20250220 + 4)
   args = ap.parse_args()
   cfg = CONFIGS[args.config]
@@ -491,6 +494,37 @@ def cpu_baseline(objs, d, n, seconds, gpu=None):
   return out
 
 
+def e2e_run(images, seed, timeout=420):
+  """The drop-in evaluation end to end, after the timed region: a YCB-V-layout
+  dataset of `images` 640x480 images with 6 of configs[3]'s kind of objects
+  each (21 superellipsoids of 5,002 vertices, Pillow-written 16-bit depth
+  PNGs, a BOP19 results CSV) written to local disk, then calc_gt_info and ONE
+  cold eval_bop19_pose (VSD + MSSD + MSPD errors and the 120 score settings)
+  in a fresh process (tools/e2e_bench.py, a child of this one). Returns the
+  child's JSON summary (tuples/s of eval_bop19_pose, phases, recalls)."""
+  import shutil
+  import subprocess
+  root = os.path.join(os.environ.get("TMPDIR", "/tmp"), "bopx_bench_e2e_%d" % os.getpid())
+  try:
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "e2e_bench.py"), "--images",
+                        str(images), "--root", root, "--seed", str(seed)],
+                       capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+      return {"error": "e2e_bench exit %d: %s" % (r.returncode, r.stderr[-400:])}
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+  except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+    return {"error": repr(e)[:400]}
+  finally:
+    shutil.rmtree(root, ignore_errors=True)
+  keep = ("images", "tuples", "eval_bop19_s", "eval_tuples_per_s", "calc_gt_info_s", "errors_s",
+          "scores_s", "host_s", "gen_s", "depth_decoder", "depth_decoder_first_run", "ar")
+  res = {k: out[k] for k in keep if k in out}
+  res["note"] = ("cold: one drop-in eval_bop19_pose (errors VSD/MSSD/MSPD + 120 score settings) "
+                 "in a fresh process on PNG files on local disk; tuples/s = its tuples / its wall "
+                 "time; calc_gt_info separate")
+  return res
+
+
 def cpu_baseline_point(objs, d, n):
   """configs[0] on the host: the oracle's ADD and brute-force ADI (C restatement
   of pose_error.py:147-184), one tuple after the other on one core."""
@@ -675,6 +709,10 @@ def main():
       cpu = cpu_baseline(objs, d, n, args.cpu_seconds, (out_vsd, out_mssd, out_mspd))
     elif world == 1 and not args.no_cpu_baseline and args.cfg["errors"] == ("add", "adi"):
       cpu = cpu_baseline_point(objs, d, n)
+    e2e_images = args.e2e_images
+    if e2e_images is None:
+      e2e_images = 4002 if args.config == 3 and world == 1 and "multi" not in args.cfg else 0
+    e2e = e2e_run(e2e_images, args.seed) if e2e_images > 0 and world == 1 else None
     line = {
         "metric": "pose-error tuples/sec (%s) at %dx%d, ~%dk-vert meshes" % (
             "+".join(e.upper() for e in args.cfg["errors"]), W, H,
@@ -693,7 +731,7 @@ def main():
                    "tuples_rank0": n,
                    "roi_mean_px": round(cost["roi_mean"], 1),
                    **({"axes_scale": args.axes_scale} if args.axes_scale != 1.0 else {})},
-        "roofline": roof, "kernels": kernels, "cpu_baseline": cpu}
+        "roofline": roof, "kernels": kernels, "cpu_baseline": cpu, "e2e": e2e}
     if multi:
       rd = d["renders"]
       if roof is not None and roof["kernel"] == "k_vsd":
