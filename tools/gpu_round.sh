@@ -13,6 +13,6 @@ timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { echo "bench failed"; tail -30 gpurun_out/bench_${TAG}.err; exit 1; }
 cat gpurun_out/bench_${TAG}.json
 if [ -n "${PROFILE}" ]; then
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/prof_${TAG}.log 2>&1 || { echo "rocprof failed"; tail -30 gpurun_out/prof_${TAG}.log; exit 1; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python3 bench.py --no-cpu-baseline --e2e-images 0 ${BENCH_ARGS} > gpurun_out/prof_${TAG}.log 2>&1 || { echo "rocprof failed"; tail -30 gpurun_out/prof_${TAG}.log; exit 1; }
   find gpurun_out/prof_${TAG} -name "*stats*" | head
 fi

@@ -43,6 +43,7 @@ FUNCS = {  # device function -> phase
     "filt_b": "coeffs_touch", "filt_thr": "prologue", "step_threshold": "prologue",
     "meshlet_rect": "prologue", "wave_max_nonneg_f32": "prologue", "region_min8": "cull",
     "region_covered": "cull", "make_region": "cull", "wave_incl_scan": "setup",
+    "r_regular": "large", "r_floor_div256": "slow_raster",
     "wave_sum_u32": "epilogue", "wave_sum_f64": "epilogue",
 }
 REGIONS = [  # (start, stop, phase) inside k_vsd
@@ -119,6 +120,15 @@ def ranges():
         ph.append((fname, r[0], r[1], phase))
   k = src["kern_vsd.hip"]
   reg = [("kern_vsd.hip",) + _region(k, a, b) + (p,) for a, b, p in REGIONS]
+  r = src["raster.h"]
+  big = "if (__builtin_expect(__builtin_amdgcn_ballot_w64(!t.small) != 0, 0)) {"
+  i0 = next(i for i, l in enumerate(r) if big in l)
+  i1 = next(i for i in range(i0 + 1, len(r)) if big in r[i])
+  reg += [("raster.h", i0 + 1, _region(r[i0:], big, "const RVtx b = neg ? c0 : b0")[1] + i0, "large"),
+          ("raster.h", i1 + 1, _region(r[i1:], big, "const RVtx s[3]")[1] + i1, "large"),
+          # r_raster's int64 edges (triangles of >= 128 px extent)
+          ("raster.h",) + _region(r, "const int64_t py = 256 * (int64_t)row + 128;",
+                                  "// Row items (the k_vsd fast path)") + ("large",)]
   _RANGES["phases"] = reg + ph  # k_vsd regions first (lambdas inside k_vsd), then functions
   for a, b, name in LOOP_REGIONS:
     if a == "func":
@@ -287,17 +297,54 @@ def loop_counter(blocks, header):
 
 def block_rare(b):
   """Blocks of the IEEE division fall-back of rcp_rn (inputs outside the
-  normal range) and the diag-free error paths: not executed on the bench."""
-  return any(op.startswith(("v_div_fmas", "v_div_scale", "v_div_fixup")) for op, _ in b["insts"])
+  normal range): not executed on the bench."""
+  if any(op.startswith(("v_div_fmas", "v_div_scale", "v_div_fixup")) for op, _ in b["insts"]):
+    return True
+  locs = [loc for _, loc in b["insts"] if loc]
+  rcp = _func_range(_lines(os.path.join(os.path.dirname(SRC), "raster.h")), "rcp_rn")
+  # `return ok ? r : 1.0f / x` alone (the ballot-guarded IEEE branch)
+  return bool(locs) and rcp is not None and all(
+      l[0] == "raster.h" and l[1] == rcp[1] - 2 for l in locs)
+
+
+def _fine(loc):
+  """Lines of the float64 per-pixel sequence (dist_of, sqrt_depth, visib19t,
+  vsd_exact_px): in k_vsd's step-cost pixel loop only the exact path uses them."""
+  if not loc or loc[0] != "kern_vsd.hip":
+    return None
+  for f, a0, a1, name in ranges()["phases"]:
+    if f == "kern_vsd.hip" and a0 <= loc[1] <= a1:
+      break
+  src = _lines(SRC)
+  for fn in ("sqrt_depth", "dist_of", "visib19t", "vsd_exact_px"):
+    r = _func_range(src, fn)
+    if r and r[0] <= loc[1] <= r[1]:
+      return "pixel_exact"
+  return None
+
+
+HELPERS = ("lib", "?", "rcp")  # lines of shared helpers: counted in the calling block's phase
+
+
+def block_phase(b, fallback="?"):
+  """Majority phase of a block's instructions, helper / compiler lines aside."""
+  c = collections.Counter()
+  for _, loc in b["insts"]:
+    ph = phase_of(loc)
+    if ph not in HELPERS and not ph.startswith("other"):
+      c[ph] += 1
+  return c.most_common(1)[0][0] if c else fallback
 
 
 def loop_phase(blocks, header):
-  """Majority phase of the instructions of a loop's own blocks."""
+  """Majority phase of the instructions of a loop's own blocks (helpers aside)."""
   cnt = collections.Counter()
   for b in blocks:
     if b["loop"] == header:
       for op, loc in b["insts"]:
-        cnt[phase_of(loc)] += 1
+        ph = phase_of(loc)
+        if ph not in HELPERS and not ph.startswith("other"):
+          cnt[ph] += 1
   return cnt.most_common(1)[0][0] if cnt else "?"
 
 
@@ -345,22 +392,35 @@ def main():
   loop_ctr["<top>"] = "<top>"
   dyn = collections.defaultdict(collections.Counter)
   if counts:
+    claim_taken = counts["claim_iters"] - counts["tile_iters"]  # iterations past the break
+    lphase = {key: (loop_phase(blocks, key) if key != "<top>" else "prologue") for key in loops}
+    per_loop_dyn = collections.Counter()
     for b in blocks:
       key = b["loop"] or "<top>"
-      ph_b = collections.Counter(phase_of(loc) for _, loc in b["insts"])
       name = loop_ctr.get(key)
-      major = ph_b.most_common(1)[0][0] if ph_b else None
-      if block_rare(b):
+      major = block_phase(b, lphase.get(key, "?"))
+      lines = {phase_of(loc) for _, loc in b["insts"]}
+      if block_rare(b) or major in ("cull", "large"):
         name = "zero"
-      elif major in BLOCK_COUNTERS and not (major == "slow_raster" and str(name).startswith("slow")):
-        name = BLOCK_COUNTERS[major]
+      elif name == "pix_iters" and lines & {"exact"} or (name == "pix_iters" and "pixel_exact"
+                                                          in {_fine(loc) for _, loc in b["insts"]}):
+        name = "exact_ballots"  # the float64 sequence: the filter's re-runs (and !filter)
+      elif major == "slow_raster" and not str(name).startswith("slow"):
+        name = "slow_chunks"
+      elif name == "claim_iters" and b["label"] != key:
+        name = claim_taken  # everything after the claim and its break test
       trip = name if isinstance(name, float) else counts.get(name)
       if trip is None:
         print("  no counter for block %s (loop %s, %s): %d instructions" % (
             b["label"], key, name, len(b["insts"])))
         continue
       for op, loc in b["insts"]:
-        dyn[phase_of(loc)][iclass(op)] += trip
+        ph = phase_of(loc)
+        if ph in HELPERS or ph.startswith("other"):
+          ph = major  # helper / compiler lines: the block's phase
+        dyn[ph][iclass(op)] += trip
+        if iclass(op) == "VALU":
+          per_loop_dyn[key] += trip
   rows = []
   for key, info in sorted(loops.items(), key=lambda kv: (kv[1]["depth"], kv[0])):
     c = per_loop[key]
@@ -383,6 +443,9 @@ def main():
       print("  %-18s VALU %9.0f  SALU %9.0f  LDS %8.0f" % (p, c["VALU"], c["SALU"], c["LDS"]))
     print("  %-18s VALU %9.0f  SALU %9.0f  LDS %8.0f" % ("total", tot["VALU"], tot["SALU"],
                                                         tot["LDS"]))
+    print("\nVALU per tuple by loop:")
+    for key, v in per_loop_dyn.most_common(12):
+      print("  %-10s %-18s %9.0f" % (key, lphase.get(key), v))
   if a.json:
     with open(a.json, "w") as f:
       json.dump({"kernel": a.kernel, "static_total": total, "loops": rows,
