@@ -149,8 +149,9 @@ def main():
   ap.add_argument("--profile", action="store_true")
   ap.add_argument("--instances", type=int, default=1,
                   help="instances (and estimates) per object and image; > 1: multi-instance")
-  ap.add_argument("--ab-group", action="store_true",
-                  help="with --ab-depth: warm runs with per-scene and grouped GPU decode launches")
+  ap.add_argument("--ab-group", default=None,
+                  help="with --ab-depth: comma list of BOPX_DEPTH_GROUP_FRAMES values (0 = one "
+                       "decode launch per scene), each run warm twice, interleaved")
   ap.add_argument("--ab-depth", action="store_true",
                   help="evaluate twice: test depth decoded on the GPU, then on the host "
                        "(BOPX_DEPTH_GPU=0); both timings and identical scores reported")
@@ -230,9 +231,9 @@ def main():
     first_phases, first_err = dict(phases), dict(err_t)
     ab = {}
     runs = (("host_decode_warm", "0", None), ("gpu_decode_warm", "1", None))
-    if a.ab_group:  # per-scene decode launches vs shared launches of ~4,096 frames
-      runs = (("gpu_decode_per_scene_warm", "1", "0"), ("gpu_decode_grouped_warm", "1", "4096"),
-              ("gpu_decode_per_scene_warm2", "1", "0"), ("gpu_decode_grouped_warm2", "1", "4096"))
+    if a.ab_group:  # decode launches per scene (0) vs shared launches of ~G frames
+      gs = a.ab_group.split(",")
+      runs = tuple(("gpu_decode_group%s_warm%d" % (g, r), "1", g) for r in (1, 2) for g in gs)
     for name, env, grp in runs:
       if grp is None:
         os.environ.pop("BOPX_DEPTH_GROUP_FRAMES", None)
