@@ -88,48 +88,78 @@ def pack(paths, H, W, buf_for, workers=None):
   return buf, need.value, z_off, z_len, st
 
 
+class Packed:
+  """A batch packed for the device decoder (DepthDecoder.pack): the staging
+  buffer holding the concatenated IDAT payloads and the per-file offsets,
+  lengths and host-side status."""
+
+  def __init__(self, **kw):
+    self.__dict__.update(kw)
+
+
 class DepthDecoder:
   """Decodes batches of 16-bit depth PNGs of one size into device frames.
 
-  Owns a libbopx context (one per thread, include/bopx.h) and a page-locked
-  staging buffer reused across calls; load() enqueues on torch's current
-  stream of the device and returns once the frames are final (it reads the
-  per-frame status back)."""
+  Owns a libbopx context (one per thread, include/bopx.h) and page-locked
+  staging buffers reused across calls (`slot` 0 / 1: a batch can be packed
+  into one while the other's upload is in flight). load() = decode(pack()):
+  enqueues on torch's current stream of the device and returns once the
+  frames are final (it reads the per-frame status back)."""
 
-  def __init__(self, device=0):
-    self.ctx = _lib.Context(device)
+  def __init__(self, device=0, lazy=False):
     self.device = int(device)
-    self._pinned = None
+    self._ctx = None if lazy else _lib.Context(device)
+    self._pinned = [None, None]
 
-  def _staging(self, torch, nbytes):
-    if self._pinned is None or self._pinned.numel() < nbytes:
-      self._pinned = None
-      self._pinned = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, pin_memory=True)
-    return self._pinned
+  @property
+  def ctx(self):
+    """The libbopx context (lazy=True: created by the first decode, on the
+    thread that decodes)."""
+    if self._ctx is None:
+      self._ctx = _lib.Context(self.device)
+    return self._ctx
 
-  def load(self, paths, scales, H, W, torch, workers=None):
-    """(n, H, W) float32 frames on the device: sample * (float32)scales[k]
-    (scales None: 1). Raises ValueError like inout.load_depths when a file
-    that the device decoder cannot take has another size."""
+  def _staging(self, torch, nbytes, slot=0):
+    if self._pinned[slot] is None or self._pinned[slot].numel() < nbytes:
+      self._pinned[slot] = None
+      self._pinned[slot] = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, pin_memory=True)
+    return self._pinned[slot]
+
+  def pack(self, paths, scales, H, W, torch, workers=None, slot=0):
+    """Host half of load(): read and check the files into staging slot `slot`
+    (no GPU work; the slot must not be in use by an unfinished decode)."""
     n = len(paths)
+    sc = np.ones(n, np.float32) if scales is None else np.asarray(
+        [np.float32(float(s)) for s in scales], np.float32)
+    t0 = time.perf_counter()
+    host_only = n == 0 or W > MAX_WIDTH or H * (2 * W + 1) > MAX_RAW  # outside the kernel's range
+    buf = need = z_off = z_len = st = None
+    if not host_only:
+      buf, need, z_off, z_len, st = pack(paths, H, W, lambda nb: self._staging(torch, nb, slot),
+                                         workers)
+    return Packed(paths=paths, scales=scales, sc=sc, H=int(H), W=int(W), workers=workers,
+                  host_only=host_only, buf=buf, need=need, z_off=z_off, z_len=z_len, st=st,
+                  pack_s=time.perf_counter() - t0)
+
+  def decode(self, pk, torch):
+    """Device half of load(): upload, kernels, status, host fall-back for the
+    frames the device did not take. Returns the (n, H, W) float32 frames."""
+    n, H, W, paths, scales, sc, workers = (len(pk.paths), pk.H, pk.W, pk.paths, pk.scales, pk.sc,
+                                           pk.workers)
     dev = torch.device("cuda", self.device)
     frames = torch.empty((n, H, W), dtype=torch.float32, device=dev)
     if n == 0:
       return frames
-    if W > MAX_WIDTH or H * (2 * W + 1) > MAX_RAW:  # outside the kernel's range: host decoder
+    if pk.host_only:
       frames.copy_(torch.from_numpy(_host_frames(paths, scales, H, W, workers)))
       torch.cuda.current_stream(dev).synchronize()
       self.last_host = n
       return frames
-    sc = np.ones(n, np.float32) if scales is None else np.asarray(
-        [np.float32(float(s)) for s in scales], np.float32)
-    t0 = time.perf_counter()
-    buf, need, z_off, z_len, st = pack(paths, H, W, lambda nb: self._staging(torch, nb), workers)
     t1 = time.perf_counter()
     stream = torch.cuda.current_stream(dev)
-    z_d = buf[:need].to(dev, non_blocking=True)
-    off_d = torch.from_numpy(z_off).to(dev)
-    len_d = torch.from_numpy(z_len).to(dev)
+    z_d = pk.buf[:pk.need].to(dev, non_blocking=True)
+    off_d = torch.from_numpy(pk.z_off).to(dev)
+    len_d = torch.from_numpy(pk.z_len).to(dev)
     sc_d = torch.from_numpy(sc).to(dev)
     raw_stride = raw_stride_of(H, W)
     raw = torch.empty(n * raw_stride, dtype=torch.uint8, device=dev)
@@ -140,7 +170,7 @@ class DepthDecoder:
     gst = status.view(n, 2)[:, 0].cpu().numpy()  # synchronises: staging reusable after this
     del raw, z_d
     t2 = time.perf_counter()
-    host = np.nonzero((st != 0) | (gst != 0))[0]
+    host = np.nonzero((pk.st != 0) | (gst != 0))[0]
     if len(host):
       arr = _host_frames([paths[k] for k in host], None if scales is None else
                          [float(sc[k]) for k in host], H, W, workers)
@@ -149,8 +179,14 @@ class DepthDecoder:
       # streams (the scene prefetch threads), so the frames are final on return
       stream.synchronize()
     self.last_host = len(host)
-    _stat(calls=1, frames=n, pack_s=t1 - t0, decode_s=t2 - t1, host_s=time.perf_counter() - t2)
+    _stat(calls=1, frames=n, pack_s=pk.pack_s, decode_s=t2 - t1, host_s=time.perf_counter() - t2)
     return frames
+
+  def load(self, paths, scales, H, W, torch, workers=None):
+    """(n, H, W) float32 frames on the device: sample * (float32)scales[k]
+    (scales None: 1). Raises ValueError like inout.load_depths when a file
+    that the device decoder cannot take has another size."""
+    return self.decode(self.pack(paths, scales, H, W, torch, workers), torch)
 
 
 class GroupPrefetch:
@@ -158,35 +194,45 @@ class GroupPrefetch:
 
   A scene's frames alone leave most of the chip idle during k_png_inflate (one
   wave per stream: a launch takes one stream's latency, ~70 ms for 640x480
-  frames, whether it holds 100 or 5,000 streams). A worker thread walks the
+  frames, whether it holds 100 or 5,000 streams). A packing thread walks the
   scenes in order, collects their PNG paths (items: (key, thunk), thunk() ->
-  (paths, scales), run in the worker) until a group holds max_frames frames,
-  and decodes the group with one DepthDecoder.load on `stream`; each scene
-  gets its slice of the group's frames. At most max_groups decoded groups wait
-  for their consumer (device memory bound). get(key) blocks until the scene's
-  frames are final and returns them (None: no images; raises the decoder's
-  ValueError for a group it could not take, e.g. a frame of another size).
+  (paths, scales), run in that thread) until a group holds max_frames frames,
+  and packs the group on host threads (DepthDecoder.pack) into one of two
+  staging slots; a decoding thread uploads and decodes the groups in order
+  (DepthDecoder.decode on `stream`), so group g + 1 is read and checked while
+  group g is on the GPU. Each scene gets its slice of its group's frames. At
+  most max_groups decoded groups wait for their consumer (device memory
+  bound). get(key) blocks until the scene's frames are final and returns them
+  (None: no images; raises the decoder's ValueError for a group it could not
+  take, e.g. a frame of another size).
   """
 
   def __init__(self, device, items, H, W, torch, stream, consumer, max_frames=4096, max_groups=2):
     import concurrent.futures as cf
-    import threading
+    import queue
     self._torch = torch
     self._items = list(items)
     self._fut = {k: cf.Future() for k, _ in self._items}
     self._left = {}  # group id -> keys not yet taken
     self._group_of = {}
     self._sem = threading.Semaphore(max_groups)
+    self._slot_free = [threading.Semaphore(1), threading.Semaphore(1)]
     self._lock = threading.Lock()
+    self._q = queue.Queue(maxsize=1)
     self._stop = False
     self.H, self.W, self.max_frames = int(H), int(W), int(max_frames)
     self.stream, self.consumer, self.device = stream, consumer, device
     self.groups = 0
-    self._thread = threading.Thread(target=self._run, name="bopx-depth-groups", daemon=True)
-    self._thread.start()
+    # the decoding thread creates the decoder's context (lazy); the packing
+    # thread only fills its page-locked staging slots
+    self._dec = DepthDecoder(device, lazy=True)
+    self._packer = threading.Thread(target=self._pack_run, name="bopx-depth-pack", daemon=True)
+    self._decoder = threading.Thread(target=self._decode_run, name="bopx-depth-decode",
+                                     daemon=True)
+    self._packer.start()
+    self._decoder.start()
 
-  def _run(self):
-    dec = None
+  def _pack_run(self):
     pending, n = [], 0
     try:
       for key, thunk in self._items:
@@ -203,43 +249,65 @@ class GroupPrefetch:
         pending.append((key, paths, scales))
         n += len(paths)
         if n >= self.max_frames:
-          dec = self._flush(pending, dec)
+          self._pack(pending)
           pending, n = [], 0
       if pending and not self._stop:
-        self._flush(pending, dec)
+        self._pack(pending)
     finally:
-      for f in self._fut.values():
-        if not f.done():
-          f.set_exception(RuntimeError("depth prefetch stopped"))
+      self._q.put(None)  # end of groups
 
-  def _flush(self, pending, dec):
-    torch = self._torch
-    self._sem.acquire()
-    if self._stop:
-      return dec
-    if dec is None:
-      dec = DepthDecoder(self.device)
-    paths = [q for _, ps, _ in pending for q in ps]
-    scales = [c for _, _, cs in pending for c in cs]
+  def _pack(self, pending):
     gid = self.groups
     self.groups += 1
-    with self._lock:
-      self._left[gid] = len(pending)
-      for key, _, _ in pending:
-        self._group_of[key] = gid
+    slot = gid & 1
+    self._slot_free[slot].acquire()  # the decode of group gid - 2 is done with the slot
+    if self._stop:
+      self._slot_free[slot].release()
+      return
+    paths = [q for _, ps, _ in pending for q in ps]
+    scales = [c for _, _, cs in pending for c in cs]
     try:
-      with torch.cuda.stream(self.stream):
-        frames = dec.load(paths, scales, self.H, self.W, torch)
-      frames.record_stream(self.consumer)  # freed behind the consumer's use
+      pk = self._dec.pack(paths, scales, self.H, self.W, self._torch, slot=slot)
     except BaseException as e:  # noqa: BLE001
+      self._slot_free[slot].release()
       for key, _, _ in pending:
         self._fut[key].set_exception(e)
-      return dec
-    o = 0
-    for key, ps, _ in pending:
-      self._fut[key].set_result(frames[o:o + len(ps)])
-      o += len(ps)
-    return dec
+      return
+    self._q.put((gid, slot, pending, pk))
+
+  def _decode_run(self):
+    torch = self._torch
+    while True:
+      job = self._q.get()
+      if job is None:
+        break
+      gid, slot, pending, pk = job
+      try:
+        if not self._stop:
+          self._sem.acquire()  # at most max_groups decoded groups wait for their consumer
+        if self._stop:
+          continue  # drain the queue (the finally frees the slot)
+        with self._lock:
+          self._left[gid] = len(pending)
+          for key, _, _ in pending:
+            self._group_of[key] = gid
+        try:
+          with torch.cuda.stream(self.stream):
+            frames = self._dec.decode(pk, torch)
+          frames.record_stream(self.consumer)  # freed behind the consumer's use
+        except BaseException as e:  # noqa: BLE001
+          for key, _, _ in pending:
+            self._fut[key].set_exception(e)
+          continue
+        o = 0
+        for key, ps, _ in pending:
+          self._fut[key].set_result(frames[o:o + len(ps)])
+          o += len(ps)
+      finally:
+        self._slot_free[slot].release()
+    for f in self._fut.values():
+      if not f.done():
+        f.set_exception(RuntimeError("depth prefetch stopped"))
 
   def get(self, key):
     try:
@@ -256,7 +324,14 @@ class GroupPrefetch:
   def close(self):
     self._stop = True
     self._sem.release()
-    self._thread.join(timeout=60)
+    for sf in self._slot_free:
+      sf.release()
+    try:
+      self._q.put_nowait(None)
+    except Exception:  # noqa: BLE001 - full: the decoder still has a job; it sees _stop
+      pass
+    self._packer.join(timeout=60)
+    self._decoder.join(timeout=60)
 
   def __enter__(self):
     return self

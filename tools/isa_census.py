@@ -445,7 +445,8 @@ def main():
                                                         tot["LDS"]))
     print("\nVALU per tuple by loop:")
     for key, v in per_loop_dyn.most_common(12):
-      print("  %-10s %-18s %9.0f" % (key, lphase.get(key), v))
+      lc = loop_ctr.get(key)
+      print("  %-10s %-18s %9.0f" % (key, lc if isinstance(lc, str) else "fixed x%g" % lc, v))
   if a.json:
     with open(a.json, "w") as f:
       json.dump({"kernel": a.kernel, "static_total": total, "loops": rows,
