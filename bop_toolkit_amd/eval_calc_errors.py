@@ -810,178 +810,185 @@ def run(p, device=0):
     dp_split = dataset_params.get_split_params(p["datasets_path"], dataset, split, split_type)
     dp_model = dataset_params.get_model_params(p["datasets_path"], dataset, "eval")
     et = p["error_type"]
-    models_info = None
-    if et in ("ad", "add", "adi", "vsd", "mssd", "mspd", "cus"):
-      models_info = cached_load(inout.load_json, dp_model["models_info_path"], keys_to_int=True)
-    if et not in ("re", "te", "rete"):
-      if ev is None:
-        ev = evaluator(device)
-      log("Loading object models...")
-      Models(ev, p, dp_model, models_info)
-    targets = cached_load(inout.load_json, os.path.join(dp_split["base_path"], p["targets_filename"]))
-    log("Loading pose estimates...")
-    ests = cached_load(inout.load_bop_results, os.path.join(p["results_path"], result_filename))
-    targets_org, ests_org = organize(targets, ests)
-    sym_ids = set(dp_model["symmetric_obj_ids"] or [])
-    ests_counter = 0
+    # VSD test depth: every target image of every scene, decoded on the GPU in
+    # shared launches (depth_gpu.GroupPrefetch) from here on, so the decode
+    # overlaps the model upload, the results parse and the planning below
     rank, world = _dist()
-    arrays = (et in ARRAY_TYPES and world == 1 and ev is not None and
-              os.environ.get("BOPX_ERRORS_ARRAYS", "1") != "0")
-    # VSD test depth goes to the GPU from the prepare thread on a stream of its
-    # own, overlapping the current scene's kernels (the main stream only ever
-    # sees frames already resident)
+    if et not in ("re", "te", "rete") and ev is None:
+      ev = evaluator(device)
     up = None
     if et == "vsd" and ev is not None and torch.cuda.is_available():
+      # (the prepare thread's uploads and the decoder run on this stream, the
+      # main stream only ever sees frames already resident)
       up = (torch.cuda.Stream(ev.device), torch.cuda.current_stream(ev.device))
-
-    decoder = [None]  # depth_gpu.DepthDecoder, used by the prefetch thread only
-
-    def prefetch_depths(ims, scene_id, scene_camera):
-      # the scene's test depth, resident on the device when the GPU runs the
-      # VSD: PNGs decoded by kern_png.hip (depth_gpu; BOPX_DEPTH_GPU=0: host
-      # decoder + one upload), on the upload stream
-      if up is not None and depth_gpu.enabled():
-        paths, scales = scene_depth_paths(dp_split, scene_camera, scene_id, ims)
-        W, H = dp_split["im_size"]
-        if decoder[0] is None:
-          decoder[0] = depth_gpu.DepthDecoder(ev.device.index or 0)
-        try:
-          with torch.cuda.stream(up[0]):
-            d = decoder[0].load(paths, scales, H, W, torch)
-          d.record_stream(up[1])  # freed behind the main stream's use
-          return d
-        except ValueError:
-          pass  # a frame of another size: the host path below
-      depths = load_scene_depths(dp_split, scene_camera, scene_id, ims, torch,
-                                 reuse=up is not None)
-      if up is not None and torch.is_tensor(depths):
-        with torch.cuda.stream(up[0]):
-          d = depths.to(ev.device, non_blocking=True)
-        up[0].synchronize()
-        d.record_stream(up[1])  # freed behind the main stream's use
-        depths = d
-      return depths
-
-    scenes = list(targets_org.items())
-    groups = None
+    arrays = (et in ARRAY_TYPES and world == 1 and ev is not None and
+              os.environ.get("BOPX_ERRORS_ARRAYS", "1") != "0")
+    groups, group_ims = None, {}
     if arrays and et == "vsd" and up is not None and depth_gpu.enabled() and depth_group_frames() > 0:
-      def scene_images(scene_id, scene_targets):
-        # every target image of the scene that has estimates (a superset of the
-        # images of the scene's VSD batch: gated pairs may leave some out; the
-        # batch maps its tuples to these frames, evaluate_batch_arrays)
+      targets = cached_load(inout.load_json,
+                            os.path.join(dp_split["base_path"], p["targets_filename"]))
+      scene_ims = {}  # scenes in the order organize() gives them, images sorted
+      for t in targets:
+        scene_ims.setdefault(t["scene_id"], set()).add(t["im_id"])
+
+      def scene_images(scene_id, ims):
         scene_camera = cached_load(inout.load_scene_camera,
                                    dp_split["scene_camera_tpath"].format(scene_id=scene_id))
-        se = ests_org.get(scene_id, {})
-        ims = sorted(im for im, tg in scene_targets.items()
-                     if any(se.get(im, {}).get(o) for o in tg))
         group_ims[scene_id] = ims
         return scene_depth_paths(dp_split, scene_camera, scene_id, ims)
       W_, H_ = dp_split["im_size"]
-      group_ims = {}
       groups = depth_gpu.GroupPrefetch(
           ev.device.index or 0,
-          [(sid, (lambda sid=sid, st=st: scene_images(sid, st))) for sid, st in scenes],
+          [(sid, (lambda sid=sid, ims=sorted(v): scene_images(sid, ims)))
+           for sid, v in scene_ims.items()],
           H_, W_, torch, up[0], up[1], max_frames=depth_group_frames())
+    try:
+      models_info = None
+      if et in ("ad", "add", "adi", "vsd", "mssd", "mspd", "cus"):
+        models_info = cached_load(inout.load_json, dp_model["models_info_path"], keys_to_int=True)
+      if et not in ("re", "te", "rete"):
+        log("Loading object models...")
+        Models(ev, p, dp_model, models_info)
+      targets = cached_load(inout.load_json, os.path.join(dp_split["base_path"], p["targets_filename"]))
+      log("Loading pose estimates...")
+      ests = cached_load(inout.load_bop_results, os.path.join(p["results_path"], result_filename))
+      targets_org, ests_org = organize(targets, ests)
+      sym_ids = set(dp_model["symmetric_obj_ids"] or [])
+      ests_counter = 0
 
-    def prepare(scene_id, scene_targets):
-      # host side of one scene: annotations, records, gates, this rank's share
-      # of the tuples and (VSD) its test-depth PNGs, decoded while the previous
-      # scene runs and is saved
-      scene_camera = cached_load(inout.load_scene_camera,
-                                 dp_split["scene_camera_tpath"].format(scene_id=scene_id))
-      scene_gt = cached_load(inout.load_scene_gt,
-                             dp_split["scene_gt_tpath"].format(scene_id=scene_id))
-      planned = None
-      if arrays:
-        arr, n_ests = scene_arrays_direct_cached(p, scene_id, scene_targets, ests_org, scene_gt)
-        recs = None
-        vals, todo = plan_arrays(p, arr, models_info)
-        depths = depth_ims = None
-        if et == "vsd" and len(todo):
-          if groups is not None:
-            try:
-              depths = groups.get(scene_id)
-              depth_ims = group_ims.get(scene_id)
-            except ValueError:
-              depths = None  # a frame of another size in the group: per-scene path
-          if depths is None:
-            depth_ims = None
-            depths = prefetch_depths(
-                np.unique(arr["rec_im"][arr["pair_ri"][todo]]).tolist(), scene_id, scene_camera)
-        planned = ("arrays", arr, vals, todo, (depths, depth_ims))
-        return scene_camera, recs, n_ests, planned
-      recs, n_ests = scene_records_cached(p, scene_id, scene_targets, ests_org, scene_gt)
-      if recs:
-        errs, todo, mine = plan_rank(p, recs, models_info, ev.objects if ev else None,
-                                     scene_camera, dp_split["im_size"], rank, world)
-        depths = None
-        if et == "vsd" and len(mine):
-          depths = prefetch_depths(todo_images(recs, [todo[i] for i in mine]), scene_id,
-                                   scene_camera)
-        planned = (errs, todo, mine, depths)
-      return scene_camera, recs, n_ests, planned
+      decoder = [None]  # depth_gpu.DepthDecoder, used by the prefetch thread only
 
-    import contextlib
-    from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(1) as ahead, (groups or contextlib.nullcontext()):
-      nxt = ahead.submit(prepare, *scenes[0]) if scenes else None
-      for k, (scene_id, scene_targets) in enumerate(scenes):
-        scene_camera, recs, n_ests, planned = nxt.result()
-        if k + 1 < len(scenes):
-          nxt = ahead.submit(prepare, *scenes[k + 1])
-        log("Calculating error {} - method: {}, dataset: {}{}, scene: {}".format(
-            et, method, dataset, split_type_str, scene_id))
-        ests_counter += n_ests
+      def prefetch_depths(ims, scene_id, scene_camera):
+        # the scene's test depth, resident on the device when the GPU runs the
+        # VSD: PNGs decoded by kern_png.hip (depth_gpu; BOPX_DEPTH_GPU=0: host
+        # decoder + one upload), on the upload stream
+        if up is not None and depth_gpu.enabled():
+          paths, scales = scene_depth_paths(dp_split, scene_camera, scene_id, ims)
+          W, H = dp_split["im_size"]
+          if decoder[0] is None:
+            decoder[0] = depth_gpu.DepthDecoder(ev.device.index or 0)
+          try:
+            with torch.cuda.stream(up[0]):
+              d = decoder[0].load(paths, scales, H, W, torch)
+            d.record_stream(up[1])  # freed behind the main stream's use
+            return d
+          except ValueError:
+            pass  # a frame of another size: the host path below
+        depths = load_scene_depths(dp_split, scene_camera, scene_id, ims, torch,
+                                   reuse=up is not None)
+        if up is not None and torch.is_tensor(depths):
+          with torch.cuda.stream(up[0]):
+            d = depths.to(ev.device, non_blocking=True)
+          up[0].synchronize()
+          d.record_stream(up[1])  # freed behind the main stream's use
+          depths = d
+        return depths
+
+      scenes = list(targets_org.items())
+
+      def prepare(scene_id, scene_targets):
+        # host side of one scene: annotations, records, gates, this rank's share
+        # of the tuples and (VSD) its test-depth PNGs, decoded while the previous
+        # scene runs and is saved
+        scene_camera = cached_load(inout.load_scene_camera,
+                                   dp_split["scene_camera_tpath"].format(scene_id=scene_id))
+        scene_gt = cached_load(inout.load_scene_gt,
+                               dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+        planned = None
         if arrays:
-          _, arr, vals, todo, (depths, depth_ims) = planned
-          if len(todo):
-            rows = evaluate_batch_arrays(ev, torch, p, dataset, dp_split, scene_camera,
-                                         scene_id, arr, todo, models_info, depths, depth_ims)
-            vals[todo] = rows.cpu().numpy()
-          if et == "vsd":  # one file per tau (:401-415)
-            signs = [misc.get_error_signature(et, p["n_top"], vsd_delta=p["vsd_deltas"][dataset],
-                                              vsd_tau=tau) for tau in p["vsd_taus"]]
-          else:
-            signs = [misc.get_error_signature(et, p["n_top"])]
-          paths = [p["out_errors_tpath"].format(eval_path=p["eval_path"], result_name=result_name,
-                                                error_sign=sg, scene_id=scene_id) for sg in signs]
-          for path in paths:
+          arr, n_ests = scene_arrays_direct_cached(p, scene_id, scene_targets, ests_org, scene_gt)
+          recs = None
+          vals, todo = plan_arrays(p, arr, models_info)
+          depths = depth_ims = None
+          if et == "vsd" and not len(todo) and groups is not None:
+            groups.get(scene_id)  # not needed: taken so that its group can be freed
+          if et == "vsd" and len(todo):
+            if groups is not None:
+              try:
+                depths = groups.get(scene_id)
+                depth_ims = group_ims.get(scene_id)
+              except ValueError:
+                depths = None  # a frame of another size in the group: per-scene path
+            if depths is None:
+              depth_ims = None
+              depths = prefetch_depths(
+                  np.unique(arr["rec_im"][arr["pair_ri"][todo]]).tolist(), scene_id, scene_camera)
+          planned = ("arrays", arr, vals, todo, (depths, depth_ims))
+          return scene_camera, recs, n_ests, planned
+        recs, n_ests = scene_records_cached(p, scene_id, scene_targets, ests_org, scene_gt)
+        if recs:
+          errs, todo, mine = plan_rank(p, recs, models_info, ev.objects if ev else None,
+                                       scene_camera, dp_split["im_size"], rank, world)
+          depths = None
+          if et == "vsd" and len(mine):
+            depths = prefetch_depths(todo_images(recs, [todo[i] for i in mine]), scene_id,
+                                     scene_camera)
+          planned = (errs, todo, mine, depths)
+        return scene_camera, recs, n_ests, planned
+
+      from concurrent.futures import ThreadPoolExecutor
+      with ThreadPoolExecutor(1) as ahead:
+        nxt = ahead.submit(prepare, *scenes[0]) if scenes else None
+        for k, (scene_id, scene_targets) in enumerate(scenes):
+          scene_camera, recs, n_ests, planned = nxt.result()
+          if k + 1 < len(scenes):
+            nxt = ahead.submit(prepare, *scenes[k + 1])
+          log("Calculating error {} - method: {}, dataset: {}{}, scene: {}".format(
+              et, method, dataset, split_type_str, scene_id))
+          ests_counter += n_ests
+          if arrays:
+            _, arr, vals, todo, (depths, depth_ims) = planned
+            if len(todo):
+              rows = evaluate_batch_arrays(ev, torch, p, dataset, dp_split, scene_camera,
+                                           scene_id, arr, todo, models_info, depths, depth_ims)
+              vals[todo] = rows.cpu().numpy()
+            if et == "vsd":  # one file per tau (:401-415)
+              signs = [misc.get_error_signature(et, p["n_top"], vsd_delta=p["vsd_deltas"][dataset],
+                                                vsd_tau=tau) for tau in p["vsd_taus"]]
+            else:
+              signs = [misc.get_error_signature(et, p["n_top"])]
+            paths = [p["out_errors_tpath"].format(eval_path=p["eval_path"], result_name=result_name,
+                                                  error_sign=sg, scene_id=scene_id) for sg in signs]
+            for path in paths:
+              os.makedirs(os.path.dirname(path), exist_ok=True)
+              log("Saving errors to: {}".format(path))
+            inout.save_errors_arrays(paths, arr["rec_im"], arr["rec_obj"], arr["rec_est"],
+                                     arr["rec_score"], arr["pair_off"], arr["pair_gt"], vals)
+            written.extend(paths)
+            continue
+          errs = evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
+                          models_info, sym_ids, planned=planned) if recs else []
+          if errs is None or _dist()[0] != 0:  # rank 0 writes (also for a scene with no records)
+            continue
+          scene_errs = [{"im_id": r["im_id"], "obj_id": r["obj_id"], "est_id": r["est_id"],
+                         "score": r["score"], "errors": e} for r, e in zip(recs, errs)]
+
+          def save(sign, content):
+            path = p["out_errors_tpath"].format(eval_path=p["eval_path"], result_name=result_name,
+                                               error_sign=sign, scene_id=scene_id)
             os.makedirs(os.path.dirname(path), exist_ok=True)
             log("Saving errors to: {}".format(path))
-          inout.save_errors_arrays(paths, arr["rec_im"], arr["rec_obj"], arr["rec_est"],
-                                   arr["rec_score"], arr["pair_off"], arr["pair_gt"], vals)
-          written.extend(paths)
-          continue
-        errs = evaluate(ev, torch, p, dataset, dp_split, scene_camera, scene_id, recs,
-                        models_info, sym_ids, planned=planned) if recs else []
-        if errs is None or _dist()[0] != 0:  # rank 0 writes (also for a scene with no records)
-          continue
-        scene_errs = [{"im_id": r["im_id"], "obj_id": r["obj_id"], "est_id": r["est_id"],
-                       "score": r["score"], "errors": e} for r, e in zip(recs, errs)]
+            inout.save_json(path, content)
+            written.append(path)
 
-        def save(sign, content):
-          path = p["out_errors_tpath"].format(eval_path=p["eval_path"], result_name=result_name,
-                                             error_sign=sign, scene_id=scene_id)
-          os.makedirs(os.path.dirname(path), exist_ok=True)
-          log("Saving errors to: {}".format(path))
-          inout.save_json(path, content)
-          written.append(path)
-
-        if et == "vsd":
-          # one file per tau (:401-415), all written from one encoding per record
-          paths = []
-          for tau in p["vsd_taus"]:
-            sign = misc.get_error_signature(et, p["n_top"], vsd_delta=p["vsd_deltas"][dataset],
-                                            vsd_tau=tau)
-            paths.append(p["out_errors_tpath"].format(eval_path=p["eval_path"],
-                                                      result_name=result_name, error_sign=sign,
-                                                      scene_id=scene_id))
-            os.makedirs(os.path.dirname(paths[-1]), exist_ok=True)
-            log("Saving errors to: {}".format(paths[-1]))
-          inout.save_json_per_value(paths, scene_errs, len(paths))
-          written.extend(paths)
-        else:
-          save(misc.get_error_signature(et, p["n_top"]), scene_errs)
+          if et == "vsd":
+            # one file per tau (:401-415), all written from one encoding per record
+            paths = []
+            for tau in p["vsd_taus"]:
+              sign = misc.get_error_signature(et, p["n_top"], vsd_delta=p["vsd_deltas"][dataset],
+                                              vsd_tau=tau)
+              paths.append(p["out_errors_tpath"].format(eval_path=p["eval_path"],
+                                                        result_name=result_name, error_sign=sign,
+                                                        scene_id=scene_id))
+              os.makedirs(os.path.dirname(paths[-1]), exist_ok=True)
+              log("Saving errors to: {}".format(paths[-1]))
+            inout.save_json_per_value(paths, scene_errs, len(paths))
+            written.extend(paths)
+          else:
+            save(misc.get_error_signature(et, p["n_top"]), scene_errs)
+    finally:
+      if groups is not None:
+        groups.close()
     log("Calculation of errors for {} estimates took {}s.".format(
         ests_counter, time.time() - time_start))
   log("Done.")

@@ -189,12 +189,31 @@ def main():
   run0, score0 = ece.run, ecs.score_error_dir
   err_t = {}
 
+  marks = {}  # wall clock of the last error pass's end; scorer job intervals
+
   def run_wrap(p, device=0):
     t = time.perf_counter()
     out = run0(p, device)
     err_t[p["error_type"]] = time.perf_counter() - t
+    marks["errors_end"] = time.perf_counter()
     return out
   ece.run = run_wrap
+  job0 = ecs._score_job_threaded
+
+  def job_wrap(job, cache, threads):
+    t = time.perf_counter()
+    try:
+      return job0(job, cache, threads)
+    finally:
+      marks.setdefault("jobs", []).append((t, time.perf_counter(), os.path.basename(job[0])))
+  ecs._score_job_threaded = job_wrap
+
+  def tail_info(t_end):
+    jobs = marks.get("jobs", [])
+    return {"after_last_error_pass_s": round(t_end - marks.get("errors_end", t_end), 3),
+            "scoring_busy_s": round(sum(b - a for a, b, _ in jobs), 3),
+            "scoring_after_errors_s": round(max([b for _, b, _ in jobs] or [0]) -
+                                            marks.get("errors_end", 0), 3)}
   ecs.score_error_dir = timed("scores", score0)
   # host steps of the error passes (the prepare thread's included)
   from bop_toolkit_amd import depth_gpu, inout
@@ -212,8 +231,10 @@ def main():
     prof = cProfile.Profile()
     prof.enable()
   t0 = time.perf_counter()
+  marks.clear()
   final = eval_bop19_pose.evaluate(p)
   t_eval = time.perf_counter() - t0
+  first_tail = tail_info(t0 + t_eval)
   if prof is not None:
     import io
     import pstats
@@ -247,9 +268,10 @@ def main():
         depth_gpu.STATS[k] = 0 if k in ("calls", "frames") else 0.0
       os.environ["BOPX_DEPTH_GPU"] = env
       t0 = time.perf_counter()
+      marks.clear()
       fin = eval_bop19_pose.evaluate(p)
       t_run = time.perf_counter() - t0
-      ab[name] = {"eval_bop19_s": round(t_run, 2),
+      ab[name] = {"eval_bop19_s": round(t_run, 2), "tail": tail_info(t0 + t_run),
                   "depth_decoder": {k: (round(v, 3) if isinstance(v, float) else v)
                                     for k, v in depth_gpu.STATS.items()},
                   "errors_s": {k: round(v, 2) for k, v in err_t.items()},
@@ -274,7 +296,7 @@ def main():
       "host_s": {k[5:]: round(v, 3) for k, v in phases.items() if k.startswith("host:")},
       "eval_tuples_per_s": n / t_eval,
       "depth_decoder": "gpu" if depth_gpu.enabled() else "host", "ab_depth": ab,
-      "depth_decoder_first_run": first_stats,
+      "depth_decoder_first_run": first_stats, "tail": first_tail,
       "ar": {k: round(float(v), 4) for k, v in scores.items()}}))
 
 

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out/cfg5; export TMPDIR=/tmp
 TAG=${TAG:-r05b}
 timeout -k 10 300 python tools/png_occupancy.py > gpurun_out/png_occ_${TAG}.json 2> gpurun_out/png_occ_${TAG}.err || { tail -20 gpurun_out/png_occ_${TAG}.err; exit 1; }
 cat gpurun_out/png_occ_${TAG}.json
-timeout -k 10 480 python tools/e2e_bench.py --images 16667 --ab-depth --ab-group ${GROUPS:-0,4096,5600,8400} > gpurun_out/e2e_100k_${TAG}.json 2> gpurun_out/e2e_100k_${TAG}.err || { tail -20 gpurun_out/e2e_100k_${TAG}.err; exit 1; }
+timeout -k 10 480 python tools/e2e_bench.py --images 16667 --ab-depth --ab-group ${DEPTH_GROUPS:-0,4096,5600,8400} > gpurun_out/e2e_100k_${TAG}.json 2> gpurun_out/e2e_100k_${TAG}.err || { tail -20 gpurun_out/e2e_100k_${TAG}.err; exit 1; }
 python -c "
 import json; d=json.load(open('gpurun_out/e2e_100k_${TAG}.json'))
 print('cold', d['eval_bop19_s'], d['errors_s'])
