@@ -52,7 +52,10 @@ constexpr uint16_t kNoCode = 0xFFFF;  // table entry: code longer than the root,
 __constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 struct InfLds {
-  uint16_t lit[1 << kLitRoot];    // also the code-length code's table (128 entries)
+  // literal/length root table; high half: a second literal whose code fits in
+  // the same kLitRoot bits (add_literal_pairs). Also the code-length code's
+  // table (128 entries, low halves only).
+  uint32_t lit[1 << kLitRoot];
   uint16_t dist[1 << kDistRoot];
   uint16_t sorted[288 + 32];      // symbols by code: literal/length, then distance
   uint8_t lens[288 + 32];         // code lengths: literal/length, then distance
@@ -83,8 +86,8 @@ __device__ __forceinline__ int popc_lt(uint64_t m) {
 // (all lengths 0), or -1 for an over-subscribed code or an incomplete one
 // other than a single length-1 code (zlib inftrees.c; libdeflate accepts the
 // same codes).
-template <int ROOT>
-__device__ int build_code(const uint8_t* lens, int n, uint16_t* tab, uint16_t* sorted, int& lim,
+template <int ROOT, class Tab>
+__device__ int build_code(const uint8_t* lens, int n, Tab* tab, uint16_t* sorted, int& lim,
                           int& base, int lane) {
   const bool len_lane = lane >= 1 && lane <= 15;
   const int nch = (n + 63) >> 6;
@@ -147,7 +150,7 @@ __device__ int build_code(const uint8_t* lens, int n, uint16_t* tab, uint16_t* s
         len = L;
       }
     }
-    tab[e] = idx >= 0 ? (uint16_t)(sorted[idx] << 4 | len) : kNoCode;
+    tab[e] = (Tab)(idx >= 0 ? (uint16_t)(sorted[idx] << 4 | len) : kNoCode);
   }
   wave_sync();
   return 0;
@@ -155,6 +158,31 @@ __device__ int build_code(const uint8_t* lens, int n, uint16_t* tab, uint16_t* s
 
 // A code longer than ROOT: the smallest length L > ROOT with the 15 bits
 // (first bit most significant) below lim[L]; -1 if none (no such code).
+// Second literals in the literal/length root table: entry e (bits of the
+// window, first bit lowest) whose code is a literal of length L1 leaves
+// ROOT - L1 known bits; if they hold a whole literal code of length L2 (the
+// table entry of those bits with the unknown high bits zero has L2 <= ROOT -
+// L1: a code shorter than ROOT is replicated over every suffix), entry e
+// gets sym2 << 20 | L2 << 16 in its high half. The window loop then takes two
+// literals per chain step (Huffman-coded depth rows: ~40 % 1-bit codes).
+template <int ROOT>
+__device__ void add_literal_pairs(uint32_t* tab, int lane) {
+#pragma unroll 1
+  for (int j = 0; j < (1 << ROOT) / 64; ++j) {
+    const int e = j * 64 + lane;
+    const uint32_t t = tab[e] & 0xFFFFu;
+    uint32_t pair = 0;
+    if (t < (256u << 4)) {  // a literal with a code of <= ROOT bits
+      const int L1 = (int)(t & 15u);
+      const uint32_t t2 = tab[e >> L1] & 0xFFFFu;
+      if (t2 < (256u << 4) && (int)(t2 & 15u) <= ROOT - L1) pair = (t2 >> 4) << 20 | (t2 & 15u) << 16;
+    }
+    wave_sync();  // every lane has read before any high half is written
+    tab[e] = t | pair;
+  }
+  wave_sync();
+}
+
 template <int ROOT>
 __device__ __forceinline__ int slow_index(uint64_t bb, int lim, int base, int lane, int& L) {
   const int r15 = (int)(__builtin_bitreverse32((uint32_t)bb) >> 17);
@@ -169,14 +197,17 @@ __device__ __forceinline__ int slow_index(uint64_t bb, int lim, int base, int la
 // 1024)). Returns 0 or kErr; *adler = the stream's Adler-32 field.
 __device__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t* __restrict__ out,
                               int out_n, InfLds& S, int lane, uint32_t* adler) {
-  // input: 1 KB chunks, words [base, base + 256) with lane l holding words
-  // base + 4l .. 4l + 3, read with v_readlane. The next chunk is loaded when
-  // the current one is used up (one load latency per KB of input; a prefetch
-  // into a loop-carried register makes the compiler copy it, and the copy
-  // waits for the load anyway)
-  const uint4* in128 = reinterpret_cast<const uint4*>(in);
+  // input: 1 KB chunks, words [base, base + 256) in four VGPRs, lane l
+  // holding words base + l + 64 k in component k (four coalesced dword loads),
+  // read with v_readlane from `cw`, the component of the current 64 words (a
+  // copy every 64 words instead of a four-way branch per word). The next chunk
+  // is loaded when the current one is used up (one load latency per KB of
+  // input; a prefetch into a loop-carried register makes the compiler copy it,
+  // and the copy waits for the load anyway)
+  const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
   const int in_chunks = (in_n + 2048) >> 10;  // 1 KB chunks inside the readable bytes
-  uint4 c = in128[lane];
+  uint32_t c0 = in32[lane], c1 = in32[64 + lane], c2 = in32[128 + lane], c3 = in32[192 + lane];
+  uint32_t cw = c0;
   int base = 0;
   int wi = 0;  // next input word
   uint64_t bb = 0;
@@ -184,20 +215,23 @@ __device__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t*
   int p = 0, flushed = 0;
 
   auto refill_word = [&]() -> bool {
-    if (wi - base >= 256) {
-      base += 256;
-      const int ch = min(base >> 8, max(in_chunks - 1, 0));
-      c = in128[ch * 64 + lane];
+    int i = wi - base;
+    if (__builtin_expect((i & 63) == 0 && i != 0, 0)) {  // the next 64 words
+      if (i >= 256) {
+        base += 256;
+        i = 0;
+        const int ch = min(base >> 8, max(in_chunks - 1, 0));
+        const uint32_t* w32 = in32 + ch * 256;
+        c0 = w32[lane];
+        c1 = w32[64 + lane];
+        c2 = w32[128 + lane];
+        c3 = w32[192 + lane];
+        cw = c0;
+      } else {
+        cw = i == 64 ? c1 : (i == 128 ? c2 : c3);
+      }
     }
-    const int i = wi - base;
-    const int l = i >> 2;
-    uint32_t w;
-    switch (i & 3) {
-      case 0: w = (uint32_t)__builtin_amdgcn_readlane((int)c.x, l); break;
-      case 1: w = (uint32_t)__builtin_amdgcn_readlane((int)c.y, l); break;
-      case 2: w = (uint32_t)__builtin_amdgcn_readlane((int)c.z, l); break;
-      default: w = (uint32_t)__builtin_amdgcn_readlane((int)c.w, l); break;
-    }
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cw, i & 63);
     bb |= (uint64_t)w << nb;
     nb += 32;
     ++wi;
@@ -283,7 +317,7 @@ __device__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t*
       int k = 0, prev = -1;
       while (k < ntot) {
             if (!refill()) return kErr;
-        const int e = uni(S.lit[bb & ((1 << kPreRoot) - 1)]);
+        const int e = uni((int)(S.lit[bb & ((1 << kPreRoot) - 1)] & 0xFFFFu));
         if (e == kNoCode) return kErr;  // every code-length code is <= 7 bits: no code
         const int sym = e >> 4;
         bb >>= e & 15;
@@ -323,6 +357,7 @@ __device__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t*
     }
     if (build_code<kLitRoot>(S.lens, hlit, S.lit, S.sorted, lit_lim, lit_base, lane) != 0)
       return kErr;
+    add_literal_pairs<kLitRoot>(S.lit, lane);
     const int dst =
         build_code<kDistRoot>(S.lens + 288, hdist, S.dist, S.sorted + 288, dist_lim, dist_base, lane);
     if (dst < 0) return kErr;
@@ -336,25 +371,31 @@ __device__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t*
         if (nb <= 32 && !refill_word()) return kErr;
       if (nb <= 32 && !refill_word()) return kErr;  // nb in (32, 64]
       const int lim = nb - kLitRoot;  // offsets whose lookup bits lie in the buffer
-      const int ev = S.lit[(uint32_t)(bb >> lane) & ((1 << kLitRoot) - 1)];
+      const uint32_t ev = S.lit[(uint32_t)(bb >> lane) & ((1 << kLitRoot) - 1)];
       int e, off = 0;
-      uint64_t run = 0;  // bit l: a literal code starts at offset l
+      uint64_t run = 0;  // bit l: a literal code (or a pair of them) starts at offset l
       for (;;) {
-        e = __builtin_amdgcn_readlane(ev, off);
-        if (e >= 256 << 4) break;  // not a literal with a short code: below
+        e = __builtin_amdgcn_readlane((int)ev, off);
+        if ((e & 0xFFFF) >= 256 << 4) break;  // not a literal with a short code: below
         run |= 1ull << off;
-        off += e & 15;
+        off += (e & 15) + ((e >> 16) & 15);
         if (off > lim) {
           e = -1;  // the window is used up
           break;
         }
       }
       if (run) {
-        const int nlit = __popcll(run);
+        const bool on = (run >> lane) & 1;
+        const uint64_t run2 = __ballot(on && (ev >> 16) != 0u);  // chain steps with two literals
+        const int nlit = __popcll(run) + __popcll(run2);
         if (nlit > out_n - p) return kErr;
         bb = off < 64 ? bb >> off : 0;
         nb -= off;
-        if ((run >> lane) & 1) S.ring[(p + popc_lt(run)) & kRingMask] = (uint8_t)(ev >> 4);
+        if (on) {
+          const int q = p + popc_lt(run) + popc_lt(run2);
+          S.ring[q & kRingMask] = (uint8_t)(ev >> 4);
+          if (ev >> 16) S.ring[(q + 1) & kRingMask] = (uint8_t)(ev >> 20);
+        }
         p += nlit;
         while (p - flushed >= kFlush) {
           flush_block(flushed);
