@@ -195,7 +195,7 @@ __device__ __forceinline__ int slow_index(uint64_t bb, int lim, int base, int la
 // Inflate one zlib stream (in, in_n bytes, 16-byte aligned, readable up to
 // in_n + 2048) into out (out_n bytes exactly; writable up to round_up(out_n,
 // 1024)). Returns 0 or kErr; *adler = the stream's Adler-32 field.
-__device__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t* __restrict__ out,
+__device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t* __restrict__ out,
                               int out_n, InfLds& S, int lane, uint32_t* adler) {
   // input: 1 KB chunks, words [base, base + 256) in four VGPRs, lane l
   // holding words base + l + 64 k in component k (four coalesced dword loads),
@@ -214,7 +214,7 @@ __device__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t*
   int nb = 0;
   int p = 0, flushed = 0;
 
-  auto refill_word = [&]() -> bool {
+  auto refill_word = [&]() __attribute__((always_inline)) -> bool {
     int i = wi - base;
     if (__builtin_expect((i & 63) == 0 && i != 0, 0)) {  // the next 64 words
       if (i >= 256) {
@@ -228,7 +228,10 @@ __device__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t*
         c3 = w32[192 + lane];
         cw = c0;
       } else {
-        cw = i == 64 ? c1 : (i == 128 ? c2 : c3);
+        // values, not lvalues: a conditional over the captured variables would
+        // select their addresses and put them in scratch
+        const uint32_t v1 = c1, v2 = c2, v3 = c3;
+        cw = i == 64 ? v1 : (i == 128 ? v2 : v3);
       }
     }
     const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cw, i & 63);
@@ -237,15 +240,15 @@ __device__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t*
     ++wi;
     return wi * 4 <= in_n + 8;
   };
-  auto refill = [&]() -> bool { return nb > 32 || refill_word(); };
-  auto flush_block = [&](int f) {
+  auto refill = [&]() __attribute__((always_inline)) -> bool { return nb > 32 || refill_word(); };
+  auto flush_block = [&](int f) __attribute__((always_inline)) {
     wave_sync();
     const uint4 v = reinterpret_cast<const uint4*>(S.ring)[((f & kRingMask) >> 4) + lane];
     __builtin_amdgcn_s_waitcnt(kVmcnt0);  // earlier flushes have landed: far reads below see them
     reinterpret_cast<uint4*>(out)[(f >> 4) + lane] = v;
   };
   // one output byte (p - flushed < kFlush before and after)
-  auto put = [&](int byte) {
+  auto put = [&](int byte) __attribute__((always_inline)) {
     if (lane == 0) S.ring[p & kRingMask] = (uint8_t)byte;
     ++p;
     if ((p & (kFlush - 1)) == 0) {

@@ -101,3 +101,18 @@ def test_load_traffic_keyed_on_code_object(tmp_path, monkeypatch):
   summ["_meta"]["code_sha256"] = dict(code, k_vsd="f" * 64)
   (prof / "x_pmc.json").write_text(json.dumps(summ))
   assert bench.load_traffic("vsd", args, 1000) is None
+
+
+def test_committed_pmc_matches_the_shipped_kernels(monkeypatch):
+  """The driver's bench line carries `roofline.traffic` only if a committed
+  PMC summary records this build's k_vsd code object and the default
+  workload: after a kernel change the PMC passes must be collected again
+  (tools/pmc.sh)."""
+  from bop_toolkit_amd import _lib
+  if not os.path.exists(_lib.LIB_PATH):
+    pytest.skip("libbopx.so not built")
+  monkeypatch.setattr(sys, "argv", ["bench.py"])
+  args = bench.parse()
+  n = (args.tuples + 5) // 6 * 6  # build_workload: whole images of 6 objects
+  assert bench.load_traffic("vsd", args, n) is not None
+  assert bench.load_traffic("mssd", args, n) is not None

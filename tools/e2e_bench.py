@@ -218,6 +218,37 @@ def main():
   # host steps of the error passes (the prepare thread's included)
   from bop_toolkit_amd import depth_gpu, inout
   depth_gpu.DepthDecoder.load = timed("host:gpu_depth_load", depth_gpu.DepthDecoder.load)
+  # timeline of the cold run: (name, start, end) of the host steps on every thread
+  tl = []
+
+  def traced(name, fn):
+    import functools
+
+    @functools.wraps(fn)
+    def wrap(*args, **kw):
+      t = time.perf_counter()
+      try:
+        return fn(*args, **kw)
+      finally:
+        tl.append((name, t, time.perf_counter()))
+    return wrap
+  depth_gpu.DepthDecoder.pack = traced("decoder.pack", depth_gpu.DepthDecoder.pack)
+  depth_gpu.DepthDecoder.decode = traced("decoder.decode", depth_gpu.DepthDecoder.decode)
+  inout.load_bop_results = traced("load_bop_results", inout.load_bop_results)
+  for nm in ("organize", "evaluate_batch_arrays", "run"):
+    setattr(ece, nm, traced(nm, getattr(ece, nm)))
+  inout.save_errors_arrays = traced("save_errors_arrays", inout.save_errors_arrays)
+
+  def timeline(t0):
+    agg = {}
+    for name, a0, a1 in tl:
+      g = agg.setdefault(name, [a0, a1, 0.0, 0])
+      g[0], g[1] = min(g[0], a0), max(g[1], a1)
+      g[2] += a1 - a0
+      g[3] += 1
+    return {k: {"first_start": round(v[0] - t0, 3), "last_end": round(v[1] - t0, 3),
+                "busy": round(v[2], 3), "n": v[3]} for k, v in sorted(agg.items(),
+                                                                    key=lambda kv: kv[1][0])}
   for mod, name in ((ece, "scene_records"), (ece, "scene_arrays_direct"), (ece, "plan_rank"),
                     (ece, "load_scene_depths"),
                     (ece, "evaluate_batch"), (ece, "evaluate"), (ece, "Models"), (inout, "save_json"), (inout, "save_json_per_value")):
@@ -232,9 +263,11 @@ def main():
     prof.enable()
   t0 = time.perf_counter()
   marks.clear()
+  tl.clear()
   final = eval_bop19_pose.evaluate(p)
   t_eval = time.perf_counter() - t0
   first_tail = tail_info(t0 + t_eval)
+  first_timeline = timeline(t0)
   if prof is not None:
     import io
     import pstats
@@ -296,7 +329,7 @@ def main():
       "host_s": {k[5:]: round(v, 3) for k, v in phases.items() if k.startswith("host:")},
       "eval_tuples_per_s": n / t_eval,
       "depth_decoder": "gpu" if depth_gpu.enabled() else "host", "ab_depth": ab,
-      "depth_decoder_first_run": first_stats, "tail": first_tail,
+      "depth_decoder_first_run": first_stats, "tail": first_tail, "timeline": first_timeline,
       "ar": {k: round(float(v), 4) for k, v in scores.items()}}))
 
 

@@ -14,3 +14,11 @@ for r in 1 2; do
     python -c "import json;d=json.load(open('gpurun_out/png_ab_${TAG}_${v}_$r.json'));print('$v $r', [(x['frames'], x['decode_us_per_frame']) for x in d['runs']])"
   done
 done
+if [ -n "$E2E" ]; then
+  timeout -k 10 480 python tools/e2e_bench.py --images 16667 --ab-depth --ab-group ${DEPTH_GROUPS:-4096,8400} > gpurun_out/e2e_100k_${TAG}.json 2> gpurun_out/e2e_100k_${TAG}.err || { tail -20 gpurun_out/e2e_100k_${TAG}.err; exit 1; }
+  python -c "
+import json; d=json.load(open('gpurun_out/e2e_100k_${TAG}.json'))
+print('cold', d['eval_bop19_s'], d['errors_s'], d['host_s'], d['tail'])
+for k,v in d['timeline'].items(): print('  ', k, v)
+for k,v in d['ab_depth'].items(): print(k, v['eval_bop19_s'], v['errors_s'], v['depth_decoder']['decode_s'], v['tail'], v['identical_scores'])"
+fi
