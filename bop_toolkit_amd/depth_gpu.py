@@ -88,10 +88,10 @@ def pack(paths, H, W, buf_for, workers=None):
   return buf, need.value, z_off, z_len, st
 
 
-class Packed:
-  """A batch packed for the device decoder (DepthDecoder.pack): the staging
-  buffer holding the concatenated IDAT payloads and the per-file offsets,
-  lengths and host-side status."""
+class Pending:
+  """A batch submitted to the device decoder (DepthDecoder.submit): frames
+  being produced on the stream, the per-frame device status, and what the
+  host fall-back needs."""
 
   def __init__(self, **kw):
     self.__dict__.update(kw)
@@ -100,16 +100,23 @@ class Packed:
 class DepthDecoder:
   """Decodes batches of 16-bit depth PNGs of one size into device frames.
 
-  Owns a libbopx context (one per thread, include/bopx.h) and page-locked
-  staging buffers reused across calls (`slot` 0 / 1: a batch can be packed
-  into one while the other's upload is in flight). load() = decode(pack()):
-  enqueues on torch's current stream of the device and returns once the
-  frames are final (it reads the per-frame status back)."""
+  Owns a libbopx context (one per thread, include/bopx.h; lazy=True creates
+  it on first use) and two page-locked staging slots of CHUNK files each,
+  reused across calls. submit() packs the files a chunk at a time on host
+  threads into one slot while the other slot's bytes go up on a copy stream,
+  then launches the kernels on torch's current stream (waiting for the
+  copies); finish() reads the per-frame status back (the frames are final
+  then) and decodes on the host what the device did not take. load() =
+  finish(submit())."""
+
+  CHUNK = 512  # files per staging slot (~0.2 GB of 640x480 depth PNGs)
 
   def __init__(self, device=0, lazy=False):
     self.device = int(device)
     self._ctx = None if lazy else _lib.Context(device)
     self._pinned = [None, None]
+    self._copied = [None, None]  # per slot: event of its last upload
+    self._copy_stream = None
 
   @property
   def ctx(self):
@@ -125,41 +132,72 @@ class DepthDecoder:
       self._pinned[slot] = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, pin_memory=True)
     return self._pinned[slot]
 
-  def pack(self, paths, scales, H, W, torch, workers=None, slot=0):
-    """Host half of load(): read and check the files into staging slot `slot`
-    (no GPU work; the slot must not be in use by an unfinished decode)."""
+  def submit(self, paths, scales, H, W, torch, workers=None):
+    """Pack, upload and launch (asynchronous on torch's current stream)."""
     n = len(paths)
+    dev = torch.device("cuda", self.device)
+    stream = torch.cuda.current_stream(dev)
+    frames = torch.empty((n, H, W), dtype=torch.float32, device=dev)
     sc = np.ones(n, np.float32) if scales is None else np.asarray(
         [np.float32(float(s)) for s in scales], np.float32)
-    t0 = time.perf_counter()
-    host_only = n == 0 or W > MAX_WIDTH or H * (2 * W + 1) > MAX_RAW  # outside the kernel's range
-    buf = need = z_off = z_len = st = None
-    if not host_only:
-      buf, need, z_off, z_len, st = pack(paths, H, W, lambda nb: self._staging(torch, nb, slot),
-                                         workers)
-    return Packed(paths=paths, scales=scales, sc=sc, H=int(H), W=int(W), workers=workers,
-                  host_only=host_only, buf=buf, need=need, z_off=z_off, z_len=z_len, st=st,
-                  pack_s=time.perf_counter() - t0)
-
-  def decode(self, pk, torch):
-    """Device half of load(): upload, kernels, status, host fall-back for the
-    frames the device did not take. Returns the (n, H, W) float32 frames."""
-    n, H, W, paths, scales, sc, workers = (len(pk.paths), pk.H, pk.W, pk.paths, pk.scales, pk.sc,
-                                           pk.workers)
-    dev = torch.device("cuda", self.device)
-    frames = torch.empty((n, H, W), dtype=torch.float32, device=dev)
-    if n == 0:
-      return frames
-    if pk.host_only:
-      frames.copy_(torch.from_numpy(_host_frames(paths, scales, H, W, workers)))
-      torch.cuda.current_stream(dev).synchronize()
-      self.last_host = n
-      return frames
+    pend = Pending(paths=paths, scales=scales, sc=sc, H=int(H), W=int(W), workers=workers,
+                   frames=frames, n=n, host_only=n == 0 or W > MAX_WIDTH or
+                   H * (2 * W + 1) > MAX_RAW, t0=time.perf_counter(), pack_s=0.0)
+    if pend.host_only:  # nothing, or outside the kernel's range: host decoder in finish()
+      return pend
+    L = _io()
+    enc = [os.fsencode(q) for q in paths]
+    z_off = np.zeros(n, np.int64)
+    z_len = np.zeros(n, np.int32)
+    st = np.zeros(n, np.int32)
+    need = ctypes.c_int64(0)
+    hh = (ctypes.c_int * n)(*([int(H)] * n))
+    ww = (ctypes.c_int * n)(*([int(W)] * n))
+    # the whole batch's layout (file sizes, 256-byte aligned), one stat per file
+    L.bopx_pack_depth_pngs((ctypes.c_char_p * n)(*enc), n, hh, ww, None, 0, z_off.ctypes.data,
+                           z_len.ctypes.data, 0, st.ctypes.data, ctypes.byref(need))
+    z_d = torch.empty(need.value, dtype=torch.uint8, device=dev)
+    if self._copy_stream is None:
+      self._copy_stream = torch.cuda.Stream(dev)
+    cs = self._copy_stream
+    cs.wait_stream(stream)  # z_d's allocation is ordered on `stream`
+    nt = int(workers or min(16, os.cpu_count() or 1))
+    for k, c0 in enumerate(range(0, n, self.CHUNK)):
+      c1 = min(n, c0 + self.CHUNK)
+      m = c1 - c0
+      slot = k & 1
+      if self._copied[slot] is not None:
+        self._copied[slot].synchronize()  # the slot's previous bytes are up
+      t = time.perf_counter()
+      off = np.zeros(m, np.int64)
+      ln = np.zeros(m, np.int32)
+      cst = np.zeros(m, np.int32)
+      cneed = ctypes.c_int64(0)
+      cp = (ctypes.c_char_p * m)(*enc[c0:c1])
+      L.bopx_pack_depth_pngs(cp, m, hh, ww, None, 0, off.ctypes.data, ln.ctypes.data, 0,
+                             cst.ctypes.data, ctypes.byref(cneed))
+      buf = self._staging(torch, cneed.value, slot)
+      rc = L.bopx_pack_depth_pngs(cp, m, hh, ww, buf.data_ptr(), buf.numel(), off.ctypes.data,
+                                  ln.ctypes.data, nt, cst.ctypes.data, ctypes.byref(cneed))
+      if rc < 0:
+        raise RuntimeError("bopx_pack_depth_pngs: %d bytes needed" % cneed.value)
+      pend.pack_s += time.perf_counter() - t
+      base = int(z_off[c0])
+      if not np.array_equal(off + base, z_off[c0:c1]):  # a file changed size since the stat
+        raise RuntimeError("depth PNG files changed while being packed")
+      nbytes = int(cneed.value) - 2048  # the chunk's files (the pad is the next chunk's)
+      with torch.cuda.stream(cs):
+        z_d[base:base + nbytes].copy_(buf[:nbytes], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(cs)
+      self._copied[slot] = ev
+      z_len[c0:c1] = ln
+      st[c0:c1] = cst
+    stream.wait_stream(cs)  # the kernels read the uploaded bytes
+    z_d.record_stream(cs)
     t1 = time.perf_counter()
-    stream = torch.cuda.current_stream(dev)
-    z_d = pk.buf[:pk.need].to(dev, non_blocking=True)
-    off_d = torch.from_numpy(pk.z_off).to(dev)
-    len_d = torch.from_numpy(pk.z_len).to(dev)
+    off_d = torch.from_numpy(z_off).to(dev)
+    len_d = torch.from_numpy(z_len).to(dev)
     sc_d = torch.from_numpy(sc).to(dev)
     raw_stride = raw_stride_of(H, W)
     raw = torch.empty(n * raw_stride, dtype=torch.uint8, device=dev)
@@ -167,26 +205,44 @@ class DepthDecoder:
     self.ctx.call("bopx_png_decode_dev", n, z_d.data_ptr(), off_d.data_ptr(), len_d.data_ptr(),
                   int(H), int(W), sc_d.data_ptr(), raw.data_ptr(), raw_stride, frames.data_ptr(),
                   status.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
-    gst = status.view(n, 2)[:, 0].cpu().numpy()  # synchronises: staging reusable after this
-    del raw, z_d
+    pend.__dict__.update(st=st, status=status, stream=stream, keep=(z_d, raw, off_d, len_d, sc_d),
+                         t1=t1)
+    return pend
+
+  def finish(self, pend, torch):
+    """Wait for a submitted batch: (n, H, W) float32 frames, final on return."""
+    n, H, W, paths, scales, sc, workers = (pend.n, pend.H, pend.W, pend.paths, pend.scales,
+                                           pend.sc, pend.workers)
+    frames = pend.frames
+    if n == 0:
+      return frames
+    dev = torch.device("cuda", self.device)
+    if pend.host_only:
+      frames.copy_(torch.from_numpy(_host_frames(paths, scales, H, W, workers)))
+      torch.cuda.current_stream(dev).synchronize()
+      self.last_host = n
+      return frames
+    gst = pend.status.view(n, 2)[:, 0].cpu().numpy()  # synchronises with the kernels
+    pend.keep = None
     t2 = time.perf_counter()
-    host = np.nonzero((pk.st != 0) | (gst != 0))[0]
+    host = np.nonzero((pend.st != 0) | (gst != 0))[0]
     if len(host):
       arr = _host_frames([paths[k] for k in host], None if scales is None else
                          [float(sc[k]) for k in host], H, W, workers)
       frames[torch.from_numpy(host).to(dev)] = torch.from_numpy(arr).to(dev)
-      # the index_put is queued on `stream`; callers consume the frames on other
-      # streams (the scene prefetch threads), so the frames are final on return
-      stream.synchronize()
+      # the index_put is queued on the batch's stream; callers consume the
+      # frames on other streams (the scene prefetch threads): final on return
+      pend.stream.synchronize()
     self.last_host = len(host)
-    _stat(calls=1, frames=n, pack_s=pk.pack_s, decode_s=t2 - t1, host_s=time.perf_counter() - t2)
+    _stat(calls=1, frames=n, pack_s=pend.pack_s, decode_s=t2 - pend.t0 - pend.pack_s,
+          host_s=time.perf_counter() - t2)
     return frames
 
   def load(self, paths, scales, H, W, torch, workers=None):
     """(n, H, W) float32 frames on the device: sample * (float32)scales[k]
     (scales None: 1). Raises ValueError like inout.load_depths when a file
     that the device decoder cannot take has another size."""
-    return self.decode(self.pack(paths, scales, H, W, torch, workers), torch)
+    return self.finish(self.submit(paths, scales, H, W, torch, workers), torch)
 
 
 class GroupPrefetch:
@@ -194,45 +250,41 @@ class GroupPrefetch:
 
   A scene's frames alone leave most of the chip idle during k_png_inflate (one
   wave per stream: a launch takes one stream's latency, ~70 ms for 640x480
-  frames, whether it holds 100 or 5,000 streams). A packing thread walks the
-  scenes in order, collects their PNG paths (items: (key, thunk), thunk() ->
-  (paths, scales), run in that thread) until a group holds max_frames frames,
-  and packs the group on host threads (DepthDecoder.pack) into one of two
-  staging slots; a decoding thread uploads and decodes the groups in order
-  (DepthDecoder.decode on `stream`), so group g + 1 is read and checked while
-  group g is on the GPU. Each scene gets its slice of its group's frames. At
-  most max_groups decoded groups wait for their consumer (device memory
-  bound). get(key) blocks until the scene's frames are final and returns them
-  (None: no images; raises the decoder's ValueError for a group it could not
-  take, e.g. a frame of another size).
+  frames, whether it holds 100 or 5,000 streams; past ~3,000 frames it is
+  throughput-bound, tools/png_occupancy.py). A worker thread walks the scenes
+  in order, collects their PNG paths (items: (key, thunk), thunk() ->
+  (paths, scales), run in the worker) until a group holds max_frames frames,
+  and submits the group (DepthDecoder.submit on `stream`: chunked packing on
+  host threads, uploads on a copy stream, one kernel launch); it then
+  finishes the previous group (status, host fall-back), so a group's
+  packing and upload overlap the previous group's kernels. Each scene gets
+  its slice of its group's frames. At most max_groups (>= 2) submitted groups
+  wait for their consumer (device memory bound). get(key) blocks until the
+  scene's frames are final and returns them (None: no images; raises the
+  decoder's ValueError for a group it could not take, e.g. a frame of
+  another size).
   """
 
   def __init__(self, device, items, H, W, torch, stream, consumer, max_frames=4096, max_groups=2):
     import concurrent.futures as cf
-    import queue
     self._torch = torch
     self._items = list(items)
     self._fut = {k: cf.Future() for k, _ in self._items}
     self._left = {}  # group id -> keys not yet taken
     self._group_of = {}
-    self._sem = threading.Semaphore(max_groups)
-    self._slot_free = [threading.Semaphore(1), threading.Semaphore(1)]
+    self._sem = threading.Semaphore(max(2, int(max_groups)))
     self._lock = threading.Lock()
-    self._q = queue.Queue(maxsize=1)
     self._stop = False
     self.H, self.W, self.max_frames = int(H), int(W), int(max_frames)
     self.stream, self.consumer, self.device = stream, consumer, device
     self.groups = 0
-    # the decoding thread creates the decoder's context (lazy); the packing
-    # thread only fills its page-locked staging slots
-    self._dec = DepthDecoder(device, lazy=True)
-    self._packer = threading.Thread(target=self._pack_run, name="bopx-depth-pack", daemon=True)
-    self._decoder = threading.Thread(target=self._decode_run, name="bopx-depth-decode",
-                                     daemon=True)
-    self._packer.start()
-    self._decoder.start()
+    self._thread = threading.Thread(target=self._run, name="bopx-depth-groups", daemon=True)
+    self._thread.start()
 
-  def _pack_run(self):
+  def _run(self):
+    # the worker's decoder (its libbopx context lives on this thread)
+    self._dec = DepthDecoder(self.device, lazy=True)
+    prev = None
     pending, n = [], 0
     try:
       for key, thunk in self._items:
@@ -249,65 +301,57 @@ class GroupPrefetch:
         pending.append((key, paths, scales))
         n += len(paths)
         if n >= self.max_frames:
-          self._pack(pending)
-          pending, n = [], 0
+          cur = self._submit(pending)
+          self._finish(prev)
+          prev, pending, n = cur, [], 0
       if pending and not self._stop:
-        self._pack(pending)
+        cur = self._submit(pending)
+        self._finish(prev)
+        prev = cur
+      self._finish(prev)
     finally:
-      self._q.put(None)  # end of groups
+      for f in self._fut.values():
+        if not f.done():
+          f.set_exception(RuntimeError("depth prefetch stopped"))
 
-  def _pack(self, pending):
+  def _submit(self, pending):
+    torch = self._torch
+    self._sem.acquire()  # at most max_groups submitted groups wait for their consumer
+    if self._stop:
+      return None
     gid = self.groups
     self.groups += 1
-    slot = gid & 1
-    self._slot_free[slot].acquire()  # the decode of group gid - 2 is done with the slot
-    if self._stop:
-      self._slot_free[slot].release()
-      return
+    with self._lock:
+      self._left[gid] = len(pending)
+      for key, _, _ in pending:
+        self._group_of[key] = gid
     paths = [q for _, ps, _ in pending for q in ps]
     scales = [c for _, _, cs in pending for c in cs]
     try:
-      pk = self._dec.pack(paths, scales, self.H, self.W, self._torch, slot=slot)
+      with torch.cuda.stream(self.stream):
+        pend = self._dec.submit(paths, scales, self.H, self.W, torch)
     except BaseException as e:  # noqa: BLE001
-      self._slot_free[slot].release()
+      for key, _, _ in pending:
+        self._fut[key].set_exception(e)
+      return None
+    return pending, pend
+
+  def _finish(self, job):
+    if job is None:
+      return
+    pending, pend = job
+    torch = self._torch
+    try:
+      frames = self._dec.finish(pend, torch)
+      frames.record_stream(self.consumer)  # freed behind the consumer's use
+    except BaseException as e:  # noqa: BLE001
       for key, _, _ in pending:
         self._fut[key].set_exception(e)
       return
-    self._q.put((gid, slot, pending, pk))
-
-  def _decode_run(self):
-    torch = self._torch
-    while True:
-      job = self._q.get()
-      if job is None:
-        break
-      gid, slot, pending, pk = job
-      try:
-        if not self._stop:
-          self._sem.acquire()  # at most max_groups decoded groups wait for their consumer
-        if self._stop:
-          continue  # drain the queue (the finally frees the slot)
-        with self._lock:
-          self._left[gid] = len(pending)
-          for key, _, _ in pending:
-            self._group_of[key] = gid
-        try:
-          with torch.cuda.stream(self.stream):
-            frames = self._dec.decode(pk, torch)
-          frames.record_stream(self.consumer)  # freed behind the consumer's use
-        except BaseException as e:  # noqa: BLE001
-          for key, _, _ in pending:
-            self._fut[key].set_exception(e)
-          continue
-        o = 0
-        for key, ps, _ in pending:
-          self._fut[key].set_result(frames[o:o + len(ps)])
-          o += len(ps)
-      finally:
-        self._slot_free[slot].release()
-    for f in self._fut.values():
-      if not f.done():
-        f.set_exception(RuntimeError("depth prefetch stopped"))
+    o = 0
+    for key, ps, _ in pending:
+      self._fut[key].set_result(frames[o:o + len(ps)])
+      o += len(ps)
 
   def get(self, key):
     try:
@@ -324,14 +368,7 @@ class GroupPrefetch:
   def close(self):
     self._stop = True
     self._sem.release()
-    for sf in self._slot_free:
-      sf.release()
-    try:
-      self._q.put_nowait(None)
-    except Exception:  # noqa: BLE001 - full: the decoder still has a job; it sees _stop
-      pass
-    self._packer.join(timeout=60)
-    self._decoder.join(timeout=60)
+    self._thread.join(timeout=60)
 
   def __enter__(self):
     return self

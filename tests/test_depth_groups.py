@@ -39,13 +39,13 @@ def fake_decoder(monkeypatch):
     def __init__(self, device, lazy=False):
       pass
 
-    def pack(self, paths, scales, H, W, torch, workers=None, slot=0):
+    def submit(self, paths, scales, H, W, torch, workers=None):
+      calls.append(list(paths))
       return list(paths)
 
-    def decode(self, paths, torch):
+    def finish(self, paths, torch):
       if any(p.startswith("bad") for p in paths):
         raise ValueError("frame of another size")
-      calls.append(list(paths))
       arr = np.array([[int(p.split(":")[1])] for p in paths])  # one value per frame
       return _Frames(arr)
   monkeypatch.setattr(depth_gpu, "DepthDecoder", Dec)
@@ -99,25 +99,25 @@ def test_at_most_max_groups_wait(fake_decoder):
                               max_groups=2)
   try:
     time.sleep(0.3)
-    assert len(fake_decoder) == 2  # nothing taken yet: two groups decoded, the decoder waits
+    assert len(fake_decoder) == 2  # nothing taken yet: two groups submitted, the worker waits
     g.get(0)
     time.sleep(0.3)
     assert len(fake_decoder) == 3
   finally:
     g.close()
-  assert not g._packer.is_alive() and not g._decoder.is_alive()
+  assert not g._thread.is_alive()
 
 
 def test_close_while_groups_wait(fake_decoder):
   """A consumer that stops early (an error in the scene loop): close() ends
   both threads at once, with groups packed and decoded but not taken."""
   g = depth_gpu.GroupPrefetch(0, [_scene(k, 4) for k in range(10)], 4, 4, _fake_torch(), None,
-                              None, max_frames=4, max_groups=1)
+                              None, max_frames=4, max_groups=2)
   assert len(g.get(0)) == 4
   time.sleep(0.2)
   t = time.perf_counter()
   g.close()
   assert time.perf_counter() - t < 5
-  assert not g._packer.is_alive() and not g._decoder.is_alive()
+  assert not g._thread.is_alive()
   with pytest.raises(RuntimeError):
     g.get(9)

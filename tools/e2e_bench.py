@@ -232,8 +232,8 @@ def main():
       finally:
         tl.append((name, t, time.perf_counter()))
     return wrap
-  depth_gpu.DepthDecoder.pack = traced("decoder.pack", depth_gpu.DepthDecoder.pack)
-  depth_gpu.DepthDecoder.decode = traced("decoder.decode", depth_gpu.DepthDecoder.decode)
+  depth_gpu.DepthDecoder.submit = traced("decoder.submit", depth_gpu.DepthDecoder.submit)
+  depth_gpu.DepthDecoder.finish = traced("decoder.finish", depth_gpu.DepthDecoder.finish)
   inout.load_bop_results = traced("load_bop_results", inout.load_bop_results)
   for nm in ("organize", "evaluate_batch_arrays", "run"):
     setattr(ece, nm, traced(nm, getattr(ece, nm)))
