@@ -158,27 +158,32 @@ __device__ int build_code(const uint8_t* lens, int n, Tab* tab, uint16_t* sorted
 
 // A code longer than ROOT: the smallest length L > ROOT with the 15 bits
 // (first bit most significant) below lim[L]; -1 if none (no such code).
-// Second literals in the literal/length root table: entry e (bits of the
-// window, first bit lowest) whose code is a literal of length L1 leaves
+// High half of the literal/length root table entries, for the window loop:
+// bits 24-30 = the bits a chain step consumes (kStop: the entry is not a
+// literal with a code of <= ROOT bits, the chain stops there), bit 31 = the
+// step emits a second literal, bits 16-23 = that literal. Entry e (bits of
+// the window, first bit lowest) whose code is a literal of length L1 leaves
 // ROOT - L1 known bits; if they hold a whole literal code of length L2 (the
 // table entry of those bits with the unknown high bits zero has L2 <= ROOT -
-// L1: a code shorter than ROOT is replicated over every suffix), entry e
-// gets sym2 << 20 | L2 << 16 in its high half. The window loop then takes two
-// literals per chain step (Huffman-coded depth rows: ~40 % 1-bit codes).
+// L1: a code shorter than ROOT is replicated over every suffix), the step
+// takes both (L1 + L2 bits). Depth rows are ~40 % 1-bit codes.
+constexpr uint32_t kStop = 127;
 template <int ROOT>
-__device__ void add_literal_pairs(uint32_t* tab, int lane) {
+__device__ void add_literal_steps(uint32_t* tab, int lane) {
 #pragma unroll 1
   for (int j = 0; j < (1 << ROOT) / 64; ++j) {
     const int e = j * 64 + lane;
     const uint32_t t = tab[e] & 0xFFFFu;
-    uint32_t pair = 0;
+    uint32_t hi = kStop << 24;
     if (t < (256u << 4)) {  // a literal with a code of <= ROOT bits
       const int L1 = (int)(t & 15u);
       const uint32_t t2 = tab[e >> L1] & 0xFFFFu;
-      if (t2 < (256u << 4) && (int)(t2 & 15u) <= ROOT - L1) pair = (t2 >> 4) << 20 | (t2 & 15u) << 16;
+      hi = (uint32_t)L1 << 24;
+      if (t2 < (256u << 4) && (int)(t2 & 15u) <= ROOT - L1)
+        hi = 1u << 31 | (uint32_t)(L1 + (int)(t2 & 15u)) << 24 | (t2 >> 4) << 16;
     }
     wave_sync();  // every lane has read before any high half is written
-    tab[e] = t | pair;
+    tab[e] = t | hi;
   }
   wave_sync();
 }
@@ -360,7 +365,7 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
     }
     if (build_code<kLitRoot>(S.lens, hlit, S.lit, S.sorted, lit_lim, lit_base, lane) != 0)
       return kErr;
-    add_literal_pairs<kLitRoot>(S.lit, lane);
+    add_literal_steps<kLitRoot>(S.lit, lane);
     const int dst =
         build_code<kDistRoot>(S.lens + 288, hdist, S.dist, S.sorted + 288, dist_lim, dist_base, lane);
     if (dst < 0) return kErr;
@@ -370,34 +375,34 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
       // Literal runs, a bit-buffer window at a time: lane l looks the table up
       // at bit offset l (one LDS gather), the chain of short literal codes
       // through the window is followed with v_readlane (no LDS round trip per
-      // symbol), and the lanes on the chain store their bytes at once.
-        if (nb <= 32 && !refill_word()) return kErr;
+      // symbol), and the lanes on the chain store their bytes at once. A step
+      // is taken while its code(s) end inside the buffer's nb valid bits: the
+      // bits above nb are zero, and a code that reaches past them cannot match
+      // a shorter entry (prefix-free), so its entry's step ends past nb too.
+      if (nb <= 32 && !refill_word()) return kErr;
       if (nb <= 32 && !refill_word()) return kErr;  // nb in (32, 64]
-      const int lim = nb - kLitRoot;  // offsets whose lookup bits lie in the buffer
+      const int lim = min(nb, 63);  // chain offsets stay lane indices
       const uint32_t ev = S.lit[(uint32_t)(bb >> lane) & ((1 << kLitRoot) - 1)];
       int e, off = 0;
-      uint64_t run = 0;  // bit l: a literal code (or a pair of them) starts at offset l
+      uint64_t run = 0;  // bit l: a chain step (one or two literals) starts at offset l
       for (;;) {
         e = __builtin_amdgcn_readlane((int)ev, off);
-        if ((e & 0xFFFF) >= 256 << 4) break;  // not a literal with a short code: below
+        const int nxt = off + ((e >> 24) & (int)kStop);
+        if (nxt > lim) break;
         run |= 1ull << off;
-        off += (e & 15) + ((e >> 16) & 15);
-        if (off > lim) {
-          e = -1;  // the window is used up
-          break;
-        }
+        off = nxt;
       }
       if (run) {
         const bool on = (run >> lane) & 1;
-        const uint64_t run2 = __ballot(on && (ev >> 16) != 0u);  // chain steps with two literals
+        const uint64_t run2 = __ballot(on && (int)ev < 0);  // chain steps with two literals
         const int nlit = __popcll(run) + __popcll(run2);
         if (nlit > out_n - p) return kErr;
-        bb = off < 64 ? bb >> off : 0;
+        bb >>= off;  // off <= 63
         nb -= off;
         if (on) {
           const int q = p + popc_lt(run) + popc_lt(run2);
           S.ring[q & kRingMask] = (uint8_t)(ev >> 4);
-          if (ev >> 16) S.ring[(q + 1) & kRingMask] = (uint8_t)(ev >> 20);
+          if ((int)ev < 0) S.ring[(q + 1) & kRingMask] = (uint8_t)(ev >> 16);
         }
         p += nlit;
         while (p - flushed >= kFlush) {
@@ -405,10 +410,11 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
           flushed += kFlush;
         }
       }
-      if (e < 0) continue;
-      // e: the entry at the current position (a window leaves >= kLitRoot bits;
-      // a long code plus length extra bits need up to 20)
+      if (((e >> 24) & (int)kStop) != (int)kStop) continue;  // a literal past the window
+      // not a literal with a short code: its entry again, from valid bits (a
+      // long code plus length extra bits need up to 20)
       if (nb <= 32 && !refill_word()) return kErr;
+      e = uni((int)(S.lit[(uint32_t)bb & ((1 << kLitRoot) - 1)] & 0xFFFFu));
       int L = e & 15, sym = e >> 4;
       if (e == kNoCode) {
         const int idx = slow_index<kLitRoot>(bb, lit_lim, lit_base, lane, L);
