@@ -141,7 +141,7 @@ class DepthDecoder:
     sc = np.ones(n, np.float32) if scales is None else np.asarray(
         [np.float32(float(s)) for s in scales], np.float32)
     pend = Pending(paths=paths, scales=scales, sc=sc, H=int(H), W=int(W), workers=workers,
-                   frames=frames, n=n, host_only=n == 0 or W > MAX_WIDTH or
+                   frames=frames, n=n, stream=stream, host_only=n == 0 or W > MAX_WIDTH or
                    H * (2 * W + 1) > MAX_RAW, t0=time.perf_counter(), pack_s=0.0)
     if pend.host_only:  # nothing, or outside the kernel's range: host decoder in finish()
       return pend
@@ -205,24 +205,34 @@ class DepthDecoder:
     self.ctx.call("bopx_png_decode_dev", n, z_d.data_ptr(), off_d.data_ptr(), len_d.data_ptr(),
                   int(H), int(W), sc_d.data_ptr(), raw.data_ptr(), raw_stride, frames.data_ptr(),
                   status.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
-    pend.__dict__.update(st=st, status=status, stream=stream, keep=(z_d, raw, off_d, len_d, sc_d),
+    pend.__dict__.update(st=st, status=status, keep=(z_d, raw, off_d, len_d, sc_d),
                          t1=t1)
     return pend
 
   def finish(self, pend, torch):
-    """Wait for a submitted batch: (n, H, W) float32 frames, final on return."""
+    """Wait for a submitted batch: (n, H, W) float32 frames, final on return.
+
+    May run on another thread than submit: everything here is queued on the
+    batch's stream (a thread's current stream does not order after the
+    batch's kernels), and the batch's stream is drained before returning."""
+    frames = pend.frames
+    if pend.n == 0:
+      return frames
+    with torch.cuda.stream(pend.stream):
+      self._finish_on_stream(pend, torch)
+    pend.stream.synchronize()
+    return frames
+
+  def _finish_on_stream(self, pend, torch):
     n, H, W, paths, scales, sc, workers = (pend.n, pend.H, pend.W, pend.paths, pend.scales,
                                            pend.sc, pend.workers)
     frames = pend.frames
-    if n == 0:
-      return frames
     dev = torch.device("cuda", self.device)
     if pend.host_only:
       frames.copy_(torch.from_numpy(_host_frames(paths, scales, H, W, workers)))
-      torch.cuda.current_stream(dev).synchronize()
       self.last_host = n
-      return frames
-    gst = pend.status.view(n, 2)[:, 0].cpu().numpy()  # synchronises with the kernels
+      return
+    gst = pend.status.view(n, 2)[:, 0].cpu().numpy()  # waits for the kernels
     pend.keep = None
     t2 = time.perf_counter()
     host = np.nonzero((pend.st != 0) | (gst != 0))[0]
@@ -230,13 +240,9 @@ class DepthDecoder:
       arr = _host_frames([paths[k] for k in host], None if scales is None else
                          [float(sc[k]) for k in host], H, W, workers)
       frames[torch.from_numpy(host).to(dev)] = torch.from_numpy(arr).to(dev)
-      # the index_put is queued on the batch's stream; callers consume the
-      # frames on other streams (the scene prefetch threads): final on return
-      pend.stream.synchronize()
     self.last_host = len(host)
     _stat(calls=1, frames=n, pack_s=pend.pack_s, decode_s=t2 - pend.t0 - pend.pack_s,
           host_s=time.perf_counter() - t2)
-    return frames
 
   def load(self, paths, scales, H, W, torch, workers=None):
     """(n, H, W) float32 frames on the device: sample * (float32)scales[k]

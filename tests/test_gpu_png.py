@@ -157,6 +157,39 @@ def test_gpu_decode_host_rows_final_for_other_streams(tmp_path, dec):
   assert np.array_equal(snap.cpu().numpy(), _host(paths, [0.1] * len(paths), h, w))
 
 
+def test_group_prefetch_frames_final_for_consumer(tmp_path):
+  """GroupPrefetch submits and finishes groups on its worker thread (whose
+  current stream is not the decode stream): every scene's slice is the host
+  decode when get() returns, read on a third stream without further sync,
+  across several groups and one host-only file."""
+  if not torch.cuda.is_available():
+    pytest.skip("no GPU")
+  from bop_toolkit_amd import depth_gpu
+  rng = np.random.default_rng(29)
+  h, w = 480, 640
+  scenes = {}
+  for s in range(5):
+    ps = []
+    for k in range(3 + s):
+      p = str(tmp_path / ("s%d_%d.png" % (s, k)))
+      if s == 2 and k == 1:
+        Image.fromarray((_image(rng, 0, h, w) % 256).astype(np.uint8)).save(p)
+      else:
+        write_png16(p, _image(rng, (s + k) % 6, h, w))
+      ps.append(p)
+    scenes[s] = ps
+  items = [(s, (lambda ps=ps: (ps, [0.1] * len(ps)))) for s, ps in scenes.items()]
+  stream, consumer = torch.cuda.Stream(), torch.cuda.Stream()
+  with depth_gpu.GroupPrefetch(0, items, h, w, torch, stream, consumer, max_frames=7) as g:
+    for s, ps in scenes.items():
+      fr = g.get(s)
+      with torch.cuda.stream(consumer):
+        snap = fr.clone()
+      consumer.synchronize()
+      assert np.array_equal(snap.cpu().numpy(), _host(ps, [0.1] * len(ps), h, w)), s
+    assert g.groups >= 3
+
+
 def test_gpu_decode_rejects_what_the_host_rejects(tmp_path, dec):
   """Mutated zlib streams (valid chunk CRCs, so the packer passes them on):
   a stream the device accepts decodes to the host decoder's frame; any other
