@@ -234,6 +234,7 @@ def main():
     return wrap
   depth_gpu.DepthDecoder.submit = traced("decoder.submit", depth_gpu.DepthDecoder.submit)
   depth_gpu.DepthDecoder.finish = traced("decoder.finish", depth_gpu.DepthDecoder.finish)
+  depth_gpu.GroupPrefetch.get = traced("groups.get", depth_gpu.GroupPrefetch.get)
   inout.load_bop_results = traced("load_bop_results", inout.load_bop_results)
   for nm in ("organize", "evaluate_batch_arrays", "run"):
     setattr(ece, nm, traced(nm, getattr(ece, nm)))
@@ -302,6 +303,7 @@ def main():
       os.environ["BOPX_DEPTH_GPU"] = env
       t0 = time.perf_counter()
       marks.clear()
+      tl.clear()
       fin = eval_bop19_pose.evaluate(p)
       t_run = time.perf_counter() - t0
       ab[name] = {"eval_bop19_s": round(t_run, 2), "tail": tail_info(t0 + t_run),
@@ -311,7 +313,11 @@ def main():
                   "host_s": {k[5:]: round(v, 3) for k, v in phases.items()
                              if k.startswith("host:") and v},
                   "eval_tuples_per_s": n / t_run,
-                  "identical_scores": fin[os.path.splitext(result)[0]] == scores}
+                  "identical_scores": fin[os.path.splitext(result)[0]] == scores,
+                  "timeline": timeline(t0),
+                  # the host steps one by one (name, start, end; s from the run's start)
+                  "events": [(nm, round(e0 - t0, 4), round(e1 - t0, 4))
+                             for nm, e0, e1 in sorted(tl, key=lambda x: x[1])]}
     os.environ.pop("BOPX_DEPTH_GPU")
     os.environ.pop("BOPX_DEPTH_GROUP_FRAMES", None)
     phases.clear()

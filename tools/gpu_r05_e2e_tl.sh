@@ -1,0 +1,10 @@
+#!/bin/bash
+# 100k e2e with per-event host timelines of the warm runs (tools/e2e_bench.py)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${TAG:-r05t}
+timeout -k 10 480 python tools/e2e_bench.py --images 16667 --ab-depth --ab-group ${DEPTH_GROUPS:-4096} > gpurun_out/e2e_100k_${TAG}.json 2> gpurun_out/e2e_100k_${TAG}.err || { tail -20 gpurun_out/e2e_100k_${TAG}.err; exit 1; }
+python -c "
+import json; d=json.load(open('gpurun_out/e2e_100k_${TAG}.json'))
+print('cold', d['eval_bop19_s'], d['errors_s'], d['tail'])
+for k,v in d['ab_depth'].items(): print(k, v['eval_bop19_s'], v['errors_s'], v['depth_decoder'], v['identical_scores'])"
