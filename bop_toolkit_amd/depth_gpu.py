@@ -261,17 +261,19 @@ class GroupPrefetch:
   in order, collects their PNG paths (items: (key, thunk), thunk() ->
   (paths, scales), run in the worker) until a group holds max_frames frames,
   and submits the group (DepthDecoder.submit on `stream`: chunked packing on
-  host threads, uploads on a copy stream, one kernel launch); it then
-  finishes the previous group (status, host fall-back), so a group's
-  packing and upload overlap the previous group's kernels. Each scene gets
-  its slice of its group's frames. At most max_groups (>= 2) submitted groups
-  wait for their consumer (device memory bound). get(key) blocks until the
+  host threads, uploads on a copy stream, one kernel launch), so a group's
+  packing and upload overlap the previous group's kernels; a second thread
+  finishes the groups in order (status readback, host fall-back) as their
+  kernels end. Each scene gets its slice of its group's frames. The first
+  group closes at first_frames (default max_frames). At most max_groups
+  (>= 2) submitted groups wait for their consumer (device memory bound). get(key) blocks until the
   scene's frames are final and returns them (None: no images; raises the
   decoder's ValueError for a group it could not take, e.g. a frame of
   another size).
   """
 
-  def __init__(self, device, items, H, W, torch, stream, consumer, max_frames=4096, max_groups=2):
+  def __init__(self, device, items, H, W, torch, stream, consumer, max_frames=4096, max_groups=2,
+               first_frames=None):
     import concurrent.futures as cf
     self._torch = torch
     self._items = list(items)
@@ -282,6 +284,8 @@ class GroupPrefetch:
     self._lock = threading.Lock()
     self._stop = False
     self.H, self.W, self.max_frames = int(H), int(W), int(max_frames)
+    # the first group may be smaller (the consumer starts on it sooner)
+    self.first_frames = int(max_frames if first_frames is None else max(1, first_frames))
     self.stream, self.consumer, self.device = stream, consumer, device
     self.groups = 0
     self._thread = threading.Thread(target=self._run, name="bopx-depth-groups", daemon=True)
@@ -290,8 +294,16 @@ class GroupPrefetch:
   def _run(self):
     # the worker's decoder (its libbopx context lives on this thread)
     self._dec = DepthDecoder(self.device, lazy=True)
-    prev = None
+    # groups are finished (status readback, host fall-back) on a thread of
+    # their own, in submission order, so a group's frames are released when
+    # its kernels end, not after the next group's packing
+    import queue
+    fin_q = queue.Queue()
+    fin = threading.Thread(target=self._finisher, args=(fin_q,), name="bopx-depth-finish",
+                           daemon=True)
+    fin.start()
     pending, n = [], 0
+    cap = self.first_frames
     try:
       for key, thunk in self._items:
         if self._stop:
@@ -306,19 +318,24 @@ class GroupPrefetch:
           continue
         pending.append((key, paths, scales))
         n += len(paths)
-        if n >= self.max_frames:
-          cur = self._submit(pending)
-          self._finish(prev)
-          prev, pending, n = cur, [], 0
+        if n >= cap:
+          fin_q.put(self._submit(pending))
+          pending, n, cap = [], 0, self.max_frames
       if pending and not self._stop:
-        cur = self._submit(pending)
-        self._finish(prev)
-        prev = cur
-      self._finish(prev)
+        fin_q.put(self._submit(pending))
     finally:
+      fin_q.put(StopIteration)
+      fin.join()
       for f in self._fut.values():
         if not f.done():
           f.set_exception(RuntimeError("depth prefetch stopped"))
+
+  def _finisher(self, q):
+    while True:
+      job = q.get()
+      if job is StopIteration:
+        return
+      self._finish(job)
 
   def _submit(self, pending):
     torch = self._torch

@@ -121,3 +121,27 @@ def test_close_while_groups_wait(fake_decoder):
   assert not g._thread.is_alive()
   with pytest.raises(RuntimeError):
     g.get(9)
+
+
+def test_first_group_and_release_before_next_pack(fake_decoder, monkeypatch):
+  """A smaller first group (first_frames), and a group's frames are released
+  as soon as it is finished, while the next group's submit (packing) is still
+  running (finishing runs on its own thread)."""
+  gate = threading.Event()
+  sub0 = depth_gpu.DepthDecoder.submit
+
+  def slow_submit(self, paths, scales, H, W, torch, workers=None):
+    if fake_decoder:  # every group after the first waits for the gate
+      gate.wait(5)
+    return sub0(self, paths, scales, H, W, torch, workers)
+  monkeypatch.setattr(depth_gpu.DepthDecoder, "submit", slow_submit)
+  items = [_scene(k, 2) for k in range(6)]
+  with depth_gpu.GroupPrefetch(0, items, 4, 4, _fake_torch(), None, None, max_frames=6,
+                               first_frames=2) as g:
+    t = time.perf_counter()
+    assert len(g.get(0)) == 2
+    assert time.perf_counter() - t < 2  # not held back by the second group's submit
+    gate.set()
+    for k in range(1, 6):
+      assert len(g.get(k)) == 2
+  assert [len(c) for c in fake_decoder] == [2, 6, 4]
