@@ -52,9 +52,10 @@ constexpr uint16_t kNoCode = 0xFFFF;  // table entry: code longer than the root,
 __constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 struct InfLds {
-  // literal/length root table; high half: a second literal whose code fits in
-  // the same kLitRoot bits (add_literal_pairs). Also the code-length code's
-  // table (128 entries, low halves only).
+  // literal/length root table; high half: the entry's chain step (its bit
+  // count, or kStop) and a second literal whose code fits in the same kLitRoot
+  // bits (add_literal_steps). Also the code-length code's table (128 entries,
+  // low halves only).
   uint32_t lit[1 << kLitRoot];
   uint16_t dist[1 << kDistRoot];
   uint16_t sorted[288 + 32];      // symbols by code: literal/length, then distance
