@@ -10,3 +10,8 @@ python -c "
 import json; d=json.load(open('gpurun_out/e2e_100k_${TAG}.json'))
 print('cold', d['eval_bop19_s'], d['errors_s'], d['tail'])
 for k,v in d['ab_depth'].items(): print(k, v['eval_bop19_s'], v['errors_s'], v['depth_decoder'], v['identical_scores'])"
+# the same job under a kernel trace (GPU timeline of the decode and error kernels)
+if [ -n "$KTRACE" ]; then
+  timeout -k 10 600 rocprofv3 --kernel-trace -d gpurun_out/e2e_kt_${TAG} -o run --output-format csv -- python3 tools/e2e_bench.py --images 16667 --ab-depth --ab-group ${KTRACE} --root /tmp/bopx_e2e_kt > gpurun_out/e2e_kt_${TAG}.json 2> gpurun_out/e2e_kt_${TAG}.err || { tail -20 gpurun_out/e2e_kt_${TAG}.err; exit 1; }
+  ls -la gpurun_out/e2e_kt_${TAG}/* | head
+fi
