@@ -156,11 +156,15 @@ class DepthDecoder:
     # the whole batch's layout (file sizes, 256-byte aligned), one stat per file
     L.bopx_pack_depth_pngs((ctypes.c_char_p * n)(*enc), n, hh, ww, None, 0, z_off.ctypes.data,
                            z_len.ctypes.data, 0, st.ctypes.data, ctypes.byref(need))
-    z_d = torch.empty(need.value, dtype=torch.uint8, device=dev)
     if self._copy_stream is None:
       self._copy_stream = torch.cuda.Stream(dev)
     cs = self._copy_stream
-    cs.wait_stream(stream)  # z_d's allocation is ordered on `stream`
+    # the compressed bytes are allocated in the copy stream's order, so the
+    # uploads need not wait for the kernels already queued on `stream` (the
+    # previous batch's decode): a batch is packed and uploaded while the one
+    # before it decodes (z_d is recorded on `stream` below)
+    with torch.cuda.stream(cs):
+      z_d = torch.empty(need.value, dtype=torch.uint8, device=dev)
     nt = int(workers or min(16, os.cpu_count() or 1))
     for k, c0 in enumerate(range(0, n, self.CHUNK)):
       c1 = min(n, c0 + self.CHUNK)
@@ -194,7 +198,7 @@ class DepthDecoder:
       z_len[c0:c1] = ln
       st[c0:c1] = cst
     stream.wait_stream(cs)  # the kernels read the uploaded bytes
-    z_d.record_stream(cs)
+    z_d.record_stream(stream)
     t1 = time.perf_counter()
     off_d = torch.from_numpy(z_off).to(dev)
     len_d = torch.from_numpy(z_len).to(dev)

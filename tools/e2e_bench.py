@@ -235,8 +235,15 @@ def main():
   depth_gpu.DepthDecoder.submit = traced("decoder.submit", depth_gpu.DepthDecoder.submit)
   depth_gpu.DepthDecoder.finish = traced("decoder.finish", depth_gpu.DepthDecoder.finish)
   depth_gpu.GroupPrefetch.get = traced("groups.get", depth_gpu.GroupPrefetch.get)
+  from bop_toolkit_amd import batch as _batch
+  _batch.BatchEvaluator.set_symmetries = traced("ev.set_symmetries",
+                                                _batch.BatchEvaluator.set_symmetries)
+  _batch.BatchEvaluator.add_object = traced("ev.add_object", _batch.BatchEvaluator.add_object)
+  misc.get_symmetry_transformations = traced("get_symmetry_transformations",
+                                             misc.get_symmetry_transformations)
   inout.load_bop_results = traced("load_bop_results", inout.load_bop_results)
-  for nm in ("organize", "evaluate_batch_arrays", "run"):
+  for nm in ("organize", "evaluate_batch_arrays", "run", "Models", "plan_arrays",
+             "scene_arrays_direct_cached"):
     setattr(ece, nm, traced(nm, getattr(ece, nm)))
   inout.save_errors_arrays = traced("save_errors_arrays", inout.save_errors_arrays)
 
