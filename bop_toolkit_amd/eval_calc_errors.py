@@ -63,13 +63,14 @@ def depth_group_frames():
   """VSD test depth of consecutive scenes is decoded in shared k_png_inflate
   launches of about this many frames (depth_gpu.GroupPrefetch;
   BOPX_DEPTH_GROUP_FRAMES=0: one launch per scene, from the scene prefetch;
-  "G/F": groups of G frames, the first one of F)."""
+  "G/F": groups of G frames, the first one of F; default 4096/1024: the error
+  kernels start on a small first group while the next ones decode)."""
   return depth_group_sizes()[0]
 
 
 def depth_group_sizes():
   """(group frames, first group frames) from BOPX_DEPTH_GROUP_FRAMES."""
-  v = os.environ.get("BOPX_DEPTH_GROUP_FRAMES", "4096").split("/")
+  v = os.environ.get("BOPX_DEPTH_GROUP_FRAMES", "4096/1024").split("/")
   g = int(v[0])
   return g, (int(v[1]) if len(v) > 1 else g)
 ERROR_TYPES = ("vsd", "mssd", "mspd", "ad", "add", "adi", "cus", "proj", "rete", "re", "te")
@@ -850,7 +851,7 @@ def run(p, device=0):
           [(sid, (lambda sid=sid, ims=sorted(v): scene_images(sid, ims)))
            for sid, v in scene_ims.items()],
           H_, W_, torch, up[0], up[1], max_frames=depth_group_sizes()[0],
-          first_frames=depth_group_sizes()[1])
+          first_frames=depth_group_sizes()[1], max_groups=3)
     try:
       models_info = None
       if et in ("ad", "add", "adi", "vsd", "mssd", "mspd", "cus"):

@@ -206,21 +206,46 @@ def _score_lib():
   return _SCORE_LIB
 
 
+# Dataset side of the native scorer, kept for the process (like the error
+# passes' file cache): the targets' organised view, the GT table and its
+# ArrayScorer, keyed on the identities of the parsed files they come from
+# (eval_calc_errors.cached_load returns a new object when a file changes), so
+# a second evaluation in the process does not rebuild them in Python while
+# its error passes run (the GIL).
+_DS_CACHE = {}
+_DS_LOCK = None
+
+
+def _ds_cached(key, keep, fn):
+  """fn() cached under key; keep: the objects whose id() is in the key (held
+  with the value so the ids stay theirs)."""
+  import threading
+  global _DS_LOCK
+  if _DS_LOCK is None:
+    _DS_LOCK = threading.RLock()
+  with _DS_LOCK:
+    hit = _DS_CACHE.get(key)
+    if hit is None:
+      if len(_DS_CACHE) > 32:
+        _DS_CACHE.clear()
+      hit = _DS_CACHE[key] = (keep, fn())
+    return hit[1]
+
+
 def _gt_table(cache, dp_split, targets_org, visib_gt_min):
   """The matches file's GT records in order (targets' scenes and images, every
   GT of an image) as arrays, with per-image offsets and scene index
   (score_error_dir's scene_gt / gt_valid, eval_calc_scores.py:183-214)."""
   import numpy as np
+  from .eval_calc_errors import cached_load  # the error passes' parses (same process)
+  gts = [(cached_load(inout.load_scene_gt, dp_split["scene_gt_tpath"].format(scene_id=scene_id)),
+          cached_load(inout.load_json, dp_split["scene_gt_info_tpath"].format(scene_id=scene_id),
+                      keys_to_int=True)) for scene_id in targets_org]
 
   def build():
     sc, im, ob, gid, val, off, fi = [], [], [], [], [], [0], []
-    from .eval_calc_errors import cached_load  # the error passes' parses (same process)
     for k, (scene_id, scene_targets) in enumerate(targets_org.items()):
-      scene_gt = cached_load(inout.load_scene_gt,
-                             dp_split["scene_gt_tpath"].format(scene_id=scene_id))
-      scene_gt_info = cached_load(inout.load_json,
-                                  dp_split["scene_gt_info_tpath"].format(scene_id=scene_id),
-                                  keys_to_int=True)
+      scene_gt, scene_gt_info = gts[k]
       for im_id, tg in scene_targets.items():
         im_gts = scene_gt[im_id]
         valid = valid_gts(im_gts, scene_gt_info[im_id], tg, visib_gt_min)
@@ -235,8 +260,9 @@ def _gt_table(cache, dp_split, targets_org, visib_gt_min):
     i32 = lambda a: np.ascontiguousarray(a, np.int32)
     return (i32(sc), i32(im), i32(ob), i32(gid), np.ascontiguousarray(val, np.uint8),
             np.ascontiguousarray(off, np.int64), i32(fi))
-  key = ("gt_table", dp_split["base_path"], id(targets_org), visib_gt_min)
-  return cache.get(key, build)
+  key = ("gt_table", dp_split["base_path"], id(targets_org), visib_gt_min,
+         tuple((id(a), id(b)) for a, b in gts))
+  return _ds_cached(key, (targets_org, gts), build)
 
 
 def score_error_dir_native(sps, error_dir_path, cache=None, do_print=True, threads=0):
@@ -268,17 +294,17 @@ def score_error_dir_native(sps, error_dir_path, cache=None, do_print=True, threa
   split_type = ds[2] if len(ds) > 2 else None
   dp_split = dataset_params.get_split_params(p["datasets_path"], dataset, split, split_type)
   dp_model = dataset_params.get_model_params(p["datasets_path"], dataset, "eval")
-  models_info = cache.get(("info", dp_model["models_info_path"]), lambda: inout.load_json(
-      dp_model["models_info_path"], keys_to_int=True))
+  from .eval_calc_errors import cached_load  # the error passes' parses (same process)
+  models_info = cached_load(inout.load_json, dp_model["models_info_path"], keys_to_int=True)
   tpath = os.path.join(dp_split["base_path"], p["targets_filename"])
-  targets = cache.get(("targets", tpath), lambda: inout.load_json(tpath))
+  targets = cached_load(inout.load_json, tpath)
 
   def org():
     t_org = {}
     for t in targets:
       t_org.setdefault(t["scene_id"], {}).setdefault(t["im_id"], {})[t["obj_id"]] = t
     return t_org
-  targets_org = cache.get(("targets_org", tpath), org)
+  targets_org = _ds_cached(("targets_org", id(targets)), targets, org)
   sc, im, ob, gid, val, off, fi = _gt_table(cache, dp_split, targets_org, p["visib_gt_min"])
   err_paths = [p["error_tpath"].format(eval_path=p["eval_path"], error_dir_path=error_dir_path,
                                        scene_id=scene_id) for scene_id in targets_org]
@@ -319,7 +345,8 @@ def score_error_dir_native(sps, error_dir_path, cache=None, do_print=True, threa
     return None
   if st != 0:
     raise RuntimeError("bopx_score_folder: %s (status %d)" % (msg.value.decode(), st))
-  scorer = cache.get(("scorer", id(sc), n_top), lambda: score.ArrayScorer(
+  scorer = _ds_cached(("scorer", id(sc), n_top, tuple(dp_split["scene_ids"]),
+                      tuple(dp_model["obj_ids"])), sc, lambda: score.ArrayScorer(
       dp_split["scene_ids"], dp_model["obj_ids"], sc, im, ob, val, n_top))
   out = []
   for k, sg in enumerate(signs):

@@ -155,6 +155,7 @@ def main():
   ap.add_argument("--ab-depth", action="store_true",
                   help="evaluate twice: test depth decoded on the GPU, then on the host "
                        "(BOPX_DEPTH_GPU=0); both timings and identical scores reported")
+  ap.add_argument("--warm-reps", type=int, default=2, help="with --ab-group: warm runs per value")
   a = ap.parse_args()
   import torch
   if os.path.exists(a.root):
@@ -295,7 +296,8 @@ def main():
     runs = (("host_decode_warm", "0", None), ("gpu_decode_warm", "1", None))
     if a.ab_group:  # decode launches per scene (0) vs shared launches of ~G frames
       gs = a.ab_group.split(",")
-      runs = tuple(("gpu_decode_group%s_warm%d" % (g, r), "1", g) for r in (1, 2) for g in gs)
+      runs = tuple(("gpu_decode_group%s_warm%d" % (g, r), "1", g)
+                   for r in range(1, a.warm_reps + 1) for g in gs)
     for name, env, grp in runs:
       if grp is None:
         os.environ.pop("BOPX_DEPTH_GROUP_FRAMES", None)
