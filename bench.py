@@ -517,7 +517,7 @@ def e2e_run(images, seed, timeout=420):
   finally:
     shutil.rmtree(root, ignore_errors=True)
   keep = ("images", "tuples", "eval_bop19_s", "eval_tuples_per_s", "calc_gt_info_s", "errors_s",
-          "scores_s", "host_s", "gen_s", "depth_decoder", "depth_decoder_first_run", "ar")
+          "tail", "host_s", "gen_s", "depth_decoder", "depth_decoder_first_run", "ar")
   res = {k: out[k] for k in keep if k in out}
   res["note"] = ("cold: one drop-in eval_bop19_pose (errors VSD/MSSD/MSPD + 120 score settings) "
                  "in a fresh process on PNG files on local disk; tuples/s = its tuples / its wall "
