@@ -335,6 +335,45 @@ struct Groups {
   std::vector<int64_t> im_grp;     // per image: its groups [im_grp[i], im_grp[i + 1])
 };
 
+// Text of n items formatted once (fmt(i, buf) appends item i), in chunks of
+// kTextChunk items on `threads` threads; item i is bufs[i / kTextChunk] at
+// [off[i], off[i] + len[i]).
+constexpr int64_t kTextChunk = 4096;
+struct TextTable {
+  std::vector<std::string> bufs;
+  std::vector<uint32_t> off, len;
+  void append_to(std::string& out, int64_t i) const {
+    out.append(bufs[(size_t)(i / kTextChunk)], off[(size_t)i], len[(size_t)i]);
+  }
+};
+
+template <class F>
+TextTable build_text(int64_t n, int threads, F fmt) {
+  TextTable t;
+  const int64_t nc = (n + kTextChunk - 1) / kTextChunk;
+  t.bufs.resize((size_t)nc);
+  t.off.resize((size_t)n);
+  t.len.resize((size_t)n);
+  std::atomic<int64_t> nx{0};
+  auto work = [&]() {
+    for (int64_t c; (c = nx.fetch_add(1)) < nc;) {
+      std::string& b = t.bufs[(size_t)c];
+      for (int64_t i = c * kTextChunk; i < std::min(n, (c + 1) * kTextChunk); ++i) {
+        const size_t o = b.size();
+        fmt(i, b);
+        t.off[(size_t)i] = (uint32_t)o;
+        t.len[(size_t)i] = (uint32_t)(b.size() - o);
+      }
+    }
+  };
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(threads, nc));
+  std::vector<std::thread> pool;
+  for (int k = 1; k < nt; ++k) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  return t;
+}
+
 }  // namespace
 
 extern "C" int bopx_py_float_repr(double v, char* out) { return py_repr(v, out); }
@@ -405,14 +444,54 @@ extern "C" int bopx_score_folder(const bopx_score_args* a, char* msg_out, int ms
     return ret(BOPX_SCORE_INVALID);
   }
   // 1. parse every errors file, normalise (eval_calc_scores.py:221-233)
+  // the files on a->threads threads, each into its own part (part-relative
+  // entry / value indices), then concatenated in file order; the first file in
+  // order that fails sets the status and message, as a sequential parse would
   Folder f;
-  for (int i = 0; i < a->n_files; ++i) {
-    f.file_r0.push_back((int64_t)f.recs.size());
-    const int st = parse_file(a->err_paths[i], f, msg);
-    if (st != BOPX_SCORE_OK) {
-      if (st == BOPX_SCORE_UNSUPPORTED && msg.empty())
-        msg = std::string(a->err_paths[i]) + ": handled by the Python path";
-      return ret(st);
+  {
+    const int nf = a->n_files;
+    std::vector<Folder> parts((size_t)nf);
+    std::vector<int> st((size_t)nf, BOPX_SCORE_OK);
+    std::vector<std::string> msgs((size_t)nf);
+    std::atomic<int> nx{0};
+    auto parse = [&]() {
+      for (int i; (i = nx.fetch_add(1)) < nf;)
+        st[(size_t)i] = parse_file(a->err_paths[i], parts[(size_t)i], msgs[(size_t)i]);
+    };
+    const int npt = std::max(1, std::min(a->threads, nf));
+    std::vector<std::thread> pp;
+    for (int t = 1; t < npt; ++t) pp.emplace_back(parse);
+    parse();
+    for (auto& t : pp) t.join();
+    size_t nr = 0, ne = 0, nv = 0;
+    for (int i = 0; i < nf; ++i) {
+      if (st[(size_t)i] != BOPX_SCORE_OK) {
+        msg = msgs[(size_t)i];
+        if (st[(size_t)i] == BOPX_SCORE_UNSUPPORTED && msg.empty())
+          msg = std::string(a->err_paths[i]) + ": handled by the Python path";
+        return ret(st[(size_t)i]);
+      }
+      nr += parts[(size_t)i].recs.size();
+      ne += parts[(size_t)i].ents.size();
+      nv += parts[(size_t)i].vals.size();
+    }
+    f.recs.reserve(nr);
+    f.ents.reserve(ne);
+    f.vals.reserve(nv);
+    for (int i = 0; i < nf; ++i) {
+      Folder& q = parts[(size_t)i];
+      f.file_r0.push_back((int64_t)f.recs.size());
+      const int64_t eo = (int64_t)f.ents.size(), vo = (int64_t)f.vals.size();
+      for (Rec r : q.recs) {
+        r.e0 += eo;
+        f.recs.push_back(r);
+      }
+      for (ErrEntry e : q.ents) {
+        e.v0 += vo;
+        f.ents.push_back(e);
+      }
+      f.vals.insert(f.vals.end(), q.vals.begin(), q.vals.end());
+      Folder().recs.swap(q.recs);
     }
   }
   f.file_r0.push_back((int64_t)f.recs.size());
@@ -496,7 +575,34 @@ extern "C" int bopx_score_folder(const bopx_score_args* a, char* msg_out, int ms
       }
   }
 
-  // 3. every setting: greedy matching (pose_matching.py:9-90) + matches file
+  // 3. the matches files' text that every setting shares, formatted once: each
+  // GT's id fields, each errors entry's values, each record's score
+  const bool write = a->matches_paths != nullptr;
+  const int nth = std::max(1, a->threads);
+  TextTable gt_txt, ent_txt, score_txt;
+  if (write) {
+    gt_txt = build_text(a->n_gt, nth, [&](int64_t g, std::string& b) {
+      b += ", \"gt_id\": ";
+      put_int(b, a->gt_id[g]);
+      b += ", \"im_id\": ";
+      put_int(b, a->gt_im[g]);
+      b += ", \"obj_id\": ";
+      put_int(b, a->gt_obj[g]);
+      b += ", \"scene_id\": ";
+      put_int(b, a->gt_scene[g]);
+      b += ", \"score\": ";
+    });
+    ent_txt = build_text((int64_t)f.ents.size(), nth, [&](int64_t e, std::string& b) {
+      const ErrEntry& en = f.ents[(size_t)e];
+      for (int k = 0; k < en.nv; ++k) {
+        if (k) b += ", ";
+        put_num(b, f.vals[(size_t)(en.v0 + k)]);
+      }
+    });
+    score_txt = build_text((int64_t)f.recs.size(), nth,
+                           [&](int64_t r, std::string& b) { put_num(b, f.recs[(size_t)r].score); });
+  }
+  // 4. every setting: greedy matching (pose_matching.py:9-90) + matches file
   std::atomic<int> next{0}, status{BOPX_SCORE_OK};
   std::vector<std::string> errs(a->n_settings);
   auto work = [&]() {
@@ -555,10 +661,7 @@ extern "C" int bopx_score_folder(const bopx_score_args* a, char* msg_out, int ms
         } else {
           const ErrEntry& en = f.ents[mt.ent];
           out += '[';
-          for (int k = 0; k < en.nv; ++k) {
-            if (k) out += ", ";
-            put_num(out, f.vals[en.v0 + k]);
-          }
+          ent_txt.append_to(out, mt.ent);
           out += "], \"error_norm\": [";
           for (int k = 0; k < en.nv; ++k) {
             if (k) out += ", ";
@@ -567,19 +670,11 @@ extern "C" int bopx_score_folder(const bopx_score_args* a, char* msg_out, int ms
           out += "], \"est_id\": ";
           put_int(out, f.recs[mt.rec].est);
         }
-        out += ", \"gt_id\": ";
-        put_int(out, a->gt_id[g]);
-        out += ", \"im_id\": ";
-        put_int(out, a->gt_im[g]);
-        out += ", \"obj_id\": ";
-        put_int(out, a->gt_obj[g]);
-        out += ", \"scene_id\": ";
-        put_int(out, a->gt_scene[g]);
-        out += ", \"score\": ";
+        gt_txt.append_to(out, g);  // , "gt_id": .. "scene_id": .., "score":
         if (mt.rec < 0)
           out += "-1";
         else
-          put_num(out, f.recs[mt.rec].score);
+          score_txt.append_to(out, mt.rec);
         out += a->gt_valid[g] ? ", \"valid\": true}" : ", \"valid\": false}";
       }
       out += a->n_gt ? "\n]" : "]";
