@@ -57,17 +57,21 @@ def my_images(scene_gt, rank, world):
 _PINNED = [None, None]  # page-locked depth staging buffers (scene_stats)
 
 
-def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_batch=128,
+def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_batch=None,
                 rank=0, world=1, frames_all=None):
   """Per image id: list of (row, masks or None) per GT instance, in GT order;
-  images are evaluated in batches of im_batch frames. With world > 1 only this
-  rank's images (my_images) are evaluated. frames_all: the test depth of those
-  images already on the device (SceneDepthPrefetch), else it is decoded here
-  on the host, a batch ahead."""
+  images are evaluated in batches of im_batch frames (default: 128 when the
+  frames are decoded here or mask planes come back; the whole scene in one
+  launch when its frames are resident and only the rows are read). With
+  world > 1 only this rank's images (my_images) are evaluated. frames_all: the
+  test depth of those images already on the device (SceneDepthPrefetch), else
+  it is decoded here on the host, a batch ahead."""
   from . import runtime
   scene_camera = inout.load_scene_camera(dp_split["scene_camera_tpath"].format(scene_id=scene_id))
   scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
   im_ids = my_images(scene_gt, rank, world)
+  if im_batch is None:
+    im_batch = max(1, len(im_ids)) if frames_all is not None and not masks else 128
   res = {}
   dev = ev.device
   W, H = dp_split["im_size"]
@@ -108,22 +112,26 @@ def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_ba
         frames = nxt.result()
         if bi + 1 < len(batches):
           nxt = ahead.submit(load, batches[bi + 1], (bi + 1) & 1)
-      cam, obj, pose, fidx, owner = [], [], [], [], []
+      cam, obj, Rs, ts, fidx, owner = [], [], [], [], [], []
       for k, im_id in enumerate(ims):
         K = scene_camera[im_id]["cam_K"]
         cam.append((K[0, 0], K[1, 1], K[0, 2], K[1, 2]))
         for gt in scene_gt[im_id]:
           obj.append(gt["obj_id"])
-          pose.append(np.concatenate([gt["cam_R_m2c"].reshape(9), gt["cam_t_m2c"].reshape(3)]))
+          Rs.append(gt["cam_R_m2c"])
+          ts.append(gt["cam_t_m2c"])
           fidx.append(k)
           owner.append(im_id)
         res[im_id] = []
       if not obj:
         continue
+      # [R row-major | t] per GT, float64
+      pose = np.concatenate([np.asarray(Rs, np.float64).reshape(-1, 9),
+                             np.asarray(ts, np.float64).reshape(-1, 3)], 1)
       T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
       d_frames = (frames.to(dev, non_blocking=True) if torch.is_tensor(frames)
                   else T(frames, torch.float32))
-      rows, mk = ev.gt_info(ev.slots(obj), T(np.stack(pose), torch.float64),
+      rows, mk = ev.gt_info(ev.slots(obj), T(pose, torch.float64),
                             T(np.array(fidx, np.int32), torch.int32), d_frames,
                             T(np.array(cam), torch.float64), delta, canvas_scale, masks,
                             runtime.delta_flags(delta))

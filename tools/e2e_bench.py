@@ -156,6 +156,7 @@ def main():
                   help="evaluate twice: test depth decoded on the GPU, then on the host "
                        "(BOPX_DEPTH_GPU=0); both timings and identical scores reported")
   ap.add_argument("--warm-reps", type=int, default=2, help="with --ab-group: warm runs per value")
+  ap.add_argument("--profile-gt", action="store_true", help="cProfile calc_gt_info")
   a = ap.parse_args()
   import torch
   if os.path.exists(a.root):
@@ -180,12 +181,27 @@ def main():
         phases[name] = phases.get(name, 0.0) + time.perf_counter() - t
     return wrap
 
+  gprof = None
+  if a.profile_gt:
+    import cProfile
+    gprof = cProfile.Profile()
+    gprof.enable()
   t0 = time.perf_counter()
   gt_side.calc_gt_info({"dataset": "ycbv", "dataset_split": "test", "dataset_split_type": None,
                         "delta": 15, "renderer_type": "hip", "datasets_path": datasets,
                         "scene_ids": scenes})
   torch.cuda.synchronize()
   phases["calc_gt_info"] = time.perf_counter() - t0
+  if gprof is not None:
+    import io
+    import pstats
+    gprof.disable()
+    s_ = io.StringIO()
+    pstats.Stats(gprof, stream=s_).sort_stats("cumulative").print_stats(35)
+    pstats.Stats(gprof, stream=s_).sort_stats("tottime").print_stats(25)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "gt_profile.txt"), "w") as f:
+      f.write(s_.getvalue())
 
   run0, score0 = ece.run, ecs.score_error_dir
   err_t = {}
