@@ -39,6 +39,32 @@ def info_from_row(row):
           "bbox_obj": bbox_obj, "bbox_visib": bbox_visib}
 
 
+def infos_from_rows(rows):
+  """info_from_row of every row of an (n, 11) array, in one conversion."""
+  rows = np.asarray(rows, np.float64).reshape(-1, 11)
+  ints = rows.astype(np.int64)
+  n_all, n_visib, n_valid = ints[:, 0].tolist(), ints[:, 1].tolist(), ints[:, 10].tolist()
+  fr = np.where(rows[:, 0] > 0, ints[:, 1] / np.where(ints[:, 0] > 0, ints[:, 0], 1), 0.0).tolist()
+  bb = ints[:, 2:10].tolist()
+  out = []
+  none = [-1, -1, -1, -1]
+  for a, v, d, f, b in zip(n_all, n_visib, n_valid, fr, bb):
+    if v > 0:
+      bo, bv = [b[0], b[1], b[2] - b[0], b[3] - b[1]], [b[4], b[5], b[6] - b[4], b[7] - b[5]]
+    else:
+      bo, bv = list(none), list(none)
+    out.append({"px_count_all": a, "px_count_valid": d, "px_count_visib": v,
+                "visib_fract": f if a > 0 else 0.0, "bbox_obj": bo, "bbox_visib": bv})
+  return out
+
+
+def _cached(loader, path):
+  """loader(path) through the evaluation's parse cache (the same objects for
+  every pass of this process; read-only)."""
+  from .eval_calc_errors import cached_load
+  return cached_load(loader, path)
+
+
 def _depth_path(dp_split, scene_id, im_id):
   path = dp_split["depth_tpath"].format(scene_id=scene_id, im_id=im_id)
   return path if os.path.exists(path) else path.replace(".tif", ".png")
@@ -67,8 +93,9 @@ def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_ba
   test depth of those images already on the device (SceneDepthPrefetch), else
   it is decoded here on the host, a batch ahead."""
   from . import runtime
-  scene_camera = inout.load_scene_camera(dp_split["scene_camera_tpath"].format(scene_id=scene_id))
-  scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+  scene_camera = _cached(inout.load_scene_camera,
+                         dp_split["scene_camera_tpath"].format(scene_id=scene_id))
+  scene_gt = _cached(inout.load_scene_gt, dp_split["scene_gt_tpath"].format(scene_id=scene_id))
   im_ids = my_images(scene_gt, rank, world)
   if im_batch is None:
     im_batch = max(1, len(im_ids)) if frames_all is not None and not masks else 128
@@ -207,8 +234,8 @@ class SceneDepthPrefetch:
     path_gt = dp["scene_gt_tpath"].format(scene_id=scene_id)
     if not os.path.exists(path_gt):
       return None
-    scene_camera = inout.load_scene_camera(dp["scene_camera_tpath"].format(scene_id=scene_id))
-    im_ids = my_images(inout.load_scene_gt(path_gt), self.rank, self.world)
+    scene_camera = _cached(inout.load_scene_camera, dp["scene_camera_tpath"].format(scene_id=scene_id))
+    im_ids = my_images(_cached(inout.load_scene_gt, path_gt), self.rank, self.world)
     W, H = dp["im_size"]
     if self.dec is None:
       self.dec = depth_gpu.DepthDecoder(self.ev.device.index or 0)
@@ -254,11 +281,15 @@ def calc_gt_info(p):
         ahead.submit(scene_ids[k + 1])
       stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 3, False, rank=rank,
                           world=world, frames_all=frames)
-      scene_gt = inout.load_scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+      scene_gt = _cached(inout.load_scene_gt, dp_split["scene_gt_tpath"].format(scene_id=scene_id))
       rows = _gather_info(torch, ev, stats, scene_gt, rank, world)
       if rows is None:
         continue
-      info = {im_id: [info_from_row(r) for r in lst] for im_id, lst in rows.items()}
+      flat = infos_from_rows([r for lst in rows.values() for r in lst])
+      info, k = {}, 0
+      for im_id, lst in rows.items():
+        info[im_id] = flat[k:k + len(lst)]
+        k += len(lst)
       path = dp_split["scene_gt_info_tpath"].format(scene_id=scene_id)
       os.makedirs(os.path.dirname(path), exist_ok=True)
       inout.save_json(path, info)

@@ -278,7 +278,13 @@ def load_json(path, keys_to_int=False):
   """JSON file; with keys_to_int, object keys that are (signed) integers
   become ints (inout.py:66-82)."""
   def hook(d):
-    return {int(k) if k.lstrip("-").isdigit() else k: v for k, v in d.items()}
+    # a key that starts with an ASCII letter or "_" never converts: such dicts
+    # (the per-instance records) are returned as they are
+    for k in d:
+      c = k[:1]
+      if not ("a" <= c <= "z" or "A" <= c <= "Z" or c == "_"):
+        return {int(k) if k.lstrip("-").isdigit() else k: v for k, v in d.items()}
+    return d
   with open(path, "r") as f:
     return json.load(f, object_hook=hook) if keys_to_int else json.load(f)
 

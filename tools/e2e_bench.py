@@ -203,6 +203,10 @@ def main():
     with open(os.path.join(REPO, "gpurun_out", "gt_profile.txt"), "w") as f:
       f.write(s_.getvalue())
 
+  # the evaluation starts cold: nothing calc_gt_info parsed stays in the caches
+  ece._FILE_CACHE.clear()
+  ece._ORG_CACHE.clear()
+  ecs._DS_CACHE.clear()
   run0, score0 = ece.run, ecs.score_error_dir
   err_t = {}
 
