@@ -39,23 +39,38 @@ def info_from_row(row):
           "bbox_obj": bbox_obj, "bbox_visib": bbox_visib}
 
 
-def infos_from_rows(rows):
-  """info_from_row of every row of an (n, 11) array, in one conversion."""
-  rows = np.asarray(rows, np.float64).reshape(-1, 11)
-  ints = rows.astype(np.int64)
-  n_all, n_visib, n_valid = ints[:, 0].tolist(), ints[:, 1].tolist(), ints[:, 10].tolist()
-  fr = np.where(rows[:, 0] > 0, ints[:, 1] / np.where(ints[:, 0] > 0, ints[:, 0], 1), 0.0).tolist()
-  bb = ints[:, 2:10].tolist()
-  out = []
-  none = [-1, -1, -1, -1]
-  for a, v, d, f, b in zip(n_all, n_visib, n_valid, fr, bb):
-    if v > 0:
-      bo, bv = [b[0], b[1], b[2] - b[0], b[3] - b[1]], [b[4], b[5], b[6] - b[4], b[7] - b[5]]
-    else:
-      bo, bv = list(none), list(none)
-    out.append({"px_count_all": a, "px_count_valid": d, "px_count_visib": v,
-                "visib_fract": f if a > 0 else 0.0, "bbox_obj": bo, "bbox_visib": bv})
-  return out
+_INFO_FMT = ('{"bbox_obj": [%d, %d, %d, %d], "bbox_visib": [%d, %d, %d, %d], "px_count_all": %d, '
+             '"px_count_valid": %d, "px_count_visib": %d, "visib_fract": %r}')
+
+
+def save_scene_gt_info(path, rows):
+  """inout.save_json(path, {im_id: [info_from_row(r) for r in lst]}) for
+  rows = {im_id: [row, ...]}, byte for byte, formatted straight from the rows
+  (sorted keys, one image per line; visib_fract by float repr like the JSON
+  encoder)."""
+  ims = sorted(rows)
+  flat = [r for im in ims for r in rows[im]]
+  lines = []
+  if flat:
+    a = np.asarray(flat, np.float64).reshape(-1, 11)
+    ints = a.astype(np.int64)
+    n_all, n_vis = ints[:, 0], ints[:, 1]
+    fr = np.where(n_all > 0, n_vis / np.where(n_all > 0, n_all, 1), 0.0)
+    bb = ints[:, 2:10].copy()
+    bb[:, 2] -= bb[:, 0]
+    bb[:, 3] -= bb[:, 1]
+    bb[:, 6] -= bb[:, 4]
+    bb[:, 7] -= bb[:, 5]
+    bb[n_vis <= 0] = -1  # both boxes only when something is visible
+    vals = np.concatenate([bb, n_all[:, None], ints[:, 10:11], n_vis[:, None]], 1).tolist()
+    recs = [_INFO_FMT % (tuple(v) + (f,)) for v, f in zip(vals, fr.tolist())]
+  k = 0
+  for im in ims:
+    n = len(rows[im])
+    lines.append('  "%d": [%s]' % (im, ", ".join(recs[k:k + n])))
+    k += n
+  with open(path, "w") as f:
+    f.write("{\n" + ",\n".join(lines) + ("\n}" if lines else "}"))
 
 
 def _cached(loader, path):
@@ -212,53 +227,54 @@ def _gather_info(torch, ev, stats, scene_gt, rank, world):
 
 
 class SceneDepthPrefetch:
-  """The next scene's test depth decoded on the GPU (depth_gpu, kern_png.hip)
-  while the current scene runs: the frames of this rank's images (my_images
-  order) land on the device from an upload stream. None for a scene (host
-  decoding in scene_stats) without a GPU, with BOPX_DEPTH_GPU=0, or when a
-  frame has another size."""
+  """The scenes' test depth decoded on the GPU (depth_gpu, kern_png.hip) ahead
+  of use, consecutive scenes in shared launches (depth_gpu.GroupPrefetch, the
+  VSD error pass's grouping: BOPX_DEPTH_GROUP_FRAMES): take(scene) returns the
+  frames of this rank's images (my_images order) on the device, final for the
+  current stream. None for a scene (host decoding in scene_stats) without a
+  GPU, with BOPX_DEPTH_GPU=0, without a GT file, or when a frame of its group
+  has another size."""
 
-  def __init__(self, ev, torch, dp_split, rank, world):
-    from concurrent.futures import ThreadPoolExecutor
+  def __init__(self, ev, torch, dp_split, rank, world, scene_ids=()):
     from . import depth_gpu
+    from .eval_calc_errors import depth_group_sizes
     self.on = torch.cuda.is_available() and depth_gpu.enabled()
-    self.ev, self.torch, self.dp_split, self.rank, self.world = ev, torch, dp_split, rank, world
-    self.pool = ThreadPoolExecutor(1)
-    self.dec = None
-    self.up = None
-    self.pending = {}
+    self.groups = None
+    g, first = depth_group_sizes()
+    if not self.on or g <= 0 or not scene_ids:
+      return
+    dp = dp_split
 
-  def _load(self, scene_id):
-    from . import depth_gpu
-    torch, dp = self.torch, self.dp_split
-    path_gt = dp["scene_gt_tpath"].format(scene_id=scene_id)
-    if not os.path.exists(path_gt):
-      return None
-    scene_camera = _cached(inout.load_scene_camera, dp["scene_camera_tpath"].format(scene_id=scene_id))
-    im_ids = my_images(_cached(inout.load_scene_gt, path_gt), self.rank, self.world)
+    def paths(scene_id):
+      path_gt = dp["scene_gt_tpath"].format(scene_id=scene_id)
+      if not os.path.exists(path_gt):
+        return [], []
+      scene_camera = _cached(inout.load_scene_camera,
+                             dp["scene_camera_tpath"].format(scene_id=scene_id))
+      im_ids = my_images(_cached(inout.load_scene_gt, path_gt), rank, world)
+      return ([_depth_path(dp, scene_id, i) for i in im_ids],
+              [scene_camera[i]["depth_scale"] for i in im_ids])
     W, H = dp["im_size"]
-    if self.dec is None:
-      self.dec = depth_gpu.DepthDecoder(self.ev.device.index or 0)
-      self.up = torch.cuda.Stream(self.ev.device)
-    try:
-      with torch.cuda.stream(self.up):
-        d = self.dec.load([_depth_path(dp, scene_id, i) for i in im_ids],
-                          [scene_camera[i]["depth_scale"] for i in im_ids], H, W, torch)
-    except ValueError:
-      return None
-    d.record_stream(torch.cuda.current_stream(self.ev.device))
-    return d
+    dev = ev.device
+    self.groups = depth_gpu.GroupPrefetch(
+        dev.index or 0, [(sid, (lambda sid=sid: paths(sid))) for sid in scene_ids], H, W, torch,
+        torch.cuda.Stream(dev), torch.cuda.current_stream(dev), max_frames=g, first_frames=first,
+        max_groups=3)
 
   def submit(self, scene_id):
-    if self.on:
-      self.pending[scene_id] = self.pool.submit(self._load, scene_id)
+    pass  # every scene was queued at construction
 
   def take(self, scene_id):
-    f = self.pending.pop(scene_id, None)
-    return f.result() if f is not None else None
+    if self.groups is None:
+      return None
+    try:
+      return self.groups.get(scene_id)
+    except ValueError:
+      return None  # a frame of another size in its group: host decoding
 
   def close(self):
-    self.pool.shutdown()
+    if self.groups is not None:
+      self.groups.close()
 
 
 def calc_gt_info(p):
@@ -269,7 +285,7 @@ def calc_gt_info(p):
   rank, world, _ = shard.init_from_env()
   torch, ev, dp_split, scene_ids = _setup(p)
   written = []
-  ahead = SceneDepthPrefetch(ev, torch, dp_split, rank, world)
+  ahead = SceneDepthPrefetch(ev, torch, dp_split, rank, world, scene_ids)
   try:
     if scene_ids:
       ahead.submit(scene_ids[0])
@@ -285,14 +301,9 @@ def calc_gt_info(p):
       rows = _gather_info(torch, ev, stats, scene_gt, rank, world)
       if rows is None:
         continue
-      flat = infos_from_rows([r for lst in rows.values() for r in lst])
-      info, k = {}, 0
-      for im_id, lst in rows.items():
-        info[im_id] = flat[k:k + len(lst)]
-        k += len(lst)
       path = dp_split["scene_gt_info_tpath"].format(scene_id=scene_id)
       os.makedirs(os.path.dirname(path), exist_ok=True)
-      inout.save_json(path, info)
+      save_scene_gt_info(path, rows)
       written.append(path)
   finally:
     ahead.close()
@@ -307,7 +318,7 @@ def calc_gt_masks(p):
   rank, world, _ = shard.init_from_env()
   torch, ev, dp_split, scene_ids = _setup(p)
   written = []
-  ahead = SceneDepthPrefetch(ev, torch, dp_split, rank, world)
+  ahead = SceneDepthPrefetch(ev, torch, dp_split, rank, world, scene_ids)
   try:
     if scene_ids:
       ahead.submit(scene_ids[0])

@@ -62,3 +62,31 @@ def test_calc_gt_masks_matches_reference(tmp_path):
     m = np.asarray(Image.open(path))
     assert set(np.unique(m)) <= {0, 255}
     assert np.array_equal(np.packbits(m > 0), exp[key]), key
+
+
+def test_save_scene_gt_info_bytes(tmp_path):
+  """The direct writer gives save_json's bytes for the info_from_row dicts:
+  visible and invisible instances, empty images, zero silhouettes, fractions
+  that need 17 digits, negative box corners."""
+  from bop_toolkit_amd import gt_side, inout
+  rng = np.random.default_rng(11)
+  rows = {}
+  for im in (0, 3, 12, 7, 100, 2):
+    n = int(rng.integers(0, 5))
+    r = np.zeros((n, 11))
+    r[:, 0] = rng.integers(0, 300000, n)
+    r[:, 1] = np.minimum(r[:, 0], rng.integers(0, 300000, n))
+    r[:, 10] = rng.integers(0, 300000, n)
+    r[:, 2:10] = rng.integers(-700, 2000, (n, 8))
+    if n:
+      r[0, 1] = 0
+    if n > 1:
+      r[1, 0] = r[1, 1] = 0
+    rows[im] = list(r)
+  a, b = tmp_path / "a.json", tmp_path / "b.json"
+  inout.save_json(str(a), {im: [gt_side.info_from_row(x) for x in lst] for im, lst in rows.items()})
+  gt_side.save_scene_gt_info(str(b), rows)
+  assert a.read_bytes() == b.read_bytes()
+  inout.save_json(str(a), {})
+  gt_side.save_scene_gt_info(str(b), {})
+  assert a.read_bytes() == b.read_bytes()
