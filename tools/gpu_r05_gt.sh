@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${TAG:-r05g}
-timeout -k 10 300 python -u -m pytest tests/test_gt_side.py tests/test_e2e_errors.py tests/test_scores.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gpu_tests_${TAG}.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/gpu_tests_${TAG}.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gt_side.py tests/test_e2e_errors.py tests/test_scores.py tests/test_gpu_fuzz.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gpu_tests_${TAG}.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/gpu_tests_${TAG}.log; exit 1; }
 tail -1 gpurun_out/gpu_tests_${TAG}.log
 timeout -k 10 480 python tools/e2e_bench.py --images 16667 --profile-gt --ab-depth --ab-group 4096/1024 --warm-reps ${WARM_REPS:-2} > gpurun_out/e2e_100k_${TAG}.json 2> gpurun_out/e2e_100k_${TAG}.err || { tail -20 gpurun_out/e2e_100k_${TAG}.err; exit 1; }
 python -c "
