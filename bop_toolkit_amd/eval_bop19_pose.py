@@ -145,6 +145,15 @@ def evaluate(p, device=0, calc_errors=True):
     # are scored in a process pool while the next error type runs on the GPU
     n_folders = sum(len(e["vsd_taus"]) if e["type"] == "vsd" else 1 for e in p["errors"])
     scorer = ecs.FolderScorer(n_folders) if ece._dist()[0] == 0 else None
+    sym_err = [e for e in p["errors"] if e["type"] in ("mssd", "mspd")]
+    if calc_errors and sym_err:
+      # MSSD / MSPD symmetry sets computed on a thread during the VSD pass, for
+      # the parameters that pass will parse
+      from . import dataset_params
+      pe = ece.parse_args(errors_argv(p, sym_err[0], result_filename))
+      dp_model = dataset_params.get_model_params(pe["datasets_path"], dataset, "eval")
+      if os.path.exists(dp_model["models_info_path"]):
+        ece.prefetch_symmetries(dp_model["models_info_path"], pe["max_sym_disc_step"])
     try:
       folder_scores = _errors_and_scores(p, result_filename, result_name, dataset, device,
                                          calc_errors, scorer, owner)

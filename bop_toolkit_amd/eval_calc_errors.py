@@ -246,6 +246,43 @@ def gate(error_type, diameter, t_e, t_g):
 
 
 # ------------------------------------------------------------------ evaluation
+_SYM_CACHE = {}  # (step, discrete, continuous) -> S x 12 symmetry rows
+
+
+def symmetry_rows(info, step):
+  """misc.get_symmetry_transformations(info, step) as S x 12 rows
+  (misc.symmetries_to_array), cached for the process on the model info's
+  symmetry fields and the step."""
+  key = (float(step), repr(info.get("symmetries_discrete")),
+         repr(info.get("symmetries_continuous")))
+  hit = _SYM_CACHE.get(key)
+  if hit is None:
+    with _key_lock(("sym",) + key):
+      hit = _SYM_CACHE.get(key)
+      if hit is None:
+        if len(_SYM_CACHE) >= 4096:
+          _SYM_CACHE.clear()
+        hit = _SYM_CACHE[key] = misc.symmetries_to_array(
+            misc.get_symmetry_transformations(info, step))
+  return hit
+
+
+def prefetch_symmetries(models_info_path, step):
+  """Start computing every object's symmetry rows on a thread (the BOP19 run
+  needs them for MSSD / MSPD after its VSD pass); returns the thread."""
+  def work():
+    try:
+      info = cached_load(inout.load_json, models_info_path, keys_to_int=True)
+      for v in info.values():
+        if isinstance(v, dict):
+          symmetry_rows(v, step)
+    except Exception:  # noqa: BLE001 - the passes compute what is missing themselves
+      pass
+  t = threading.Thread(target=work, name="bopx-symmetries", daemon=True)
+  t.start()
+  return t
+
+
 class Models:
   """Objects of one dataset resident on the GPU (+ host-side info).
 
@@ -279,7 +316,7 @@ class Models:
       keep.add(obj_id)
       if have is not None and have[0] == mkey and obj_id in ev.objects:
         if need_syms and have[1] != skey:
-          syms = misc.get_symmetry_transformations(models_info[obj_id], p["max_sym_disc_step"])
+          syms = symmetry_rows(models_info[obj_id], p["max_sym_disc_step"])
           ev.set_symmetries(obj_id, syms)
           reg[obj_id] = (mkey, skey)
         continue
@@ -288,7 +325,7 @@ class Models:
       m = cached_load(inout.load_ply, path)
       syms = None
       if need_syms:
-        syms = misc.get_symmetry_transformations(models_info[obj_id], p["max_sym_disc_step"])
+        syms = symmetry_rows(models_info[obj_id], p["max_sym_disc_step"])
       ev.add_object(obj_id, m["pts"], m.get("faces"), syms, dia)
       reg[obj_id] = (mkey, skey)
     for obj_id in [o for o in ev.objects if o not in keep]:
