@@ -384,14 +384,13 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
       if (nb <= 32 && !refill_word()) return kErr;  // nb in (32, 64]
       const int lim = min(nb, 63);  // chain offsets stay lane indices
       const uint32_t ev = S.lit[(uint32_t)(bb >> lane) & ((1 << kLitRoot) - 1)];
-      int e, off = 0;
+      int off = 0;
       uint64_t run = 0;  // bit l: a chain step (one or two literals) starts at offset l
-      for (;;) {
-        e = __builtin_amdgcn_readlane((int)ev, off);
-        const int nxt = off + ((e >> 24) & (int)kStop);
-        if (nxt > lim) break;
+      int e = __builtin_amdgcn_readlane((int)ev, 0);
+      for (int nxt = (e >> 24) & (int)kStop; nxt <= lim; nxt = off + ((e >> 24) & (int)kStop)) {
         run |= 1ull << off;
         off = nxt;
+        e = __builtin_amdgcn_readlane((int)ev, off);
       }
       if (run) {
         const bool on = (run >> lane) & 1;
