@@ -394,7 +394,8 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
       }
       if (run) {
         const bool on = (run >> lane) & 1;
-        const uint64_t run2 = __ballot(on && (int)ev < 0);  // chain steps with two literals
+        // chain steps with two literals (entries with bit 31 set, on the chain)
+        const uint64_t run2 = run & __builtin_amdgcn_ballot_w64((int)ev < 0);
         const int nlit = __popcll(run) + __popcll(run2);
         if (nlit > out_n - p) return kErr;
         bb >>= off;  // off <= 63
