@@ -128,8 +128,11 @@ class DepthDecoder:
 
   def _staging(self, torch, nbytes, slot=0):
     if self._pinned[slot] is None or self._pinned[slot].numel() < nbytes:
+      # grown with headroom (16 MiB steps, +50 %): chunks differ in size, and
+      # each page-locked allocation costs milliseconds
+      size = (max(nbytes + nbytes // 2, 1 << 24) + (1 << 24) - 1) >> 24 << 24
       self._pinned[slot] = None
-      self._pinned[slot] = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, pin_memory=True)
+      self._pinned[slot] = torch.empty(size, dtype=torch.uint8, pin_memory=True)
     return self._pinned[slot]
 
   def submit(self, paths, scales, H, W, torch, workers=None):

@@ -297,6 +297,8 @@ def main():
   t_eval = time.perf_counter() - t0
   first_tail = tail_info(t0 + t_eval)
   first_timeline = timeline(t0)
+  first_events = [(nm, round(e0 - t0, 4), round(e1 - t0, 4))
+                  for nm, e0, e1 in sorted(tl, key=lambda x: x[1])]
   if prof is not None:
     import io
     import pstats
@@ -365,6 +367,7 @@ def main():
       "eval_tuples_per_s": n / t_eval,
       "depth_decoder": "gpu" if depth_gpu.enabled() else "host", "ab_depth": ab,
       "depth_decoder_first_run": first_stats, "tail": first_tail, "timeline": first_timeline,
+      "events": first_events,
       "ar": {k: round(float(v), 4) for k, v in scores.items()}}))
 
 
