@@ -25,6 +25,7 @@ _f = ctypes.POINTER(ctypes.c_float)
 _u8 = ctypes.POINTER(ctypes.c_uint8)
 _u32 = ctypes.POINTER(ctypes.c_uint32)
 _i32 = ctypes.POINTER(ctypes.c_int32)
+_i64 = ctypes.POINTER(ctypes.c_int64)
 _I = ctypes.c_int
 _I64 = ctypes.c_int64
 _D = ctypes.c_double
@@ -43,6 +44,7 @@ SIGNATURES = {
     "bopx_add_object": (_I, [_CTX, _I, _d, _I64, _u32, _I64]),
     "bopx_remove_object": (_I, [_CTX, _I]),
     "bopx_set_symmetries": (_I, [_CTX, _I, _d, _I64]),
+    "bopx_set_symmetries_many": (_I, [_CTX, _I, _i32, _i64, _d]),
     "bopx_object_slot": (_I, [_CTX, _I, ctypes.POINTER(_I)]),
     "bopx_mssd_batch": (_I, [_CTX, _I64, _i32, _d, _d, _d]),
     "bopx_mspd_batch": (_I, [_CTX, _I64, _i32, _d, _d, _d, _d]),
@@ -200,6 +202,14 @@ class Context:
   def set_symmetries(self, obj_id, syms12):
     syms12 = np.ascontiguousarray(syms12, np.float64).reshape(-1, 12)
     self.call("bopx_set_symmetries", int(obj_id), ptr(syms12, _d), len(syms12))
+
+  def set_symmetries_many(self, obj_ids, syms12_list):
+    ids = np.ascontiguousarray(obj_ids, np.int32)
+    arrs = [np.asarray(x, np.float64).reshape(-1, 12) for x in syms12_list]
+    ns = np.array([len(x) for x in arrs], np.int64)
+    rows = np.ascontiguousarray(np.concatenate(arrs) if arrs else np.zeros((0, 12)))
+    self.call("bopx_set_symmetries_many", len(ids), ptr(ids, _i32), ptr(ns, _i64),
+              ptr(rows, _d))
 
 
 def code_object_digests(path=None):

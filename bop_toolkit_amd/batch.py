@@ -67,6 +67,17 @@ class BatchEvaluator:
     self.ctx.set_symmetries(obj_id, s12)
     self.objects[obj_id]["ns"] = len(s12)
 
+  def set_symmetries_many(self, items):
+    """set_symmetries for several objects in one library call: items is a
+    list of (obj_id, syms)."""
+    if not items:
+      return
+    ids = [int(o) for o, _ in items]
+    s12 = [s if isinstance(s, np.ndarray) else symmetries_to_array(s) for _, s in items]
+    self.ctx.set_symmetries_many(ids, s12)
+    for o, s in zip(ids, s12):
+      self.objects[o]["ns"] = len(s)
+
   def slots(self, obj_ids):
     """int32 device tensor of slots for a sequence of obj_ids."""
     table = {k: v["slot"] for k, v in self.objects.items()}

@@ -742,6 +742,39 @@ int bopx_set_symmetries(bopx_ctx* c, int obj_id, const double* syms, int64_t ns)
   return sync_desc(c);
 }
 
+int bopx_set_symmetries_many(bopx_ctx* c, int n, const int* obj_ids, const int64_t* ns,
+                             const double* syms) {
+  if (!c) return BOPX_E_INVALID;
+  if (n < 0 || (n > 0 && (!obj_ids || !ns || !syms))) return fail(c, BOPX_E_INVALID, "NULL buffer");
+  std::vector<int> slots((size_t)n);
+  for (int i = 0; i < n; ++i) {
+    if (slot_checked(c, obj_ids[i], &slots[(size_t)i]) != BOPX_OK)
+      return fail(c, BOPX_E_NOT_FOUND, "unknown obj_id %d", obj_ids[i]);
+    if (ns[i] < 1) return fail(c, BOPX_E_INVALID, "empty symmetry set");
+  }
+  if (n == 0) return BOPX_OK;
+  if (int r = set_dev(c)) return r;
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // no launch still reads the old sets
+  const double* src = syms;
+  for (int i = 0; i < n; ++i) {
+    Object& o = c->objs[(size_t)slots[(size_t)i]];
+    if (o.d_syms) HIPCHK(c, hipFree(o.d_syms));
+    o.d_syms = nullptr;
+    o.ns = 0;
+    const size_t count = 12 * (size_t)ns[i];
+    if (hipMalloc((void**)&o.d_syms, count * sizeof(double)) != hipSuccess) {
+      (void)hipGetLastError();
+      o.d_syms = nullptr;
+      return fail(c, BOPX_E_OOM, "object allocation failed");
+    }
+    HIPCHK(c, hipMemcpyAsync(o.d_syms, src, count * sizeof(double), hipMemcpyHostToDevice,
+                             c->stream));
+    o.ns = ns[i];
+    src += count;
+  }
+  return sync_desc(c);  // one descriptor upload, then the stream is drained
+}
+
 int bopx_object_slot(const bopx_ctx* c, int obj_id, int* slot) {
   if (!c || !slot) return BOPX_E_INVALID;
   return slot_checked(c, obj_id, slot);

@@ -300,6 +300,7 @@ class Models:
     self.sym_ids = set(dp_model["symmetric_obj_ids"] or [])
     reg = ev.__dict__.setdefault("_bopx_reg", {})  # obj_id -> (mesh key, symmetry key)
     keep = set()
+    pending = []  # (obj_id, symmetry rows, keys) of resident objects: one upload call
     for obj_id in dp_model["obj_ids"]:
       path = dp_model["model_tpath"].format(obj_id=obj_id)
       if not os.path.exists(path):
@@ -316,9 +317,8 @@ class Models:
       keep.add(obj_id)
       if have is not None and have[0] == mkey and obj_id in ev.objects:
         if need_syms and have[1] != skey:
-          syms = symmetry_rows(models_info[obj_id], p["max_sym_disc_step"])
-          ev.set_symmetries(obj_id, syms)
-          reg[obj_id] = (mkey, skey)
+          pending.append((obj_id, symmetry_rows(models_info[obj_id], p["max_sym_disc_step"]),
+                          (mkey, skey)))
         continue
       if obj_id in ev.objects:
         ev.remove_object(obj_id)
@@ -328,6 +328,15 @@ class Models:
         syms = symmetry_rows(models_info[obj_id], p["max_sym_disc_step"])
       ev.add_object(obj_id, m["pts"], m.get("faces"), syms, dia)
       reg[obj_id] = (mkey, skey)
+    if pending:
+      many = getattr(ev, "set_symmetries_many", None)
+      if many is not None:
+        many([(o, s) for o, s, _ in pending])
+      else:
+        for o, s, _ in pending:
+          ev.set_symmetries(o, s)
+      for o, _, keys in pending:
+        reg[o] = keys
     for obj_id in [o for o in ev.objects if o not in keep]:
       ev.remove_object(obj_id)
       reg.pop(obj_id, None)

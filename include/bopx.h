@@ -94,6 +94,12 @@ int bopx_remove_object(bopx_ctx* ctx, int obj_id);
 /* syms: ns x 12 (R row-major, t) from misc.get_symmetry_transformations
  * (misc.py:43-90); ns >= 1. */
 int bopx_set_symmetries(bopx_ctx* ctx, int obj_id, const double* syms, int64_t ns);
+/* bopx_set_symmetries for n objects in one call (one stream synchronisation and
+ * one descriptor upload instead of n): object obj_ids[i] gets the ns[i] rows
+ * starting at row sum(ns[0..i-1]) of syms. Nothing changes when an obj_id is
+ * unknown or an ns[i] < 1 (checked before any upload). */
+int bopx_set_symmetries_many(bopx_ctx* ctx, int n, const int* obj_ids, const int64_t* ns,
+                             const double* syms);
 int bopx_object_slot(const bopx_ctx* ctx, int obj_id, int* slot);
 
 /* ---- point-based pose errors, one output per tuple ----------------------- */

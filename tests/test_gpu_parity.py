@@ -902,3 +902,27 @@ def test_drop_in_vsd_return_types(oracle_mod, monkeypatch):
   with pytest.raises(NotImplementedError):
     create_renderer(640, 480, "vispy", mode="depth")
 
+
+
+def test_set_symmetries_many_matches_one_by_one(golden_errors):
+  """bopx_set_symmetries_many (one call for every object, as Models uploads
+  the MSSD / MSPD sets) gives the golden MSSD / MSPD, and refuses an unknown
+  object or an empty set without changing anything."""
+  from bop_toolkit_amd import _lib
+  g = golden_errors
+  ctx = _lib.Context(0)
+  for o in range(4):
+    ctx.add_object(200 + o, g["pts_%d" % o], g["faces_%d" % o])
+  ctx.set_symmetries_many([200 + o for o in range(4)], [g["syms_%d" % o] for o in range(4)])
+  ids = g["obj"] + 200
+  for name in ("mssd", "mspd"):
+    K = g["K"] if name == "mspd" else None
+    out = _batch(ctx, "bopx_%s_batch" % name, ids, g["pose_est"], g["pose_gt"], K)
+    np.testing.assert_allclose(out, g["out_" + name], rtol=0, atol=TOL)
+  with pytest.raises(KeyError):
+    ctx.set_symmetries_many([200, 999], [g["syms_0"], g["syms_1"]])
+  with pytest.raises(ValueError):
+    ctx.set_symmetries_many([200], [np.zeros((0, 12))])
+  out = _batch(ctx, "bopx_mssd_batch", ids, g["pose_est"], g["pose_gt"])
+  np.testing.assert_allclose(out, g["out_mssd"], rtol=0, atol=TOL)
+  ctx.close()
