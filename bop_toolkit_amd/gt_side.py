@@ -261,9 +261,6 @@ class SceneDepthPrefetch:
         torch.cuda.Stream(dev), torch.cuda.current_stream(dev), max_frames=g, first_frames=first,
         max_groups=3)
 
-  def submit(self, scene_id):
-    pass  # every scene was queued at construction
-
   def take(self, scene_id):
     if self.groups is None:
       return None
@@ -287,14 +284,10 @@ def calc_gt_info(p):
   written = []
   ahead = SceneDepthPrefetch(ev, torch, dp_split, rank, world, scene_ids)
   try:
-    if scene_ids:
-      ahead.submit(scene_ids[0])
-    for k, scene_id in enumerate(scene_ids):
+    for scene_id in scene_ids:
       misc.log("Calculating GT info - dataset: {} ({}, {}), scene: {}".format(
           p["dataset"], p["dataset_split"], p["dataset_split_type"], scene_id))
       frames = ahead.take(scene_id)
-      if k + 1 < len(scene_ids):
-        ahead.submit(scene_ids[k + 1])
       stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 3, False, rank=rank,
                           world=world, frames_all=frames)
       scene_gt = _cached(inout.load_scene_gt, dp_split["scene_gt_tpath"].format(scene_id=scene_id))
@@ -320,12 +313,8 @@ def calc_gt_masks(p):
   written = []
   ahead = SceneDepthPrefetch(ev, torch, dp_split, rank, world, scene_ids)
   try:
-    if scene_ids:
-      ahead.submit(scene_ids[0])
-    for k, scene_id in enumerate(scene_ids):
+    for scene_id in scene_ids:
       frames = ahead.take(scene_id)
-      if k + 1 < len(scene_ids):
-        ahead.submit(scene_ids[k + 1])
       if not os.path.exists(dp_split["scene_gt_tpath"].format(scene_id=scene_id)):
         print("Skip scene {} (GT file not found).".format(scene_id))
         continue
