@@ -45,6 +45,7 @@ SIGNATURES = {
     "bopx_remove_object": (_I, [_CTX, _I]),
     "bopx_set_symmetries": (_I, [_CTX, _I, _d, _I64]),
     "bopx_set_symmetries_many": (_I, [_CTX, _I, _i32, _i64, _d]),
+    "bopx_preload": (_I, [_CTX]),
     "bopx_object_slot": (_I, [_CTX, _I, ctypes.POINTER(_I)]),
     "bopx_mssd_batch": (_I, [_CTX, _I64, _i32, _d, _d, _d]),
     "bopx_mspd_batch": (_I, [_CTX, _I64, _i32, _d, _d, _d, _d]),
@@ -202,6 +203,11 @@ class Context:
   def set_symmetries(self, obj_id, syms12):
     syms12 = np.ascontiguousarray(syms12, np.float64).reshape(-1, 12)
     self.call("bopx_set_symmetries", int(obj_id), ptr(syms12, _d), len(syms12))
+
+  def preload(self):
+    """bopx_preload: the GPU code objects loaded now (returns the status;
+    touches no other context state, so it may run on a thread of its own)."""
+    return self.lib.bopx_preload(self.h)
 
   def set_symmetries_many(self, obj_ids, syms12_list):
     ids = np.ascontiguousarray(obj_ids, np.int32)

@@ -18,6 +18,8 @@ Tensor conventions (all on the evaluator's device):
   cam       float64 [n_frames, 4] (fx, fy, cx, cy)
 torch provides device memory and the stream; the arithmetic is all libbopx.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -41,6 +43,12 @@ class BatchEvaluator:
     torch.cuda.set_device(self.device)
     self.ctx = _lib.Context(int(device))
     self.objects = {}
+    # the code objects load on a thread of their own while the caller
+    # registers objects and parses its inputs, not at the first launch of each
+    # (BOPX_PRELOAD=0: at the first launch)
+    if os.environ.get("BOPX_PRELOAD", "1") != "0":
+      import threading
+      threading.Thread(target=self.ctx.preload, name="bopx-preload", daemon=True).start()
 
   # -- registry ---------------------------------------------------------------
   def add_object(self, obj_id, pts, faces=None, syms=None, diameter=None):

@@ -185,6 +185,12 @@ hipError_t launch_vsd_pair(const PairArgs& a, int cost_type, hipStream_t s);
 hipError_t launch_cover_depths(int W, int H, const float* de, const float* dg,
                                long long* acc /* kCoverCols, device */, hipStream_t s);
 hipError_t read_vsd_stats(unsigned long long* out, int reset);  // diagnostics
+// Load each translation unit's code object on the current device now (the
+// runtime otherwise loads it at the first launch of one of its kernels):
+// hipFuncGetAttributes on one kernel per unit.
+hipError_t preload_pose_kernels();
+hipError_t preload_vsd_kernels();
+hipError_t preload_png_kernels();
 hipError_t launch_vsd_depths(int W, int H, const float* dt, const float* de, const float* dg,
                              double fx, double fy, double cx, double cy, float delta32,
                              int delta_f64, double delta64, const double* taus_host, int n_tau,

@@ -658,4 +658,9 @@ hipError_t launch_png_decode(int64_t n, const uint8_t* zdata, const int64_t* z_o
   return hipGetLastError();
 }
 
+hipError_t preload_png_kernels() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_png_inflate));
+}
+
 }  // namespace bopx

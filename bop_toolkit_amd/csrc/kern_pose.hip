@@ -931,4 +931,9 @@ hipError_t launch_order_by_slot(const int32_t* slots, int64_t n, int ns, int32_t
   return hipGetLastError();
 }
 
+hipError_t preload_pose_kernels() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_sym_error<0>));
+}
+
 }  // namespace bopx

@@ -2194,4 +2194,9 @@ hipError_t launch_render_batch(const ObjDesc* objs, int max_nf, int64_t n, const
   return hipSuccess;
 }
 
+hipError_t preload_vsd_kernels() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_vsd_combine));
+}
+
 }  // namespace bopx

@@ -775,6 +775,24 @@ int bopx_set_symmetries_many(bopx_ctx* c, int n, const int* obj_ids, const int64
   return sync_desc(c);  // one descriptor upload, then the stream is drained
 }
 
+int bopx_preload(bopx_ctx* c) {
+  if (!c) return BOPX_E_INVALID;
+  // no context state is touched (a caller may run this on a thread of its own
+  // while it registers objects): the device, then the three code objects
+  if (hipSetDevice(c->device) != hipSuccess) {
+    (void)hipGetLastError();
+    return BOPX_E_HIP;
+  }
+  hipError_t e = bopx::preload_pose_kernels();
+  if (e == hipSuccess) e = bopx::preload_vsd_kernels();
+  if (e == hipSuccess) e = bopx::preload_png_kernels();
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return BOPX_E_HIP;
+  }
+  return BOPX_OK;
+}
+
 int bopx_object_slot(const bopx_ctx* c, int obj_id, int* slot) {
   if (!c || !slot) return BOPX_E_INVALID;
   return slot_checked(c, obj_id, slot);

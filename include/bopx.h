@@ -101,6 +101,11 @@ int bopx_set_symmetries(bopx_ctx* ctx, int obj_id, const double* syms, int64_t n
 int bopx_set_symmetries_many(bopx_ctx* ctx, int n, const int* obj_ids, const int64_t* ns,
                              const double* syms);
 int bopx_object_slot(const bopx_ctx* ctx, int obj_id, int* slot);
+/* Load the library's GPU code objects on the context's device now instead of
+ * at the first launch of each (the first MSSD / VSD / PNG launch of a process
+ * otherwise waits for it). Touches no other context state, so it may run on a
+ * thread of its own while the caller registers objects. */
+int bopx_preload(bopx_ctx* ctx);
 
 /* ---- point-based pose errors, one output per tuple ----------------------- */
 /* mssd: pose_error.py:96-118. */

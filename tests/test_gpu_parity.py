@@ -926,3 +926,13 @@ def test_set_symmetries_many_matches_one_by_one(golden_errors):
   out = _batch(ctx, "bopx_mssd_batch", ids, g["pose_est"], g["pose_gt"])
   np.testing.assert_allclose(out, g["out_mssd"], rtol=0, atol=TOL)
   ctx.close()
+
+
+def test_preload_code_objects():
+  """bopx_preload loads the library's code objects on the context's device (a
+  second call is a no-op) and needs no registered object."""
+  from bop_toolkit_amd import _lib
+  ctx = _lib.Context(0)
+  assert ctx.preload() == 0
+  assert ctx.preload() == 0
+  ctx.close()
