@@ -145,14 +145,6 @@ def evaluate(p, device=0, calc_errors=True):
     # are scored in a process pool while the next error type runs on the GPU
     n_folders = sum(len(e["vsd_taus"]) if e["type"] == "vsd" else 1 for e in p["errors"])
     scorer = ecs.FolderScorer(n_folders) if ece._dist()[0] == 0 else None
-    if calc_errors and scorer is not None and scorer.native:
-      # the scorer's dataset side (targets view, GT table) built on a thread
-      # while the first error pass runs
-      info = result_name.split("_")
-      ds = info[1].split("-")
-      ecs.prefetch_dataset_side(ecs.parse_args([])["datasets_path"], str(ds[0]), str(ds[1]),
-                                str(ds[2]) if len(ds) > 2 else None, p["targets_filename"],
-                                float(p["visib_gt_min"]))
     sym_err = [e for e in p["errors"] if e["type"] in ("mssd", "mspd")]
     if calc_errors and sym_err:
       # MSSD / MSPD symmetry sets computed on a thread during the VSD pass, for

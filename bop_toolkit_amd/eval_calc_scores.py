@@ -265,35 +265,6 @@ def _gt_table(cache, dp_split, targets_org, visib_gt_min):
   return _ds_cached(key, (targets_org, gts), build)
 
 
-def prefetch_dataset_side(datasets_path, dataset, split, split_type, targets_filename,
-                          visib_gt_min):
-  """Start building the native scorer's dataset side (the targets' view and
-  the GT table, from the parse cache the error passes share) on a thread, so a
-  BOP19 run's first scored folder does not build it in Python while the next
-  error pass runs; returns the thread."""
-  import threading
-
-  def work():
-    try:
-      from .eval_calc_errors import cached_load
-      dp_split = dataset_params.get_split_params(datasets_path, dataset, split, split_type)
-      tpath = os.path.join(dp_split["base_path"], targets_filename)
-      targets = cached_load(inout.load_json, tpath)
-
-      def org():
-        t_org = {}
-        for t in targets:
-          t_org.setdefault(t["scene_id"], {}).setdefault(t["im_id"], {})[t["obj_id"]] = t
-        return t_org
-      targets_org = _ds_cached(("targets_org", id(targets)), targets, org)
-      _gt_table(None, dp_split, targets_org, visib_gt_min)
-    except Exception:  # noqa: BLE001 - the scorer builds what is missing itself
-      pass
-  t = threading.Thread(target=work, name="bopx-score-prefetch", daemon=True)
-  t.start()
-  return t
-
-
 def score_error_dir_native(sps, error_dir_path, cache=None, do_print=True, threads=0):
   """score_error_dir for every setting in sps (one errors folder; the settings
   differ only in correct_th) through the native scorer (bopx_score_folder:
