@@ -156,6 +156,14 @@ def cached_load(loader, path, **kw):
   return hit
 
 
+def scene_gt_arrays(path):
+  """A scene's GT for the arrays path: load_scene_gt_lists' GTLists (cached
+  like any parse), or load_scene_gt's dict when the native reader declines
+  the file."""
+  g = cached_load(inout.load_scene_gt_lists, path)
+  return g if g is not None else cached_load(inout.load_scene_gt, path)
+
+
 # ----------------------------------------------------------------- enumeration
 _ORG_CACHE = {}
 
@@ -609,11 +617,14 @@ def scene_arrays_direct(p, scene_id, scene_targets, ests_org, scene_gt):
   """scene_arrays(scene_records(...)) without the per-record dicts (the arrays
   path keeps no records): the same traversal, ranking, n_top rule, errors and
   GT pairs (eval_calc_errors.py:238-290), straight into lists. Returns
-  (arrays, n_ests)."""
+  (arrays, n_ests). scene_gt: load_scene_gt's dict or load_scene_gt_lists'
+  GTLists (the same pairs and rows)."""
   n_top_p, skip = p["n_top"], p["skip_missing"]
   se = ests_org.get(scene_id, {})
   rec_im, rec_obj, rec_est, rec_score, est_R, est_t, cnt = [], [], [], [], [], [], []
-  pair_gt, gt_R, gt_t = [], [], []
+  pair_gt, gt_R, gt_t, pair_row = [], [], [], []
+  lists = isinstance(scene_gt, inout.GTLists)  # the native reader's arrays (load_scene_gt_lists)
+  gl_obj = scene_gt.obj.tolist() if lists else None
   for im_id, im_targets in scene_targets.items():
     ie = se.get(im_id, {})
     for obj_id, target in im_targets.items():
@@ -630,7 +641,11 @@ def scene_arrays_direct(p, scene_id, scene_targets, ests_org, scene_gt):
             .format(scene_id, im_id, obj_id, len(obj_ests), n_top))
       ranked = sorted(enumerate(obj_ests), key=lambda x: x[1]["score"], reverse=True)
       ranked = ranked[slice(0, n_top)]
-      gts = [(gt_id, gt) for gt_id, gt in enumerate(scene_gt[im_id]) if gt["obj_id"] == obj_id]
+      if lists:
+        a, b = scene_gt.rows(im_id)
+        gts = [g for g, o in enumerate(gl_obj[a:b]) if o == obj_id]
+      else:
+        gts = [(gt_id, gt) for gt_id, gt in enumerate(scene_gt[im_id]) if gt["obj_id"] == obj_id]
       for est_id, est in ranked:
         rec_im.append(im_id)
         rec_obj.append(obj_id)
@@ -639,11 +654,20 @@ def scene_arrays_direct(p, scene_id, scene_targets, ests_org, scene_gt):
         est_R.append(est["R"])
         est_t.append(est["t"])
         cnt.append(len(gts))
+        if lists:
+          pair_gt.extend(gts)
+          pair_row.extend(a + g for g in gts)
+          continue
         for gt_id, gt in gts:
           pair_gt.append(gt_id)
           gt_R.append(gt["cam_R_m2c"])
           gt_t.append(gt["cam_t_m2c"])
   n, m = len(rec_im), len(pair_gt)
+  if lists and m:  # the rows load_scene_gt's arrays give (_poses12: R row-major | t)
+    rows = np.asarray(pair_row, np.int64)
+    pg = np.concatenate([scene_gt.fields["cam_R_m2c"][rows], scene_gt.fields["cam_t_m2c"][rows]], 1)
+  else:
+    pg = _poses12(gt_R, gt_t) if m else np.zeros((0, 12))
   cnt = np.array(cnt, np.int64).reshape(n)
   pair_off = np.zeros(n + 1, np.int64)
   np.cumsum(cnt, out=pair_off[1:])
@@ -654,7 +678,7 @@ def scene_arrays_direct(p, scene_id, scene_targets, ests_org, scene_gt):
          "pe": _poses12(est_R, est_t) if n else np.zeros((0, 12)), "pair_off": pair_off,
          "pair_ri": np.repeat(np.arange(n, dtype=np.int64), cnt),
          "pair_gt": np.array(pair_gt, np.int64).reshape(m),
-         "pg": _poses12(gt_R, gt_t) if m else np.zeros((0, 12))}
+         "pg": pg}
   return arr, n
 
 
@@ -948,10 +972,12 @@ def run(p, device=0):
         # scene runs and is saved
         scene_camera = cached_load(inout.load_scene_camera,
                                    dp_split["scene_camera_tpath"].format(scene_id=scene_id))
-        scene_gt = cached_load(inout.load_scene_gt,
-                               dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+        gt_path = dp_split["scene_gt_tpath"].format(scene_id=scene_id)
         planned = None
         if arrays:
+          # the instance lists as arrays, read natively off the GIL (the main
+          # thread launches and saves the previous scene meanwhile)
+          scene_gt = scene_gt_arrays(gt_path)
           arr, n_ests = scene_arrays_direct_cached(p, scene_id, scene_targets, ests_org, scene_gt)
           recs = None
           vals, todo = plan_arrays(p, arr, models_info)
@@ -971,6 +997,7 @@ def run(p, device=0):
                   np.unique(arr["rec_im"][arr["pair_ri"][todo]]).tolist(), scene_id, scene_camera)
           planned = ("arrays", arr, vals, todo, (depths, depth_ims))
           return scene_camera, recs, n_ests, planned
+        scene_gt = cached_load(inout.load_scene_gt, gt_path)
         recs, n_ests = scene_records_cached(p, scene_id, scene_targets, ests_org, scene_gt)
         if recs:
           errs, todo, mine = plan_rank(p, recs, models_info, ev.objects if ev else None,

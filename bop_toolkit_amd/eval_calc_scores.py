@@ -237,18 +237,40 @@ def _gt_table(cache, dp_split, targets_org, visib_gt_min):
   GT of an image) as arrays, with per-image offsets and scene index
   (score_error_dir's scene_gt / gt_valid, eval_calc_scores.py:183-214)."""
   import numpy as np
-  from .eval_calc_errors import cached_load  # the error passes' parses (same process)
-  gts = [(cached_load(inout.load_scene_gt, dp_split["scene_gt_tpath"].format(scene_id=scene_id)),
-          cached_load(inout.load_json, dp_split["scene_gt_info_tpath"].format(scene_id=scene_id),
-                      keys_to_int=True)) for scene_id in targets_org]
+  from .eval_calc_errors import cached_load, scene_gt_arrays  # the error passes' parses
+  gts = []
+  for scene_id in targets_org:
+    # the native readers' arrays (no Python JSON parse under the GIL while the
+    # next error pass runs), or the dicts when either file is declined
+    gpath = dp_split["scene_gt_tpath"].format(scene_id=scene_id)
+    ipath = dp_split["scene_gt_info_tpath"].format(scene_id=scene_id)
+    g = scene_gt_arrays(gpath)
+    i = cached_load(inout.load_scene_gt_info_lists, ipath) if isinstance(g, inout.GTLists) \
+        else None
+    if i is None:
+      g = cached_load(inout.load_scene_gt, gpath)
+      i = cached_load(inout.load_json, ipath, keys_to_int=True)
+    gts.append((g, i))
+
+  def lists_image(scene_gt, scene_gt_info, im_id):
+    # (obj ids, [{"visib_fract"}]) of an image, as valid_gts reads the dicts;
+    # an info list shorter than the GT list indexes past its end there too
+    a, b = scene_gt.rows(im_id)
+    c, d = scene_gt_info.rows(im_id)
+    vf = scene_gt_info.fields["visib_fract"][c:d, 0].tolist()
+    return [{"obj_id": o} for o in scene_gt.obj[a:b].tolist()], [{"visib_fract": v} for v in vf]
 
   def build():
     sc, im, ob, gid, val, off, fi = [], [], [], [], [], [0], []
     for k, (scene_id, scene_targets) in enumerate(targets_org.items()):
       scene_gt, scene_gt_info = gts[k]
+      lists = isinstance(scene_gt, inout.GTLists)
       for im_id, tg in scene_targets.items():
-        im_gts = scene_gt[im_id]
-        valid = valid_gts(im_gts, scene_gt_info[im_id], tg, visib_gt_min)
+        if lists:
+          im_gts, im_info = lists_image(scene_gt, scene_gt_info, im_id)
+        else:
+          im_gts, im_info = scene_gt[im_id], scene_gt_info[im_id]
+        valid = valid_gts(im_gts, im_info, tg, visib_gt_min)
         for g, gt in enumerate(im_gts):
           sc.append(scene_id)
           im.append(im_id)

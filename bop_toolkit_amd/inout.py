@@ -379,6 +379,72 @@ def load_scene_gt(path):
   return scene_gt
 
 
+class GTLists:
+  """The per-image instance lists of a scene_gt.json / scene_gt_info.json as
+  arrays (bopx_gt_lists_open): im_ids in file order, off [n_im + 1] (records
+  of image k are off[k] .. off[k+1]-1), fields {name: float64 [n_rec, width]}.
+  rows(im_id) raises KeyError(im_id) like scene_gt[im_id]."""
+
+  def __init__(self, im_ids, off, fields):
+    self.im_ids, self.off, self.fields = im_ids, off, fields
+    self.index = {im: k for k, im in enumerate(im_ids.tolist())}
+
+  def rows(self, im_id):
+    k = self.index[im_id]
+    return int(self.off[k]), int(self.off[k + 1])
+
+
+def load_gt_lists(path, fields):
+  """GTLists of the file's `fields` ({name: width}), or None when the native
+  reader declines it (another structure, a missing field, NaN literals, ...:
+  the caller then parses it with load_json and meets what the reference
+  meets)."""
+  import ctypes
+  L = _io_lib()
+  if not getattr(L, "_gtl_sig", False):
+    L.bopx_gt_lists_open.argtypes = [
+        ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int64),
+        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)]
+    L.bopx_gt_lists_open.restype = ctypes.c_void_p
+    L.bopx_gt_lists_take.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.POINTER(ctypes.c_void_p)]
+    L.bopx_gt_lists_take.restype = None
+    L._gtl_sig = True
+  names = list(fields)
+  nf = len(names)
+  n_im, n_rec, st = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int(0)
+  h = L.bopx_gt_lists_open(os.fsencode(path), nf,
+                           (ctypes.c_char_p * nf)(*[n.encode() for n in names]),
+                           (ctypes.c_int * nf)(*[int(fields[n]) for n in names]),
+                           ctypes.byref(n_im), ctypes.byref(n_rec), ctypes.byref(st))
+  if not h:
+    return None
+  im = np.empty(n_im.value, np.int64)
+  off = np.empty(n_im.value + 1, np.int64)
+  vals = {n: np.empty((n_rec.value, int(fields[n])), np.float64) for n in names}
+  ptrs = (ctypes.c_void_p * nf)(*[vals[n].ctypes.data for n in names])
+  L.bopx_gt_lists_take(h, im.ctypes.data, off.ctypes.data, ptrs)
+  return GTLists(im, off, vals)
+
+
+def load_scene_gt_lists(path):
+  """scene_gt.json as GTLists (cam_R_m2c [n, 9], cam_t_m2c [n, 3], obj_id
+  [n, 1]; the values load_scene_gt gives), or None (load_scene_gt then)."""
+  g = load_gt_lists(path, {"cam_R_m2c": 9, "cam_t_m2c": 3, "obj_id": 1})
+  if g is not None:
+    o = g.fields["obj_id"][:, 0]
+    if not np.array_equal(o, np.trunc(o)) or (len(o) and np.abs(o).max() >= 2 ** 53):
+      return None  # a non-integral id: compared as the dict path compares it
+    g.obj = o.astype(np.int64)
+  return g
+
+
+def load_scene_gt_info_lists(path):
+  """scene_gt_info.json's visib_fract as GTLists, or None (load_json then)."""
+  return load_gt_lists(path, {"visib_fract": 1})
+
+
 def load_bop_results(path, version="bop19"):
   """BOP19 CSV results: scene_id,im_id,obj_id,score,R,t,time; a first line
   containing the header is skipped (inout.py:221-261). Files in the plain

@@ -69,6 +69,21 @@ enum { BOPX_RES_READ = -1, BOPX_RES_OTHER = -2, BOPX_RES_CAP = -3 };
 int64_t bopx_read_bop_results(const char* path, int64_t cap, int64_t* ids, double* score,
                               double* R, double* t, double* time, int64_t* need);
 
+/* Per-image instance lists of a BOP scene file into arrays: scene_gt.json
+ * (bop_toolkit_lib/inout.py:182-198) and scene_gt_info.json, i.e. a JSON
+ * object {"<im_id>": [{...}, ...], ...}. Fields: n_fields (1..16) member names
+ * with widths (1: a number, w > 1: a flat array of exactly w numbers), each
+ * present once in every record; other members are skipped. Numbers convert as
+ * Python's json + float64 convert them. Open parses the file: *n_im images,
+ * *n_rec records in file order, *status 0; NULL with *status BOPX_RES_READ
+ * (cannot read) or BOPX_RES_OTHER (not in this strict form: parse it with
+ * Python's json). Take copies im_ids[n_im], off[n_im + 1] (records of image k
+ * are off[k] .. off[k+1]-1) and vals[f][n_rec * width f], then frees the
+ * handle (NULL buffers: frees only). */
+void* bopx_gt_lists_open(const char* path, int n_fields, const char* const* names,
+                         const int* widths, int64_t* n_im, int64_t* n_rec, int* status);
+void bopx_gt_lists_take(void* h, int64_t* im_ids, int64_t* off, double* const* vals);
+
 /* 1 when the libdeflate inflater is in use, 0 for zlib. */
 int bopx_io_backend(void);
 

@@ -59,8 +59,9 @@ def test_io_library_exports_every_declared_symbol():
   """libbopx_io.so (host depth decoder) exports what include/bopx_io.h declares."""
   src = re.sub(r"/\*.*?\*/", "", open(IO_HEADER).read(), flags=re.S)
   syms = sorted(set(re.findall(r"\b(bopx_[a-z0-9_]+)\s*\(", src)))
-  assert syms == ["bopx_decode_depth_png", "bopx_io_backend", "bopx_load_depth_pngs",
-                  "bopx_pack_depth_pngs", "bopx_read_bop_results"]
+  assert syms == ["bopx_decode_depth_png", "bopx_gt_lists_open", "bopx_gt_lists_take",
+                  "bopx_io_backend", "bopx_load_depth_pngs", "bopx_pack_depth_pngs",
+                  "bopx_read_bop_results"]
   assert os.path.exists(IO_LIB), "libbopx_io.so not built (make -C bop_toolkit_amd/csrc)"
   L = ctypes.CDLL(IO_LIB)
   assert not [s for s in syms if not hasattr(L, s)]
