@@ -85,13 +85,32 @@ def _depth_path(dp_split, scene_id, im_id):
   return path if os.path.exists(path) else path.replace(".tif", ".png")
 
 
+def _scene_gt(path):
+  """A scene's GT: the native reader's inout.GTLists (no Python JSON parse
+  under the GIL on the prefetch thread), or load_scene_gt's dict when it
+  declines the file (eval_calc_errors.scene_gt_arrays)."""
+  from .eval_calc_errors import scene_gt_arrays
+  return scene_gt_arrays(path)
+
+
+def _gt_count(scene_gt, im_id):
+  if isinstance(scene_gt, inout.GTLists):
+    a, b = scene_gt.rows(im_id)
+    return b - a
+  return len(scene_gt[im_id])
+
+
+def _gt_ims(scene_gt):
+  return sorted(scene_gt.index if isinstance(scene_gt, inout.GTLists) else scene_gt.keys())
+
+
 def my_images(scene_gt, rank, world):
   """This rank's image ids of a scene (LPT on the GT count per image)."""
   from . import shard
-  im_ids = sorted(scene_gt.keys())
+  im_ids = _gt_ims(scene_gt)
   if world == 1:
     return im_ids
-  part = shard.lpt_shard([len(scene_gt[i]) + 1 for i in im_ids], world)[rank]
+  part = shard.lpt_shard([_gt_count(scene_gt, i) + 1 for i in im_ids], world)[rank]
   return [im_ids[k] for k in part]
 
 
@@ -110,7 +129,8 @@ def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_ba
   from . import runtime
   scene_camera = _cached(inout.load_scene_camera,
                          dp_split["scene_camera_tpath"].format(scene_id=scene_id))
-  scene_gt = _cached(inout.load_scene_gt, dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+  scene_gt = _scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+  lists = isinstance(scene_gt, inout.GTLists)
   im_ids = my_images(scene_gt, rank, world)
   if im_batch is None:
     im_batch = max(1, len(im_ids)) if frames_all is not None and not masks else 128
@@ -154,22 +174,34 @@ def scene_stats(ev, torch, dp_split, scene_id, delta, canvas_scale, masks, im_ba
         frames = nxt.result()
         if bi + 1 < len(batches):
           nxt = ahead.submit(load, batches[bi + 1], (bi + 1) & 1)
-      cam, obj, Rs, ts, fidx, owner = [], [], [], [], [], []
+      cam, obj, Rs, ts, fidx, owner, rws = [], [], [], [], [], [], []
       for k, im_id in enumerate(ims):
         K = scene_camera[im_id]["cam_K"]
         cam.append((K[0, 0], K[1, 1], K[0, 2], K[1, 2]))
-        for gt in scene_gt[im_id]:
-          obj.append(gt["obj_id"])
-          Rs.append(gt["cam_R_m2c"])
-          ts.append(gt["cam_t_m2c"])
-          fidx.append(k)
-          owner.append(im_id)
+        if lists:
+          a, b = scene_gt.rows(im_id)
+          obj.extend(scene_gt.obj[a:b].tolist())
+          rws.extend(range(a, b))
+          fidx.extend([k] * (b - a))
+          owner.extend([im_id] * (b - a))
+        else:
+          for gt in scene_gt[im_id]:
+            obj.append(gt["obj_id"])
+            Rs.append(gt["cam_R_m2c"])
+            ts.append(gt["cam_t_m2c"])
+            fidx.append(k)
+            owner.append(im_id)
         res[im_id] = []
       if not obj:
         continue
       # [R row-major | t] per GT, float64
-      pose = np.concatenate([np.asarray(Rs, np.float64).reshape(-1, 9),
-                             np.asarray(ts, np.float64).reshape(-1, 3)], 1)
+      if lists:
+        rws = np.asarray(rws, np.int64)
+        pose = np.concatenate([scene_gt.fields["cam_R_m2c"][rws],
+                               scene_gt.fields["cam_t_m2c"][rws]], 1)
+      else:
+        pose = np.concatenate([np.asarray(Rs, np.float64).reshape(-1, 9),
+                               np.asarray(ts, np.float64).reshape(-1, 3)], 1)
       T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
       d_frames = (frames.to(dev, non_blocking=True) if torch.is_tensor(frames)
                   else T(frames, torch.float32))
@@ -208,8 +240,8 @@ def _gather_info(torch, ev, stats, scene_gt, rank, world):
   if world == 1:
     return {im: [r for r, _ in lst] for im, lst in stats.items()}
   from . import shard
-  ims = sorted(scene_gt.keys())
-  first = np.cumsum([0] + [len(scene_gt[i]) for i in ims])
+  ims = _gt_ims(scene_gt)
+  first = np.cumsum([0] + [_gt_count(scene_gt, i) for i in ims])
   pos = {im: int(first[k]) for k, im in enumerate(ims)}
   ids, rows = [], []
   for im, lst in stats.items():
@@ -223,7 +255,7 @@ def _gather_info(torch, ev, stats, scene_gt, rank, world):
   if rank != 0:
     return None
   table = table.cpu().numpy()
-  return {im: [table[pos[im] + g] for g in range(len(scene_gt[im]))] for im in ims}
+  return {im: [table[pos[im] + g] for g in range(_gt_count(scene_gt, im))] for im in ims}
 
 
 class SceneDepthPrefetch:
@@ -251,7 +283,7 @@ class SceneDepthPrefetch:
         return [], []
       scene_camera = _cached(inout.load_scene_camera,
                              dp["scene_camera_tpath"].format(scene_id=scene_id))
-      im_ids = my_images(_cached(inout.load_scene_gt, path_gt), rank, world)
+      im_ids = my_images(_scene_gt(path_gt), rank, world)
       return ([_depth_path(dp, scene_id, i) for i in im_ids],
               [scene_camera[i]["depth_scale"] for i in im_ids])
     W, H = dp["im_size"]
@@ -290,7 +322,7 @@ def calc_gt_info(p):
       frames = ahead.take(scene_id)
       stats = scene_stats(ev, torch, dp_split, scene_id, p["delta"], 3, False, rank=rank,
                           world=world, frames_all=frames)
-      scene_gt = _cached(inout.load_scene_gt, dp_split["scene_gt_tpath"].format(scene_id=scene_id))
+      scene_gt = _scene_gt(dp_split["scene_gt_tpath"].format(scene_id=scene_id))
       rows = _gather_info(torch, ev, stats, scene_gt, rank, world)
       if rows is None:
         continue
