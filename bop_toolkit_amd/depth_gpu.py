@@ -35,7 +35,10 @@ MAX_RAW = 1 << 28     # inflated bytes per frame (bopx_internal.h kPngMaxRaw)
 # (diagnostics for tools/e2e_bench.py): pack = reading and checking the files
 # on host threads; decode = upload + kernels + status readback; host = frames
 # the device did not take.
-STATS = {"calls": 0, "frames": 0, "pack_s": 0.0, "decode_s": 0.0, "host_s": 0.0}
+STATS = {"calls": 0, "frames": 0, "pack_s": 0.0, "decode_s": 0.0, "host_s": 0.0,
+         # submit's other host steps (layout stat, page-locked staging growth, waits for
+         # a slot's previous upload, the launch call) and finish's wait for the kernels
+         "stat_s": 0.0, "stage_s": 0.0, "slot_wait_s": 0.0, "launch_s": 0.0, "kernel_wait_s": 0.0}
 _STATS_LOCK = threading.Lock()
 
 
@@ -157,8 +160,10 @@ class DepthDecoder:
     hh = (ctypes.c_int * n)(*([int(H)] * n))
     ww = (ctypes.c_int * n)(*([int(W)] * n))
     # the whole batch's layout (file sizes, 256-byte aligned), one stat per file
+    t_stat = time.perf_counter()
     L.bopx_pack_depth_pngs((ctypes.c_char_p * n)(*enc), n, hh, ww, None, 0, z_off.ctypes.data,
                            z_len.ctypes.data, 0, st.ctypes.data, ctypes.byref(need))
+    _stat(stat_s=time.perf_counter() - t_stat)
     if self._copy_stream is None:
       self._copy_stream = torch.cuda.Stream(dev)
     cs = self._copy_stream
@@ -173,8 +178,10 @@ class DepthDecoder:
       c1 = min(n, c0 + self.CHUNK)
       m = c1 - c0
       slot = k & 1
+      t = time.perf_counter()
       if self._copied[slot] is not None:
         self._copied[slot].synchronize()  # the slot's previous bytes are up
+      _stat(slot_wait_s=time.perf_counter() - t)
       t = time.perf_counter()
       off = np.zeros(m, np.int64)
       ln = np.zeros(m, np.int32)
@@ -183,7 +190,10 @@ class DepthDecoder:
       cp = (ctypes.c_char_p * m)(*enc[c0:c1])
       L.bopx_pack_depth_pngs(cp, m, hh, ww, None, 0, off.ctypes.data, ln.ctypes.data, 0,
                              cst.ctypes.data, ctypes.byref(cneed))
+      t_st = time.perf_counter()
       buf = self._staging(torch, cneed.value, slot)
+      t += time.perf_counter() - t_st  # (not packing)
+      _stat(stage_s=time.perf_counter() - t_st)
       rc = L.bopx_pack_depth_pngs(cp, m, hh, ww, buf.data_ptr(), buf.numel(), off.ctypes.data,
                                   ln.ctypes.data, nt, cst.ctypes.data, ctypes.byref(cneed))
       if rc < 0:
@@ -212,6 +222,7 @@ class DepthDecoder:
     self.ctx.call("bopx_png_decode_dev", n, z_d.data_ptr(), off_d.data_ptr(), len_d.data_ptr(),
                   int(H), int(W), sc_d.data_ptr(), raw.data_ptr(), raw_stride, frames.data_ptr(),
                   status.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+    _stat(launch_s=time.perf_counter() - t1)
     pend.__dict__.update(st=st, status=status, keep=(z_d, raw, off_d, len_d, sc_d),
                          t1=t1)
     return pend
@@ -239,9 +250,11 @@ class DepthDecoder:
       frames.copy_(torch.from_numpy(_host_frames(paths, scales, H, W, workers)))
       self.last_host = n
       return
+    tw = time.perf_counter()
     gst = pend.status.view(n, 2)[:, 0].cpu().numpy()  # waits for the kernels
     pend.keep = None
     t2 = time.perf_counter()
+    _stat(kernel_wait_s=t2 - tw)
     host = np.nonzero((pend.st != 0) | (gst != 0))[0]
     if len(host):
       arr = _host_frames([paths[k] for k in host], None if scales is None else

@@ -203,6 +203,11 @@ def main():
     with open(os.path.join(REPO, "gpurun_out", "gt_profile.txt"), "w") as f:
       f.write(s_.getvalue())
 
+  # the decoder's counters of calc_gt_info, then zeroed for the evaluation
+  from bop_toolkit_amd import depth_gpu as _dg
+  gt_stats = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in _dg.STATS.items()}
+  for k in _dg.STATS:
+    _dg.STATS[k] = 0 if k in ("calls", "frames") else 0.0
   # the evaluation starts cold: nothing calc_gt_info parsed stays in the caches
   ece._FILE_CACHE.clear()
   ece._ORG_CACHE.clear()
@@ -366,7 +371,7 @@ def main():
       "host_s": {k[5:]: round(v, 3) for k, v in phases.items() if k.startswith("host:")},
       "eval_tuples_per_s": n / t_eval,
       "depth_decoder": "gpu" if depth_gpu.enabled() else "host", "ab_depth": ab,
-      "depth_decoder_first_run": first_stats, "tail": first_tail, "timeline": first_timeline,
+      "depth_decoder_first_run": first_stats, "depth_decoder_gt_info": gt_stats, "tail": first_tail, "timeline": first_timeline,
       "events": first_events,
       "ar": {k: round(float(v), 4) for k, v in scores.items()}}))
 
