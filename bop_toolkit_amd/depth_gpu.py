@@ -271,33 +271,6 @@ class DepthDecoder:
     return self.finish(self.submit(paths, scales, H, W, torch, workers), torch)
 
 
-_SWITCH = {"active": 0, "saved": None}
-
-
-def _gil_switch(enter):
-  """While a GroupPrefetch works, the interpreter's thread switch interval is
-  BOPX_GIL_SWITCH_S (default 0.5 ms, 0 = unchanged): its worker returns from
-  every ctypes / torch call needing the GIL back, and with the default 5 ms a
-  caller running Python meanwhile (organize(), the JSON parses) holds it for up
-  to 5 ms at each of those returns -- the packing of a 4,096-frame group took
-  0.27 s longer in the cold run for that alone."""
-  import sys
-  v = float(os.environ.get("BOPX_GIL_SWITCH_S", "0.0005"))
-  if v <= 0:
-    return
-  with _STATS_LOCK:
-    if enter:
-      _SWITCH["active"] += 1
-      if _SWITCH["active"] == 1:
-        _SWITCH["saved"] = sys.getswitchinterval()
-        sys.setswitchinterval(v)
-    else:
-      _SWITCH["active"] -= 1
-      if _SWITCH["active"] == 0 and _SWITCH["saved"] is not None:
-        sys.setswitchinterval(_SWITCH["saved"])
-        _SWITCH["saved"] = None
-
-
 class GroupPrefetch:
   """Test depth of consecutive scenes decoded in shared launches, ahead of use.
 
@@ -335,7 +308,6 @@ class GroupPrefetch:
     self.first_frames = int(max_frames if first_frames is None else max(1, first_frames))
     self.stream, self.consumer, self.device = stream, consumer, device
     self.groups = 0
-    _gil_switch(True)
     self._thread = threading.Thread(target=self._run, name="bopx-depth-groups", daemon=True)
     self._thread.start()
 
@@ -374,7 +346,6 @@ class GroupPrefetch:
     finally:
       fin_q.put(StopIteration)
       fin.join()
-      _gil_switch(False)
       for f in self._fut.values():
         if not f.done():
           f.set_exception(RuntimeError("depth prefetch stopped"))
