@@ -38,7 +38,8 @@ MAX_RAW = 1 << 28     # inflated bytes per frame (bopx_internal.h kPngMaxRaw)
 STATS = {"calls": 0, "frames": 0, "pack_s": 0.0, "decode_s": 0.0, "host_s": 0.0,
          # submit's other host steps (layout stat, page-locked staging growth, waits for
          # a slot's previous upload, the launch call) and finish's wait for the kernels
-         "stat_s": 0.0, "stage_s": 0.0, "slot_wait_s": 0.0, "launch_s": 0.0, "kernel_wait_s": 0.0}
+         "stat_s": 0.0, "stage_s": 0.0, "slot_wait_s": 0.0, "launch_s": 0.0, "kernel_wait_s": 0.0,
+         "pack_c_s": 0.0}  # the packing calls alone (host threads, GIL released)
 _STATS_LOCK = threading.Lock()
 
 
@@ -194,8 +195,10 @@ class DepthDecoder:
       buf = self._staging(torch, cneed.value, slot)
       t += time.perf_counter() - t_st  # (not packing)
       _stat(stage_s=time.perf_counter() - t_st)
+      t_c = time.perf_counter()
       rc = L.bopx_pack_depth_pngs(cp, m, hh, ww, buf.data_ptr(), buf.numel(), off.ctypes.data,
                                   ln.ctypes.data, nt, cst.ctypes.data, ctypes.byref(cneed))
+      _stat(pack_c_s=time.perf_counter() - t_c)
       if rc < 0:
         raise RuntimeError("bopx_pack_depth_pngs: %d bytes needed" % cneed.value)
       pend.pack_s += time.perf_counter() - t
