@@ -66,6 +66,12 @@ def _io():
   return L
 
 
+def pack_threads():
+  """Host threads of a packing call: BOPX_PACK_THREADS, default min(16, CPUs)."""
+  v = os.environ.get("BOPX_PACK_THREADS")
+  return max(1, int(v)) if v else min(16, os.cpu_count() or 1)
+
+
 def pack(paths, H, W, buf_for, workers=None):
   """Read and pack the files (bopx_pack_depth_pngs). buf_for(nbytes) returns
   a writable uint8 buffer (numpy array or a page-locked torch tensor) of at
@@ -85,7 +91,7 @@ def pack(paths, H, W, buf_for, workers=None):
   addr = buf.ctypes.data if isinstance(buf, np.ndarray) else buf.data_ptr()
   cap = buf.nbytes if isinstance(buf, np.ndarray) else buf.numel() * buf.element_size()
   rc = L.bopx_pack_depth_pngs(cp, n, hh, ww, addr, cap, z_off.ctypes.data, z_len.ctypes.data,
-                              int(workers or min(16, os.cpu_count() or 1)), st.ctypes.data,
+                              int(workers or pack_threads()), st.ctypes.data,
                               ctypes.byref(need))
   if rc < 0:
     raise RuntimeError("bopx_pack_depth_pngs: %d bytes needed, %d given" % (need.value, cap))
@@ -174,7 +180,7 @@ class DepthDecoder:
     # before it decodes (z_d is recorded on `stream` below)
     with torch.cuda.stream(cs):
       z_d = torch.empty(need.value, dtype=torch.uint8, device=dev)
-    nt = int(workers or min(16, os.cpu_count() or 1))
+    nt = int(workers or pack_threads())
     for k, c0 in enumerate(range(0, n, self.CHUNK)):
       c1 = min(n, c0 + self.CHUNK)
       m = c1 - c0
