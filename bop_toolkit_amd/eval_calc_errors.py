@@ -177,7 +177,8 @@ def organize(targets, ests):
   hit = _ORG_CACHE.get(key)
   if hit is not None and hit[0] is targets and hit[1] is ests:
     return hit[2]
-  out = _organize(targets, ests)
+  with inout.gc_paused():
+    out = _organize(targets, ests)
   if len(_ORG_CACHE) > 8:
     _ORG_CACHE.clear()
   _ORG_CACHE[key] = (targets, ests, out)

@@ -7,6 +7,7 @@ coordinates and the texture file name, as float64 arrays like the reference.
 """
 import json
 import os
+import threading
 
 import numpy as np
 
@@ -394,6 +395,36 @@ class GTLists:
     return int(self.off[k]), int(self.off[k + 1])
 
 
+_GC_PAUSE = {"n": 0, "was": False}
+_GC_LOCK = threading.Lock()
+
+
+class gc_paused:
+  """Context manager: Python's cyclic collector off while bulk acyclic
+  structures are built (100k result / target dicts and their organised view:
+  the generation-2 passes over the millions of tracked objects are ~half of
+  such a build); re-enabled when the last concurrent user leaves, if it was on."""
+
+  def __enter__(self):
+    import gc
+    with _GC_LOCK:
+      if _GC_PAUSE["n"] == 0 and os.environ.get("BOPX_GC_PAUSE", "1") == "0":  # A/B
+        _GC_PAUSE["was"] = False
+      elif _GC_PAUSE["n"] == 0:
+        _GC_PAUSE["was"] = gc.isenabled()
+        gc.disable()
+      _GC_PAUSE["n"] += 1
+    return self
+
+  def __exit__(self, *exc):
+    import gc
+    with _GC_LOCK:
+      _GC_PAUSE["n"] -= 1
+      if _GC_PAUSE["n"] == 0 and _GC_PAUSE["was"]:
+        gc.enable()
+    return False
+
+
 def load_gt_lists(path, fields):
   """GTLists of the file's `fields` ({name: width}), or None when the native
   reader declines it (another structure, a missing field, NaN literals, ...:
@@ -492,8 +523,9 @@ def _bop_results_native(path):
     return None
   sc, im, ob = ids.T.tolist()
   score, tm = score.tolist(), tm.tolist()
-  return [{"scene_id": sc[k], "im_id": im[k], "obj_id": ob[k], "score": score[k], "R": R[k],
-           "t": t[k], "time": tm[k]} for k in range(n)]
+  with gc_paused():
+    return [{"scene_id": sc[k], "im_id": im[k], "obj_id": ob[k], "score": score[k], "R": R[k],
+             "t": t[k], "time": tm[k]} for k in range(n)]
 
 
 def _bop_results_lines(body):
