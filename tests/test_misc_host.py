@@ -163,3 +163,28 @@ def test_bop_results_native_reader_matches_the_line_reader(tmp_path):
       _same_results(inout.load_bop_results(p), want)
   with pytest.raises(OSError):
     inout.load_bop_results(str(tmp_path / "missing.csv"))
+
+
+def test_gc_paused_nests_and_restores(monkeypatch):
+  """inout.gc_paused: the collector is off inside (nested too) and back to its
+  previous state after; BOPX_GC_PAUSE=0 leaves it alone."""
+  import gc
+  from bop_toolkit_amd import inout
+  assert gc.isenabled()
+  with inout.gc_paused():
+    assert not gc.isenabled()
+    with inout.gc_paused():
+      assert not gc.isenabled()
+    assert not gc.isenabled()
+  assert gc.isenabled()
+  gc.disable()
+  try:
+    with inout.gc_paused():
+      pass
+    assert not gc.isenabled()  # was off: stays off
+  finally:
+    gc.enable()
+  monkeypatch.setenv("BOPX_GC_PAUSE", "0")
+  with inout.gc_paused():
+    assert gc.isenabled()
+  assert gc.isenabled()
