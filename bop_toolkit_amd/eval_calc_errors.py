@@ -152,7 +152,8 @@ def cached_load(loader, path, **kw):
       if hit is None:
         if len(_FILE_CACHE) >= _FILE_CACHE_MAX:
           _FILE_CACHE.pop(next(iter(_FILE_CACHE)))
-        hit = _FILE_CACHE[key] = loader(path, **kw)
+        with inout.gc_paused():  # parsed files are acyclic
+          hit = _FILE_CACHE[key] = loader(path, **kw)
   return hit
 
 

@@ -228,7 +228,8 @@ def _ds_cached(key, keep, fn):
     if hit is None:
       if len(_DS_CACHE) > 32:
         _DS_CACHE.clear()
-      hit = _DS_CACHE[key] = (keep, fn())
+      with inout.gc_paused():  # bulk acyclic builds (the GT table, the targets' view)
+        hit = _DS_CACHE[key] = (keep, fn())
     return hit[1]
 
 
