@@ -18,6 +18,7 @@ Tensor conventions (all on the evaluator's device):
   cam       float64 [n_frames, 4] (fx, fy, cx, cy)
 torch provides device memory and the stream; the arithmetic is all libbopx.
 """
+import atexit
 import os
 
 import numpy as np
@@ -35,6 +36,25 @@ def _p(t):
   return t.data_ptr() if t is not None else None
 
 
+_PRELOADS = set()  # preload threads not yet joined
+
+
+def _join_preload(t, box):
+  t.join()
+  _PRELOADS.discard(t)
+  rc = box.get("rc", 0)
+  if rc:
+    import warnings
+    warnings.warn("bopx_preload returned status %d (the code objects load at the first launch)"
+                  % rc, RuntimeWarning)
+
+
+@atexit.register
+def _join_preloads():
+  for t in list(_PRELOADS):
+    t.join()
+
+
 class BatchEvaluator:
   """Registry of resident objects + batched error launches on one GPU."""
 
@@ -45,10 +65,33 @@ class BatchEvaluator:
     self.objects = {}
     # the code objects load on a thread of their own while the caller
     # registers objects and parses its inputs, not at the first launch of each
-    # (BOPX_PRELOAD=0: at the first launch)
+    # (BOPX_PRELOAD=0: at the first launch). The thread is joined before the
+    # first launch through this evaluator and at interpreter exit (_PRELOADS),
+    # so it never runs into the HIP runtime's teardown; a failure is reported
+    # as a warning, not dropped.
+    self._preload = None
     if os.environ.get("BOPX_PRELOAD", "1") != "0":
       import threading
-      threading.Thread(target=self.ctx.preload, name="bopx-preload", daemon=True).start()
+      box = {}
+      ctx = self.ctx
+      t = threading.Thread(target=lambda: box.setdefault("rc", ctx.preload()),
+                           name="bopx-preload", daemon=True)
+      self._preload = (t, box)
+      _PRELOADS.add(t)
+      t.start()
+
+  def wait_preload(self):
+    """Join the code-object preload thread (once); a non-zero status is
+    reported as a RuntimeWarning (the launches load the code objects
+    themselves and raise their own errors)."""
+    pre, self._preload = self._preload, None
+    if pre is not None:
+      _join_preload(*pre)
+
+  def _call(self, name, *args):
+    if self._preload is not None:
+      self.wait_preload()
+    return self.ctx.call(name, *args)
 
   # -- registry ---------------------------------------------------------------
   def add_object(self, obj_id, pts, faces=None, syms=None, diameter=None):
@@ -100,35 +143,35 @@ class BatchEvaluator:
   def mssd(self, slots, pose_est, pose_gt, out=None):
     n = slots.numel()
     out = self._out(n) if out is None else out
-    self.ctx.call("bopx_mssd_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(out),
+    self._call("bopx_mssd_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(out),
                   _stream(self.device))
     return out
 
   def mspd(self, slots, pose_est, pose_gt, K, out=None):
     n = slots.numel()
     out = self._out(n) if out is None else out
-    self.ctx.call("bopx_mspd_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(K),
+    self._call("bopx_mspd_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(K),
                   _p(out), _stream(self.device))
     return out
 
   def add(self, slots, pose_est, pose_gt, out=None):
     n = slots.numel()
     out = self._out(n) if out is None else out
-    self.ctx.call("bopx_add_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(out),
+    self._call("bopx_add_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(out),
                   _stream(self.device))
     return out
 
   def adi(self, slots, pose_est, pose_gt, out=None):
     n = slots.numel()
     out = self._out(n) if out is None else out
-    self.ctx.call("bopx_adi_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(out),
+    self._call("bopx_adi_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(out),
                   _stream(self.device))
     return out
 
   def proj(self, slots, pose_est, pose_gt, K, out=None):
     n = slots.numel()
     out = self._out(n) if out is None else out
-    self.ctx.call("bopx_proj_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(K),
+    self._call("bopx_proj_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(K),
                   _p(out), _stream(self.device))
     return out
 
@@ -176,7 +219,7 @@ class BatchEvaluator:
         v[:, k0:k1] = r
       return self._vsd_result(buf, n, len(taus), delta_flags)
     H, W = int(frames.shape[-2]), int(frames.shape[-1])
-    self.ctx.call("bopx_vsd_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(frame_idx),
+    self._call("bopx_vsd_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt), _p(frame_idx),
                   _p(frames), W, H, _p(cam), float(delta), int(delta_flags),
                   taus.ctypes.data_as(_lib._d), len(taus), int(bool(normalized_by_diameter)),
                   _p(diameters), code, _p(buf), _stream(self.device))
@@ -209,7 +252,7 @@ class BatchEvaluator:
         v[:, k0:k1] = r
       return self._vsd_result(buf, n, len(taus), delta_flags)
     H, W = int(frames.shape[-2]), int(frames.shape[-1])
-    self.ctx.call("bopx_vsd_shared_batch_dev", render_slots.numel(), _p(render_slots),
+    self._call("bopx_vsd_shared_batch_dev", render_slots.numel(), _p(render_slots),
                   _p(render_poses), _p(render_frame_idx), n, _p(est_render), _p(gt_render),
                   _p(frames), W, H, _p(cam), float(delta), int(delta_flags),
                   taus.ctypes.data_as(_lib._d), len(taus), int(bool(normalized_by_diameter)),
@@ -221,7 +264,7 @@ class BatchEvaluator:
     union, inter, est bbox (x0, y0, x1, y1), gt bbox (empty: x1 = y1 = -1)."""
     n = slots.numel()
     out = self._out(n, 10) if out is None else out
-    self.ctx.call("bopx_cover_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt),
+    self._call("bopx_cover_batch_dev", n, _p(slots), _p(pose_est), _p(pose_gt),
                   _p(frame_idx), int(width), int(height), _p(cam), _p(out),
                   _stream(self.device))
     return out
@@ -236,7 +279,7 @@ class BatchEvaluator:
     H, W = int(frames.shape[-2]), int(frames.shape[-1])
     out = self._out(n, 11)
     mk = torch.empty((n, 2, H, W), dtype=torch.uint8, device=self.device) if masks else None
-    self.ctx.call("bopx_gt_info_batch_dev", n, _p(slots), _p(pose), _p(frame_idx), _p(frames),
+    self._call("bopx_gt_info_batch_dev", n, _p(slots), _p(pose), _p(frame_idx), _p(frames),
                   W, H, _p(cam), float(delta), int(delta_flags), int(canvas_scale), _p(out),
                   _p(mk), _stream(self.device))
     return out, mk
@@ -248,10 +291,10 @@ class BatchEvaluator:
       frames = torch.empty((n_frames, height, width), dtype=torch.float32, device=self.device)
     npx = frames.numel()
     s = _stream(self.device)
-    self.ctx.call("bopx_depth_clear_dev", _p(frames), npx, s)
-    self.ctx.call("bopx_render_depth_batch_dev", slots.numel(), _p(slots), _p(pose),
+    self._call("bopx_depth_clear_dev", _p(frames), npx, s)
+    self._call("bopx_render_depth_batch_dev", slots.numel(), _p(slots), _p(pose),
                   _p(frame_idx), _p(cam), _p(frames), width, height, s)
-    self.ctx.call("bopx_depth_finish_dev", _p(frames), npx, s)
+    self._call("bopx_depth_finish_dev", _p(frames), npx, s)
     return frames
 
   def bop19(self, slots, pose_est, pose_gt, K, frame_idx, frames, cam, delta, taus, diameters,

@@ -76,12 +76,27 @@ struct Parser {
     se = p++;
     return true;
   }
+  static bool hex(char c) {
+    return digit(c) || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F');
+  }
+  // a string member value that is skipped: JSON's escapes only (\" \\ \/ \b
+  // \f \n \r \t \uXXXX), as Python's json accepts them; anything else is
+  // declined (json raises on it). ADVICE r5.
   bool skip_string() {
     if (p >= e || *p != '"') return false;
     ++p;
     while (p < e && *p != '"') {
       if ((unsigned char)*p < 0x20) return false;
-      if (*p == '\\') ++p;
+      if (*p == '\\') {
+        if (++p >= e) return false;
+        const char c = *p;
+        if (c == 'u') {
+          if (e - p < 5 || !hex(p[1]) || !hex(p[2]) || !hex(p[3]) || !hex(p[4])) return false;
+          p += 4;
+        } else if (!std::strchr("\"\\/bfnrt", c) || c == 0) {
+          return false;
+        }
+      }
       ++p;
     }
     if (p >= e) return false;
@@ -173,8 +188,43 @@ struct Parser {
   }
 };
 
+// Well-formed UTF-8 (RFC 3629: shortest form, no surrogates, <= U+10FFFF):
+// the reference opens the file as text (inout.py:66-82), so other bytes raise
+// UnicodeDecodeError there; such a file is declined and Python raises it.
+bool utf8_ok(const unsigned char* s, const unsigned char* e) {
+  while (s < e) {
+    const unsigned c = *s;
+    if (c < 0x80) {
+      ++s;
+      continue;
+    }
+    int n;
+    unsigned lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) {
+      n = 1;
+    } else if (c >= 0xE0 && c <= 0xEF) {
+      n = 2;
+      if (c == 0xE0) lo = 0xA0;
+      if (c == 0xED) hi = 0x9F;
+    } else if (c >= 0xF0 && c <= 0xF4) {
+      n = 3;
+      if (c == 0xF0) lo = 0x90;
+      if (c == 0xF4) hi = 0x8F;
+    } else {
+      return false;
+    }
+    if (e - s <= n) return false;
+    if (s[1] < lo || s[1] > hi) return false;
+    for (int k = 2; k <= n; ++k)
+      if (s[k] < 0x80 || s[k] > 0xBF) return false;
+    s += n + 1;
+  }
+  return true;
+}
+
 bool parse(const char* data, size_t n, int nf, const char* const* names, const int* widths,
            Lists& L) {
+  if (!utf8_ok((const unsigned char*)data, (const unsigned char*)data + n)) return false;
   Parser P{data, data + n};
   std::vector<size_t> name_len(nf);
   for (int f = 0; f < nf; ++f) name_len[f] = std::strlen(names[f]);

@@ -725,6 +725,45 @@ int bopx_remove_object(bopx_ctx* c, int obj_id) {
   return sync_desc(c);
 }
 
+// The new sets are allocated and uploaded first and swapped in only when every
+// one of them is resident: a failure part-way (OOM, a copy error) frees the new
+// buffers and leaves every object's old set and the device descriptor table as
+// they were, so no later launch reads a freed buffer.
+static int replace_symmetries(bopx_ctx* c, int n, const int* slots, const int64_t* ns,
+                              const double* syms) {
+  std::vector<double*> fresh((size_t)n, nullptr);
+  auto drop = [&]() {
+    for (double* p : fresh)
+      if (p) (void)hipFree(p);
+  };
+  const double* src = syms;
+  for (int i = 0; i < n; ++i) {
+    const size_t count = 12 * (size_t)ns[i];
+    if (hipMalloc((void**)&fresh[(size_t)i], count * sizeof(double)) != hipSuccess) {
+      (void)hipGetLastError();
+      fresh[(size_t)i] = nullptr;
+      drop();
+      return fail(c, BOPX_E_OOM, "symmetry set allocation failed");
+    }
+    hipError_t e = hipMemcpyAsync(fresh[(size_t)i], src, count * sizeof(double),
+                                  hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipStreamSynchronize(c->stream);
+      drop();
+      return fail(c, BOPX_E_HIP, "symmetry upload: %s", hipGetErrorString(e));
+    }
+    src += count;
+  }
+  for (int i = 0; i < n; ++i) {  // every new set is resident: swap them in
+    Object& o = c->objs[(size_t)slots[i]];
+    if (o.d_syms) (void)hipFree(o.d_syms);  // no launch reads it (the stream was drained)
+    o.d_syms = fresh[(size_t)i];
+    o.ns = ns[i];
+  }
+  return sync_desc(c);  // one descriptor upload, then the stream is drained
+}
+
 int bopx_set_symmetries(bopx_ctx* c, int obj_id, const double* syms, int64_t ns) {
   if (!c) return BOPX_E_INVALID;
   int s;
@@ -732,14 +771,8 @@ int bopx_set_symmetries(bopx_ctx* c, int obj_id, const double* syms, int64_t ns)
     return fail(c, BOPX_E_NOT_FOUND, "unknown obj_id %d", obj_id);
   if (ns < 1 || !syms) return fail(c, BOPX_E_INVALID, "empty symmetry set");
   if (int r = set_dev(c)) return r;
-  Object& o = c->objs[s];
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (o.d_syms) HIPCHK(c, hipFree(o.d_syms));
-  o.d_syms = nullptr;
-  o.ns = 0;
-  if (int r = upload(c, &o.d_syms, syms, 12 * (size_t)ns)) return r;
-  o.ns = ns;
-  return sync_desc(c);
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // no launch still reads the old set
+  return replace_symmetries(c, 1, &s, &ns, syms);
 }
 
 int bopx_set_symmetries_many(bopx_ctx* c, int n, const int* obj_ids, const int64_t* ns,
@@ -755,24 +788,7 @@ int bopx_set_symmetries_many(bopx_ctx* c, int n, const int* obj_ids, const int64
   if (n == 0) return BOPX_OK;
   if (int r = set_dev(c)) return r;
   HIPCHK(c, hipStreamSynchronize(c->stream));  // no launch still reads the old sets
-  const double* src = syms;
-  for (int i = 0; i < n; ++i) {
-    Object& o = c->objs[(size_t)slots[(size_t)i]];
-    if (o.d_syms) HIPCHK(c, hipFree(o.d_syms));
-    o.d_syms = nullptr;
-    o.ns = 0;
-    const size_t count = 12 * (size_t)ns[i];
-    if (hipMalloc((void**)&o.d_syms, count * sizeof(double)) != hipSuccess) {
-      (void)hipGetLastError();
-      o.d_syms = nullptr;
-      return fail(c, BOPX_E_OOM, "object allocation failed");
-    }
-    HIPCHK(c, hipMemcpyAsync(o.d_syms, src, count * sizeof(double), hipMemcpyHostToDevice,
-                             c->stream));
-    o.ns = ns[i];
-    src += count;
-  }
-  return sync_desc(c);  // one descriptor upload, then the stream is drained
+  return replace_symmetries(c, n, slots.data(), ns, syms);
 }
 
 int bopx_preload(bopx_ctx* c) {

@@ -73,6 +73,23 @@ def depth_group_sizes():
   v = os.environ.get("BOPX_DEPTH_GROUP_FRAMES", "4096/1024").split("/")
   g = int(v[0])
   return g, (int(v[1]) if len(v) > 1 else g)
+
+
+def release_group_slice(groups, scene_id):
+  """Take a scene's slice of its decode group without using it (a scene with
+  no VSD tuples), so the group can be freed once its last scene is taken. The
+  frames are never read, so whatever the group failed with (a frame of another
+  size in another scene of the group, ...) is not this scene's error: the
+  reference reads every target image's depth (eval_calc_errors.py:238-243) but
+  uses it only per estimate, where a size mismatch would surface. The scenes
+  of the group that do use their frames still get the group's error (and fall
+  back to per-scene decoding on ValueError). ADVICE r5."""
+  try:
+    groups.get(scene_id)
+  except Exception:  # noqa: BLE001 - frames unused; the scenes that need them re-raise
+    pass
+
+
 ERROR_TYPES = ("vsd", "mssd", "mspd", "ad", "add", "adi", "cus", "proj", "rete", "re", "te")
 
 
@@ -985,7 +1002,7 @@ def run(p, device=0):
           vals, todo = plan_arrays(p, arr, models_info)
           depths = depth_ims = None
           if et == "vsd" and not len(todo) and groups is not None:
-            groups.get(scene_id)  # not needed: taken so that its group can be freed
+            release_group_slice(groups, scene_id)
           if et == "vsd" and len(todo):
             if groups is not None:
               try:

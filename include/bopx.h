@@ -97,7 +97,9 @@ int bopx_set_symmetries(bopx_ctx* ctx, int obj_id, const double* syms, int64_t n
 /* bopx_set_symmetries for n objects in one call (one stream synchronisation and
  * one descriptor upload instead of n): object obj_ids[i] gets the ns[i] rows
  * starting at row sum(ns[0..i-1]) of syms. Nothing changes when an obj_id is
- * unknown or an ns[i] < 1 (checked before any upload). */
+ * unknown or an ns[i] < 1 (checked before any upload), nor when an allocation
+ * or copy fails (the new sets are uploaded first and swapped in only when all
+ * are resident; the same holds for bopx_set_symmetries). */
 int bopx_set_symmetries_many(bopx_ctx* ctx, int n, const int* obj_ids, const int64_t* ns,
                              const double* syms);
 int bopx_object_slot(const bopx_ctx* ctx, int obj_id, int* slot);

@@ -145,3 +145,19 @@ def test_first_group_and_release_before_next_pack(fake_decoder, monkeypatch):
     for k in range(1, 6):
       assert len(g.get(k)) == 2
   assert [len(c) for c in fake_decoder] == [2, 6, 4]
+
+
+def test_unused_scene_slice_ignores_the_group_error(fake_decoder):
+  """a scene without VSD tuples takes its slice only so that its
+  group can be freed (eval_calc_errors.release_group_slice); the group's error
+  (another scene's frame of another size) must not stop the pass there, while
+  the scene that uses its frames still gets it, and the group is released."""
+  from bop_toolkit_amd import eval_calc_errors as ece
+  items = [_scene(0, 2), (1, lambda: (["bad:0"], [1.0])), _scene(2, 4), _scene(3, 4)]
+  with depth_gpu.GroupPrefetch(0, items, 4, 4, _fake_torch(), None, None, max_frames=3,
+                               max_groups=2) as g:
+    ece.release_group_slice(g, 0)  # no tuples in scene 0: the group's ValueError is not raised
+    with pytest.raises(ValueError):
+      g.get(1)  # the scene that needs the frames
+    assert len(g.get(2)) == 4  # the failed group was released: later groups still come
+    assert len(g.get(3)) == 4

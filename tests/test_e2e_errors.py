@@ -191,3 +191,45 @@ def test_caller_shared_oom_falls_back_to_fused(tmp_path, monkeypatch):
     ev.vsd_shared(ev.slots([1]), pose, z, z, z, torch.zeros((1, 480, 640), device=d),
                   torch.tensor([[572.0, 573.0, 320.0, 240.0]], dtype=torch.float64, device=d),
                   15.0, [0.05], torch.tensor([100.0], dtype=torch.float64, device=d))
+
+
+@pytest.mark.gpu
+def test_caller_scene_without_estimates_in_a_failing_group(tmp_path):
+  """a scene with targets but no estimates shares a depth-decode
+  group with a scene that has them, and the group fails (the estimate-free
+  scene's frames are of another size, a ValueError). The estimate-free scene
+  only releases its slice; the other scene falls back to per-scene decoding.
+  The reference never uses the estimate-free scene's depth
+  (eval_calc_errors.py:238-243, used per estimate only), so the pass must
+  finish: scene 2's files byte-identical to the reference's, scene 3's the
+  empty list save_json writes."""
+  import shutil
+  from PIL import Image
+  ds = tmp_path / "datasets"
+  shutil.copytree(os.path.join(E2E, "datasets"), str(ds))
+  lmo = ds / "lmo"
+  s3 = lmo / "test" / "000003"
+  shutil.copytree(str(lmo / "test" / "000002"), str(s3))
+  for f in sorted((s3 / "depth").iterdir()):
+    Image.fromarray(np.full((240, 320), 700, np.uint16)).save(str(f))  # another size
+  tp = lmo / "test_targets_bop19.json"
+  targets = json.load(open(str(tp)))
+  extra = [dict(t, scene_id=3) for t in targets if t["scene_id"] == 2]
+  inout.save_json(str(tp), extra + targets)  # scene 3 first: its release comes first
+  out = tmp_path / "eval"
+  p = ece.parse_args([
+      "--error_type", "vsd", "--n_top", "-1", "--result_filenames", RUNS["result"],
+      "--results_path", os.path.join(E2E, "results"), "--eval_path", str(out),
+      "--datasets_path", str(ds)])
+  written = ece.run(p, 0)
+  empty = tmp_path / "empty.json"
+  inout.save_json(str(empty), [])
+  n2 = 0
+  for path in written:
+    rel = os.path.relpath(path, os.path.join(str(out), "synth_lmo-test"))
+    if rel.endswith("errors_000003.json"):
+      assert _load(path)[0] == _load(str(empty))[0], rel
+      continue
+    n2 += 1
+    assert _load(path)[0] == _load(os.path.join(E2E, "expected", rel))[0], rel
+  assert n2 == len(p["vsd_taus"])

@@ -151,3 +151,40 @@ def test_arrays_path_matches_dict_path(tmp_path):
   assert n0 == n1
   for k in a0:
     assert np.array_equal(a0[k], a1[k]), k
+
+
+_GOOD_REC = '"cam_R_m2c": [1,2,3,4,5,6,7,8,9], "cam_t_m2c": [1,2,3], "obj_id": 1'
+
+
+@pytest.mark.parametrize("raw", [
+    ('{"1": [{%s, "x": "a\\qb"}]}' % _GOOD_REC).encode(),  # unknown escape
+    ('{"1": [{%s, "x": "a\\u12"}]}' % _GOOD_REC).encode(),  # short \u escape
+    ('{"1": [{%s, "x": "a\\u12G4"}]}' % _GOOD_REC).encode(),  # not hex
+    ('{"1": [{%s, "x": "a\\' % _GOOD_REC).encode(),  # escape at the end of the file
+    ('{"1": [{%s, "x": "' % _GOOD_REC).encode() + b'\xff"}]}',  # not UTF-8
+    ('{"1": [{%s, "x": "' % _GOOD_REC).encode() + b'\xc3"}]}',  # truncated sequence
+    ('{"1": [{%s, "x": "' % _GOOD_REC).encode() + b'\xed\xa0\x80"}]}',  # a surrogate
+    ('{"1": [{%s, "x": "' % _GOOD_REC).encode() + b'\xc0\xaf"}]}',  # overlong form
+])
+def test_declined_bad_strings(tmp_path, raw):
+  """text Python's json (as the reference opens it, inout.py:66-82)
+  refuses is declined, so the Python path raises the reference's error."""
+  import json
+  p = tmp_path / "scene_gt.json"
+  p.write_bytes(raw)
+  assert inout.load_scene_gt_lists(str(p)) is None
+  with pytest.raises(ValueError):  # JSONDecodeError and UnicodeDecodeError are ValueErrors
+    with open(str(p), "r", encoding="utf-8") as f:
+      json.load(f)
+
+
+@pytest.mark.parametrize("member", ['"a\\"b\\\\c\\/d\\b\\f\\n\\r\\t"', '"\\u00e9\\uD83D\\ude00"',
+                                    '"' + "é中\U0001f600" + '"'])
+def test_taken_escapes_and_utf8(tmp_path, member):
+  """Every JSON escape and well-formed multi-byte UTF-8 in a skipped member is
+  taken, with the same values as the json path."""
+  p = tmp_path / "scene_gt.json"
+  p.write_text('{"1": [{%s, "x": %s}], "2": []}' % (_GOOD_REC, member), encoding="utf-8")
+  g = inout.load_scene_gt_lists(str(p))
+  assert g is not None and g.im_ids.tolist() == [1, 2]
+  _check_gt(str(p))
