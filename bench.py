@@ -91,10 +91,13 @@ def parse():
                   help="object size factor (design experiments; 1 = the configuration's)")
   ap.add_argument("--cpu-seconds", type=float, default=10.0,
                   help="target wall time of the CPU-baseline sample")
-  ap.add_argument("--no-cpu-baseline", action="store_true")
+  ap.add_argument("--no-cpu-baseline", action="store_true",
+                  help="skip the oracle legs after the timed region (cpu_baseline and parity)")
+  ap.add_argument("--no-parity", action="store_true",
+                  help="skip the post-timed-region parity leg (every config vs the oracle)")
   ap.add_argument("--e2e-images", type=int, default=None,
                   help="images of the end-to-end drop-in run after the timed region (default "
-                       "4,002 for configs[3] at N=1, else 0 = none)")
+                       "16,667 = the whole configs[3] job at N=1, else 0 = none)")
   ap.add_argument("--seed", type=int, default=20250220 + 4)
   args = ap.parse_args()
   cfg = CONFIGS[args.config]
@@ -107,7 +110,7 @@ def parse():
   return args
 
 
-def build_objects(ev, args, torch):
+def build_objects(ev, args, torch, dia_device=None):
   from bop_toolkit_amd import misc, synth
   rng = np.random.default_rng(args.seed)
   objs = []
@@ -116,7 +119,8 @@ def build_objects(ev, args, torch):
     pts, faces = synth.superellipsoid(args.n_lat, args.n_lon, axes, float(rng.uniform(0.5, 1.0)))
     # exact diameter (max pairwise distance) on the host, in row chunks: set-up
     # only, kept off the GPU so the profile holds the measured kernels alone
-    p = torch.as_tensor(pts)
+    # (the parity leg, after the timed region, takes it on dia_device)
+    p = torch.as_tensor(pts, device=dia_device)
     dia = max(float(torch.cdist(p[i:i + 2048], p, compute_mode="donot_use_mm_for_euclid_dist").max())
               for i in range(0, len(p), 2048))
     info = {"diameter": dia}
@@ -494,7 +498,7 @@ def cpu_baseline(objs, d, n, seconds, gpu=None):
   return out
 
 
-def e2e_run(images, seed, timeout=420):
+def e2e_run(images, seed, timeout=300):
   """The drop-in evaluation end to end, after the timed region: a YCB-V-layout
   dataset of `images` 640x480 images with 6 of configs[3]'s kind of objects
   each (21 superellipsoids of 5,002 vertices, Pillow-written 16-bit depth
@@ -523,6 +527,159 @@ def e2e_run(images, seed, timeout=420):
                  "in a fresh process on PNG files on local disk; tuples/s = its tuples / its wall "
                  "time; calc_gt_info separate")
   return res
+
+
+# tuples per configuration in the parity leg (a few hundred of each workload)
+PARITY_TUPLES = {0: 100, 1: 600, 2: 300, 3: 300, 4: 240, 5: 300}
+PARITY_TOL = 1e-4  # north_star: within 1e-4 mm / 1e-4 px of the reference
+
+
+def _max_diff(a, b):
+  """(max abs, max rel) difference of two float64 vectors whose infinities
+  must coincide (gated / empty-set values); inf when they do not."""
+  a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+  fa, fb = np.isfinite(a), np.isfinite(b)
+  if not (np.array_equal(fa, fb) and np.array_equal(a[~fa], b[~fb])):
+    return float("inf"), float("inf")
+  if not fa.any():
+    return 0.0, 0.0
+  d = np.abs(a[fa] - b[fa])
+  return float(d.max()), float((d / np.maximum(np.abs(b[fa]), 1e-300)).max())
+
+
+def parity_leg(args, torch, skip=(), png_frames=None):
+  """After the timed region (rank 0, N = 1): a few hundred tuples of every
+  BASELINE.json configuration's own workload generator (build_objects /
+  build_workload / build_workload_multi with that configuration's objects,
+  camera and image size) through the HIP path, checked against the CPU oracle
+  (oracle/bopx_oracle.c, the checker): VSD rows bit-identical, MSSD / MSPD /
+  ADD / ADI within PARITY_TOL with matching infinities; then test-depth PNGs
+  (Pillow-written, several zlib levels) decoded by kern_png.hip vs Pillow, bit
+  for bit, with no frame left to the host decoder. `skip`: configurations
+  already checked by this run (cpu_baseline.check)."""
+  global W, H
+  import copy
+
+  from bop_toolkit_amd import synth
+  from bop_toolkit_amd.batch import BatchEvaluator
+  from oracle import oracle
+  t_all = time.perf_counter()
+  keep_wh = (W, H)
+  res, ok = {}, True
+  try:
+    for c in sorted(PARITY_TUPLES):
+      if c in skip:
+        continue
+      t0 = time.perf_counter()
+      cfg = CONFIGS[c]
+      a = copy.copy(args)
+      a.config, a.cfg, a.tuples, a.axes_scale = c, cfg, PARITY_TUPLES[c], 1.0
+      a.objects, a.n_lat, a.n_lon = cfg["objects"], cfg["n_lat"], cfg["n_lon"]
+      a.seed = 20250220 + 4
+      W, H = cfg["W"], cfg["H"]
+      ev = BatchEvaluator(0)
+      objs = build_objects(ev, a, torch, dia_device=ev.device)
+      multi = "multi" in cfg
+      n, d = (build_workload_multi if multi else build_workload)(ev, objs, a, 0, 1, torch)
+      h = d["host"]
+      errs = cfg["errors"]
+      got = {}
+      if "vsd" in errs:
+        rd = d.get("renders")
+        got["vsd"] = (ev.vsd_shared(rd["slots"], rd["pose"], rd["frame_idx"], rd["est"], rd["gt"],
+                                    d["frames"], d["cam"], DELTA, TAUS, d["diameters"]) if multi
+                      else ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"],
+                                  d["frames"], d["cam"], DELTA, TAUS, d["diameters"]))
+      if "mssd" in errs:
+        got["mssd"] = ev.mssd(d["slots"], d["pose_est"], d["pose_gt"])
+        got["mspd"] = ev.mspd(d["slots"], d["pose_est"], d["pose_gt"], d["K"])
+      if "add" in errs:
+        got["add"] = ev.add(d["slots"], d["pose_est"], d["pose_gt"])
+        got["adi"] = ev.adi(d["slots"], d["pose_est"], d["pose_gt"])
+      torch.cuda.synchronize()
+      got = {k: v.cpu().numpy() for k, v in got.items()}
+      t_gpu = time.perf_counter() - t0
+      want = {}
+      K = getattr(synth, cfg["K"])
+      if "vsd" in errs:
+        frames = d["frames"].cpu().numpy()
+        want["vsd"], mssd_o, mspd_o = oracle.bop19_batch(
+            objs, h["obj"], h["pe"], h["pg"], h["frame_idx"], frames, h["cam"], DELTA, TAUS,
+            np.array([objs[o]["diameter"] for o in h["obj"]]))
+        if "mssd" in errs:
+          want["mssd"], want["mspd"] = mssd_o, mspd_o
+        if c == 3 and png_frames is None:
+          png_frames = frames[:24]
+      elif "mssd" in errs:
+        want["mssd"] = np.array([oracle.mssd(objs[o]["pts"], objs[o]["syms"], h["pe"][i],
+                                             h["pg"][i]) for i, o in enumerate(h["obj"])])
+        want["mspd"] = np.array([oracle.mspd(objs[o]["pts"], objs[o]["syms"], h["pe"][i],
+                                             h["pg"][i], K) for i, o in enumerate(h["obj"])])
+      if "add" in errs:
+        want["add"] = np.array([oracle.add(objs[o]["pts"], h["pe"][i], h["pg"][i])
+                                for i, o in enumerate(h["obj"])])
+        want["adi"] = np.array([oracle.adi(objs[o]["pts"], h["pe"][i], h["pg"][i])
+                                for i, o in enumerate(h["obj"])])
+      row = {"tuples": int(n), "W": W, "H": H}
+      for k in got:
+        if k == "vsd":
+          same = int((got[k] == want[k]).all(1).sum())
+          row["vsd_rows_bit_identical"] = same
+          ok &= same == n
+        else:
+          mab, mrel = _max_diff(got[k], want[k])
+          row[k] = {"max_abs": mab, "max_rel": mrel}
+          ok &= mab < PARITY_TOL
+      row["s"] = round(time.perf_counter() - t0, 2)
+      row["gpu_s"] = round(t_gpu, 2)
+      res[str(c)] = row
+      del ev, d
+  finally:
+    W, H = keep_wh
+  png = None
+  if png_frames is not None:
+    png = png_check(png_frames, torch)
+    ok &= png["bit_identical"] == png["frames"] and png["device_decoded"] == png["frames"]
+  torch.cuda.empty_cache()
+  return {"configs": res, "png": png, "all_ok": bool(ok), "tol": PARITY_TOL,
+          "s": round(time.perf_counter() - t_all, 2),
+          "note": "HIP path vs the CPU oracle (oracle/bopx_oracle.c, the checker) on each "
+                  "BASELINE.json configuration's own generator (configs index as key; 5 = the "
+                  "multi-instance shared-render variant); VSD rows compared bit for bit, point "
+                  "errors by max abs / rel with matching infinities; png: kern_png.hip vs "
+                  "Pillow on 16-bit PNGs of configs[3] test depth"}
+
+
+def png_check(frames, torch):
+  """Test-depth frames (integer mm) written as 16-bit PNGs by Pillow at zlib
+  levels 0-9, decoded on the GPU (depth_gpu.DepthDecoder -> kern_png.hip) and
+  compared bit for bit with Pillow's decode x the depth scale (inout.py:39-46,
+  eval_calc_errors.py:242-243)."""
+  import shutil
+  import tempfile
+
+  from PIL import Image
+
+  from bop_toolkit_amd import depth_gpu
+  tmp = tempfile.mkdtemp(prefix="bopx_bench_png_")
+  try:
+    q = np.clip(np.round(frames), 0, 65535).astype(np.uint16)
+    n, Hh, Ww = q.shape
+    paths, scales = [], []
+    for i in range(n):
+      path = os.path.join(tmp, "%06d.png" % i)
+      Image.fromarray(q[i]).save(path, compress_level=i % 10)
+      paths.append(path)
+      scales.append(0.1 if i % 2 else 1.0)
+    dec = depth_gpu.DepthDecoder(0)
+    got = dec.load(paths, scales, Hh, Ww, torch).cpu().numpy()
+    want = np.stack([np.asarray(Image.open(p_)).astype(np.float32) * np.float32(s_)
+                     for p_, s_ in zip(paths, scales)])
+    same = int(sum(np.array_equal(got[i], want[i]) for i in range(n)))
+    return {"frames": n, "size": [Ww, Hh], "bit_identical": same,
+            "device_decoded": n - int(dec.last_host), "zlib_levels": "0-9"}
+  finally:
+    shutil.rmtree(tmp, ignore_errors=True)
 
 
 def cpu_baseline_point(objs, d, n):
@@ -709,9 +866,15 @@ def main():
       cpu = cpu_baseline(objs, d, n, args.cpu_seconds, (out_vsd, out_mssd, out_mspd))
     elif world == 1 and not args.no_cpu_baseline and args.cfg["errors"] == ("add", "adi"):
       cpu = cpu_baseline_point(objs, d, n)
+    parity = None
+    if world == 1 and not args.no_parity and not args.no_cpu_baseline:
+      # configurations this run already checked against the oracle (cpu_baseline.check)
+      done = (args.config,) if cpu is not None and "check" in cpu else ()
+      parity = parity_leg(args, torch, skip=done, png_frames=d["frames"][:24].cpu().numpy())
     e2e_images = args.e2e_images
     if e2e_images is None:
-      e2e_images = 4002 if args.config == 3 and world == 1 and "multi" not in args.cfg else 0
+      # the metric's whole job as a dataset on disk (16,667 images = 100,002 tuples)
+      e2e_images = 16667 if args.config == 3 and world == 1 and "multi" not in args.cfg else 0
     e2e = e2e_run(e2e_images, args.seed) if e2e_images > 0 and world == 1 else None
     line = {
         "metric": "pose-error tuples/sec (%s) at %dx%d, ~%dk-vert meshes" % (
@@ -731,7 +894,7 @@ def main():
                    "tuples_rank0": n,
                    "roi_mean_px": round(cost["roi_mean"], 1),
                    **({"axes_scale": args.axes_scale} if args.axes_scale != 1.0 else {})},
-        "roofline": roof, "kernels": kernels, "cpu_baseline": cpu, "e2e": e2e}
+        "roofline": roof, "kernels": kernels, "cpu_baseline": cpu, "parity": parity, "e2e": e2e}
     if multi:
       rd = d["renders"]
       if roof is not None and roof["kernel"] == "k_vsd":

@@ -116,3 +116,18 @@ def test_committed_pmc_matches_the_shipped_kernels(monkeypatch):
   n = (args.tuples + 5) // 6 * 6  # build_workload: whole images of 6 objects
   assert bench.load_traffic("vsd", args, n) is not None
   assert bench.load_traffic("mssd", args, n) is not None
+
+
+def test_parity_max_diff():
+  """bench._max_diff (the parity leg's point-error check): infinities must
+  coincide in place and sign, finite values compare by max abs / rel."""
+  import numpy as np
+  inf = float("inf")
+  assert bench._max_diff([1.0, inf], [1.0, inf]) == (0.0, 0.0)
+  assert bench._max_diff([1.0, inf], [1.0, 2.0]) == (inf, inf)
+  assert bench._max_diff([inf], [-inf]) == (inf, inf)
+  assert bench._max_diff([inf, inf], [inf, inf]) == (0.0, 0.0)
+  a, r = bench._max_diff(np.array([2.0, 4.0 + 1e-6]), np.array([2.0, 4.0]))
+  assert abs(a - 1e-6) < 1e-12 and abs(r - 2.5e-7) < 1e-12
+  assert set(bench.PARITY_TUPLES) == {0, 1, 2, 3, 4, 5}
+  assert all(c in bench.CONFIGS for c in bench.PARITY_TUPLES)

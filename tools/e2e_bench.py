@@ -42,9 +42,41 @@ def progress(msg):
 T_START = time.perf_counter()
 
 
-def make_dataset(root, n_im, seed, torch, inst=1):
+def _save_pngs(npy, jobs):
+  """Worker process: Pillow-encode the frames of `jobs` ((path, index) pairs)
+  from the memory-mapped uint16 array `npy` (Pillow's encoder holds the GIL,
+  so threads do not scale)."""
   from PIL import Image
-  from concurrent.futures import ThreadPoolExecutor
+  arr = np.load(npy, mmap_mode="r")
+  for path, i in jobs:
+    Image.fromarray(np.ascontiguousarray(arr[i])).save(path)
+  return len(jobs)
+
+
+def write_pngs(root, png, jobs, workers=16):
+  """The depth PNGs, Pillow-written by `workers` spawned processes (children
+  started with fork + exec, which this GPU-initialised process may do) from
+  a memory-mapped copy of the frames; progress every ~1,000 files."""
+  import multiprocessing as mp
+  from concurrent.futures import ProcessPoolExecutor, as_completed
+  npy = os.path.join(root, "frames_u16.npy")
+  np.save(npy, png)
+  chunk = 256
+  parts = [[(p, int(i)) for p, i in jobs[k:k + chunk]] for k in range(0, len(jobs), chunk)]
+  done = 0
+  try:
+    with ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("spawn")) as pool:
+      futs = [pool.submit(_save_pngs, npy, part) for part in parts]
+      for f in as_completed(futs):
+        k = f.result()
+        done += k
+        if done // 1000 != (done - k) // 1000:
+          progress("%d / %d PNGs written" % (done, len(jobs)))
+  finally:
+    os.remove(npy)
+
+
+def make_dataset(root, n_im, seed, torch, inst=1):
   from bop_toolkit_amd import inout, misc, synth
   from bop_toolkit_amd.batch import BatchEvaluator
   rng = np.random.default_rng(seed)
@@ -122,15 +154,8 @@ def make_dataset(root, n_im, seed, torch, inst=1):
       json.dump(cams, f)
     with open(os.path.join(sdir, "scene_gt.json"), "w") as f:
       json.dump(gts, f)
-  done = [0]
-
-  def save(j):
-    Image.fromarray(png[j[1]]).save(j[0])
-    done[0] += 1
-    if done[0] % 1000 == 0:
-      progress("%d / %d PNGs written" % (done[0], len(jobs)))
-  with ThreadPoolExecutor(16) as pool:
-    list(pool.map(save, jobs))
+  write_pngs(root, png, jobs)
+  del png
   with open(os.path.join(ds, "test_targets_bop19.json"), "w") as f:
     json.dump(targets, f)
   os.makedirs(os.path.join(root, "results"))
