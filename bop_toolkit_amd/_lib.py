@@ -13,7 +13,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BOPX_LIB", os.path.join(_HERE, "lib", "libbopx.so"))
 
-OK, E_INVALID, E_NOT_FOUND, E_HIP, E_OOM, E_UNSUPPORTED = 0, 1, 2, 3, 4, 5
+OK, E_INVALID, E_NOT_FOUND, E_HIP, E_OOM, E_UNSUPPORTED, E_INTERNAL = 0, 1, 2, 3, 4, 5, 6
 COST_STEP, COST_TLINEAR = 0, 1
 VISIB_BOP18, VISIB_BOP19 = 0, 1
 DELTA_F64 = 1

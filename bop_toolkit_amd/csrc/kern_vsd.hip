@@ -577,7 +577,17 @@ void k_vsd(VsdArgs a) {
   unsigned long long ph[16] = {}, t_prev = 0;
   if (VSD_DIAG(8)) t_prev = __builtin_amdgcn_s_memtime();
   const ObjDesc o = a.objs[a.slots[b]];
-  const int W = a.width, H = a.height, nm = o.nm;
+  // Capacity guard: this instantiation's entry queue and rectangle registers
+  // hold kListLen entries (launch_vsd_rpt_any picks RPT from the context's
+  // largest object; the host refuses to launch when that maximum is stale,
+  // runtime.cpp launch_dev). An object beyond them can only come from a
+  // descriptor table changed under a queued launch: the workgroup then runs
+  // with no meshlets (no queue / LDS index out of range) and writes NaN errors
+  // (render mode: no fragments). A select, not an early return: an extra exit
+  // costs this kernel 8 VGPRs and spills.
+  constexpr bool kOneP = COST == kCostGtInfo || COST == kCostRender;
+  const bool over = !kStream && (kOneP ? o.nm : 2 * o.nm) > kListLen;
+  const int W = a.width, H = a.height, nm = over ? 0 : o.nm;
   // Object arrays live in global memory: address-space-1 views give
   // global_load (vmcnt only) instead of flat_load for pointers read from memory.
   // vertex blocks are float32x4 at a 16-B stride; only x, y, z are loaded
@@ -1430,6 +1440,10 @@ void k_vsd(VsdArgs a) {
         }
         out[2 + k] = (double)v;
       }
+      if (over)  // capacity guard (above)
+        for (int k = 0; k < (S > 1 ? kVsdPartCols : COST == kCostCover ? kCoverCols : kGtInfoCols);
+             ++k)
+          out[k] = __builtin_nan("");
       return;
     }
     if (S > 1) {  // partial row of this split; k_vsd_combine applies the formula
@@ -1446,6 +1460,7 @@ void k_vsd(VsdArgs a) {
         row[2 + k] = (double)cnt;
         row[2 + kMaxTaus + k] = sum;
       }
+      if (over) row[0] = __builtin_nan("");  // k_vsd_combine: NaN union -> NaN errors
       return;
     }
     double* out = a.out + b * (int64_t)a.n_tau;
@@ -1462,7 +1477,9 @@ void k_vsd(VsdArgs a) {
         for (int w = 0; w < kVsdWaves; ++w) sum += s_lin[w][k];
         out[k] = (sum + (double)(un - in)) / (double)un;
       }
+      if (over) out[k] = __builtin_nan("");  // capacity guard (above)
     }
+    if (over && a.unions) a.unions[b] = __builtin_nan("");
   }
 }
 

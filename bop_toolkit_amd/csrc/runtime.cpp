@@ -89,6 +89,36 @@ int set_dev(bopx_ctx* c) {
   return BOPX_OK;
 }
 
+// Launch prologue: the device, then the registry invariant every kernel shape
+// relies on. The launchers size their per-workgroup state from the context's
+// maxima, not from the objects of the batch: k_vsd's instantiation (rectangle
+// registers and the LDS entry queue, RPT = ceil((1 or 2) x max_nm / 512)),
+// k_sym_error's unit layout (max_ns), k_adi's scratch stride (max_nv on the
+// device entry) and k_render_batch's (max_nf); the kernels read each object's
+// own counts from the device descriptor table. Both come from sync_desc, which
+// ends every registry change; if that failed part-way the maxima could lag a
+// live object, and a kernel sized from them would index past its LDS / scratch
+// (the class of the round-5 vertex-cache fault). So every launch
+// entry recomputes the maxima from the live objects and refuses to launch on a
+// mismatch (BOPX_E_INTERNAL), instead of launching out of range.
+int launch_dev(bopx_ctx* c) {
+  if (int r = set_dev(c)) return r;
+  int nf = 0, nv = 0, ns = 0, nm = 0;
+  for (const Object& o : c->objs)
+    if (o.live) {
+      nf = std::max(nf, (int)o.nf);
+      nv = std::max(nv, (int)o.nv);
+      ns = std::max(ns, (int)o.ns);
+      nm = std::max(nm, (int)o.nm);
+    }
+  if (nf != c->max_nf || nv != c->max_nv || ns != c->max_ns || nm != c->max_nm)
+    return fail(c, BOPX_E_INTERNAL,
+                "object registry maxima are stale (nf %d/%d nv %d/%d ns %d/%d nm %d/%d): a "
+                "registry update did not complete; re-register the objects",
+                nf, c->max_nf, nv, c->max_nv, ns, c->max_ns, nm, c->max_nm);
+  return BOPX_OK;
+}
+
 // *_dev calls run on exactly the stream they are given; NULL is the null
 // (default) stream, as for any HIP API -- never the context's private stream.
 hipStream_t pick_stream(bopx_ctx*, void* s) { return (hipStream_t)s; }
@@ -824,7 +854,7 @@ static int point_batch(bopx_ctx* c, int kind, int64_t n, const int32_t* obj_ids,
   if (!obj_ids || !pe || !pg || !out) return fail(c, BOPX_E_INVALID, "NULL buffer");
   const bool needK = kind == 1 || kind == 4;
   if (needK && !K) return fail(c, BOPX_E_INVALID, "K is NULL");
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   std::vector<int32_t> slots;
   if (int r = map_slots(c, n, obj_ids, slots, kind <= 1, false)) return r;
   const size_t bytes = carve_size({4 * (size_t)n, 96 * (size_t)n, 96 * (size_t)n,
@@ -899,7 +929,7 @@ int bopx_proj_batch(bopx_ctx* c, int64_t n, const int32_t* ids, const double* pe
 int bopx_mssd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
                         const double* pg, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   hipStream_t s = pick_stream(c, stream);
   LaunchOrder ord;
   const bopx::OrderCost sc = sym_order_cost(c);
@@ -911,7 +941,7 @@ int bopx_mssd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doub
 int bopx_mspd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
                         const double* pg, const double* K, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   hipStream_t s = pick_stream(c, stream);
   LaunchOrder ord;
   const bopx::OrderCost sc = sym_order_cost(c);
@@ -922,7 +952,7 @@ int bopx_mspd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doub
 int bopx_add_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
                        const double* pg, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   hipStream_t s = pick_stream(c, stream);
   LaunchOrder ord;
   if (int r = make_order(c, n, slots, s, ord)) return r;
@@ -932,7 +962,7 @@ int bopx_add_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doubl
 int bopx_adi_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
                        const double* pg, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   hipStream_t s = pick_stream(c, stream);
   LaunchOrder ord;
   if (int r = make_order(c, n, slots, s, ord)) return r;
@@ -943,7 +973,7 @@ int bopx_adi_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doubl
 int bopx_proj_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const double* pe,
                         const double* pg, const double* K, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   hipStream_t s = pick_stream(c, stream);
   LaunchOrder ord;
   if (int r = make_order(c, n, slots, s, ord)) return r;
@@ -1032,7 +1062,7 @@ int bopx_vsd_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const doubl
                        const double* taus, int n_tau, int normalized, const double* diameters,
                        int cost_type, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   bopx::VsdArgs a{};
   a.cull = vsd_cull_enabled();
   a.qorder = vsd_queue_order();
@@ -1076,7 +1106,7 @@ int bopx_vsd_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const double*
     if (frame_idx[i] < 0 || frame_idx[i] >= n_frames)
       return fail(c, BOPX_E_INVALID, "frame_idx[%lld] = %d out of range", (long long)i,
                   frame_idx[i]);
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   bopx::VsdArgs a{};
   a.cull = vsd_cull_enabled();
   a.qorder = vsd_queue_order();
@@ -1278,7 +1308,7 @@ int bopx_vsd_shared_batch_dev(bopx_ctx* c, int64_t n_renders, const int32_t* ren
                               double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
   if (n < 0 || n_renders < 0) return fail(c, BOPX_E_INVALID, "negative size");
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   return vsd_shared_core(c, n_renders, render_slots, render_poses, render_frame_idx, n,
                          est_render, gt_render, frames, width, height, cam, delta, flags, taus,
                          n_tau, normalized, diameters, cost_type, out, pick_stream(c, stream));
@@ -1309,7 +1339,7 @@ int bopx_vsd_shared_batch(bopx_ctx* c, int64_t n_renders, const int32_t* render_
       return fail(c, BOPX_E_INVALID, "tuple %lld: est and gt renders of different frames",
                   (long long)i);
   }
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   std::vector<int32_t> slots;
   if (int r = map_slots(c, n_renders, render_obj_ids, slots, false, true)) return r;
   const size_t fbytes = (size_t)n_frames * width * height * sizeof(float);
@@ -1385,7 +1415,7 @@ int bopx_gt_info_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const d
                            const double* cam, double delta, int flags, int canvas_scale,
                            double* out, uint8_t* masks, void* stream) {
   if (!c) return BOPX_E_INVALID;
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   bopx::VsdArgs a{};
   a.cull = vsd_cull_enabled();
   a.qorder = vsd_queue_order();
@@ -1427,7 +1457,7 @@ int bopx_gt_info_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const dou
     if (frame_idx[i] < 0 || frame_idx[i] >= n_frames)
       return fail(c, BOPX_E_INVALID, "frame_idx[%lld] = %d out of range", (long long)i,
                   frame_idx[i]);
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   bopx::VsdArgs a{};
   a.cull = vsd_cull_enabled();
   a.qorder = vsd_queue_order();
@@ -1483,7 +1513,7 @@ int bopx_cover_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, const dou
                          const double* pg, const int32_t* frame_idx, int width, int height,
                          const double* cam, double* out, void* stream) {
   if (!c) return BOPX_E_INVALID;
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   bopx::VsdArgs a{};
   a.cull = vsd_cull_enabled();
   a.qorder = vsd_queue_order();
@@ -1519,7 +1549,7 @@ int bopx_cover_batch(bopx_ctx* c, int64_t n, const int32_t* obj_ids, const doubl
     if (frame_idx[i] < 0 || frame_idx[i] >= n_frames)
       return fail(c, BOPX_E_INVALID, "frame_idx[%lld] = %d out of range", (long long)i,
                   frame_idx[i]);
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   bopx::VsdArgs a{};
   a.cull = vsd_cull_enabled();
   a.qorder = vsd_queue_order();
@@ -1684,7 +1714,7 @@ int bopx_render_depth_batch_dev(bopx_ctx* c, int64_t n, const int32_t* slots, co
                                 int width, int height, void* stream) {
   if (!c) return BOPX_E_INVALID;
   if (width <= 0 || height <= 0) return fail(c, BOPX_E_INVALID, "bad image size");
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   if (n <= 0 || c->max_nf <= 0) return BOPX_OK;
   HIPCHK(c, bopx::launch_render_batch(c->d_desc, c->max_nf, n, slots, pose, frame_idx, cam,
                                       frames, width, height, pick_stream(c, stream)));
@@ -1696,7 +1726,7 @@ int bopx_render_depth(bopx_ctx* c, int obj_id, const double* R, const double* t,
   if (!c) return BOPX_E_INVALID;
   if (!R || !t || !out) return fail(c, BOPX_E_INVALID, "NULL buffer");
   if (width <= 0 || height <= 0) return fail(c, BOPX_E_INVALID, "bad image size");
-  if (int r = set_dev(c)) return r;
+  if (int r = launch_dev(c)) return r;
   std::vector<int32_t> slots;
   int32_t id = obj_id;
   if (int r = map_slots(c, 1, &id, slots, false, true)) return r;

@@ -45,6 +45,8 @@ extern "C" {
 #define BOPX_E_HIP 3         /* HIP runtime error                              */
 #define BOPX_E_OOM 4         /* device allocation failed                       */
 #define BOPX_E_UNSUPPORTED 5 /* input outside the kernels' supported envelope  */
+#define BOPX_E_INTERNAL 6    /* object registry inconsistent (a registry update
+                                failed part-way): no kernel is launched        */
 
 /* VSD pixel matching cost (pose_error.py:82-88). */
 #define BOPX_COST_STEP 0

@@ -65,3 +65,16 @@ def test_io_library_exports_every_declared_symbol():
   assert os.path.exists(IO_LIB), "libbopx_io.so not built (make -C bop_toolkit_amd/csrc)"
   L = ctypes.CDLL(IO_LIB)
   assert not [s for s in syms if not hasattr(L, s)]
+
+
+def test_status_codes_match_header():
+  """The ctypes layer's status codes are the header's (BOPX_E_INTERNAL: a launch
+  refused because the object registry's maxima are stale, runtime.cpp
+  launch_dev)."""
+  import re
+  from bop_toolkit_amd import _lib
+  hdr = open(os.path.join(REPO, "include", "bopx.h")).read()
+  codes = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define BOPX_(OK|E_\w+) (\d+)", hdr)}
+  for name, v in codes.items():
+    assert getattr(_lib, name) == v, name
+  assert codes["E_INTERNAL"] == 6
