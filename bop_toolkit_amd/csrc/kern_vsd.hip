@@ -502,8 +502,8 @@ constexpr int kCullAutoMeshlets = 256;
 constexpr int kCullAutoDensity = 12;  // ... and at least this many meshlets per ROI tile
 
 // Each wave's first entry group of a tile is pre-assigned (no claim round trip
-// for it): -0.9 % (same-box A/B, round 2); the rest are claimed from s_next.
-constexpr int kVsdFirstClaim = kVsdWaves * kGroup;
+// for it): -0.9 % (same-box A/B, round 2); the rest are claimed from s_next,
+// which starts at NW * kGroup.
 
 // COST: 0 = step, 1 = tlinear, kCostCover = silhouette overlap, kCostGtInfo = GT stats.
 // NT (step cost): thresholds compared per pixel (>= n_tau; 10 for the BOP taus).
@@ -517,13 +517,16 @@ template <int COST, int RPT, int NT>
 // two workgroups per CU (4 waves per SIMD: VGPRs <= 128)
 __global__ __launch_bounds__(kVsdThreads, 2 * kVsdThreads / 256)
 void k_vsd(VsdArgs a) {
+  constexpr int NTH = kVsdThreads;  // threads of the workgroup
+  constexpr int NW = NTH / 64;      // its waves
+  constexpr int kPixPW = (kTileH + NW - 1) / NW * kTileW;   // pixel-list entries per wave
   // q = 1/Z bits, 0 = empty; rows padded by one dword so lanes that walk the
   // same column on consecutive rows (row-split) hit different LDS banks.
   __shared__ uint32_t s_dep[2][kTileStride * kTileH];
-  __shared__ __attribute__((aligned(16))) uint8_t s_wscr[kVsdWaves][kWaveScr];
-  __shared__ RRow s_rec[kVsdWaves][64];          // set-up triangles of the current chunk
+  __shared__ __attribute__((aligned(16))) uint8_t s_wscr[NW][kWaveScr];
+  __shared__ RRow s_rec[NW][64];          // set-up triangles of the current chunk
   // record start flags of a window of row items
-  __shared__ __attribute__((aligned(4))) uint8_t s_own[kVsdWaves][kRowWin];
+  __shared__ __attribute__((aligned(4))) uint8_t s_own[NW][kRowWin];
   // Tile entry queue. RPT <= 2 (objects of <= 512 meshlets): 32-bit words
   // entry | far << 11 | rectangle in the tile at 2-px granularity (x0/2, x1/2,
   // y0/2, y1/2: 5 bits each from bit 12) for the occlusion test; RPT 4: 16-bit
@@ -534,7 +537,7 @@ void k_vsd(VsdArgs a) {
   constexpr bool kStream = RPT == 0;
   constexpr int kR = kStream ? 4 : RPT;  // rectangles per thread and round
   constexpr bool kCull = RPT >= 1 && RPT <= 2;
-  constexpr int kListLen = kR * kVsdThreads;  // >= 2 * nm (launch_vsd) unless kStream
+  constexpr int kListLen = kR * NTH;  // >= 2 * nm (launch_vsd) unless kStream
   using ListT = typename std::conditional<kCull, uint32_t, uint16_t>::type;
   // list-ahead (objects of <= 256 meshlets, round 3: -0.8 %): two queues,
   // the next tile's listed by each wave in the current tile's raster tail
@@ -630,7 +633,7 @@ void k_vsd(VsdArgs a) {
     for (int q = 0; q < kQueues; ++q) {  // tile queue counters (reset again per tile)
       s_nlists[q] = 0;
       s_nsmalls[q] = 0;
-      s_nexts[q] = kVsdFirstClaim;
+      s_nexts[q] = (NW * kGroup);
     }
     s_roi[0] = s_roi[1] = 0x7FFFFFFF;
     s_roi[2] = s_roi[3] = -1;
@@ -667,7 +670,7 @@ void k_vsd(VsdArgs a) {
   for (int i0 = 0; i0 < (kStream ? 2 * nm : 1); i0 += kListLen)
 #pragma unroll
   for (int j = 0; j < kR; ++j) {
-    const int i = (kStream ? i0 : ebase) + tid + j * kVsdThreads;
+    const int i = (kStream ? i0 : ebase) + tid + j * NTH;
     rect[j] = make_short4(1, 1, 0, 0);
     zmin[j] = -INFINITY;
     qbv[j] = 0.0f;
@@ -736,7 +739,7 @@ void k_vsd(VsdArgs a) {
   // Both q tiles start at 0 once per tuple; afterwards the pixel pass zeroes
   // every pixel it reads (the only ones the raster can have written), so the
   // tiles are clean for the next tile without a separate clearing pass.
-  for (int i = tid; i < 2 * kTileStride * kTileH; i += kVsdThreads) (&s_dep[0][0])[i] = 0u;
+  for (int i = tid; i < 2 * kTileStride * kTileH; i += NTH) (&s_dep[0][0])[i] = 0u;
   __syncthreads();
   // render mode: the ROI its q buffer was sized for (launch_pose_roi, the same
   // rule), so every write lands inside the buffer
@@ -756,7 +759,7 @@ void k_vsd(VsdArgs a) {
   uint32_t far_bits = 0;
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
-    const int i = ebase + tid + j * kVsdThreads;
+    const int i = ebase + tid + j * NTH;
     const int r = i >= nm;
     const float zmid = 0.5f * (s_zr[r][0] + s_zr[r][1]);
     far_bits |= (uint32_t)(zmin[j] > zmid) << j;
@@ -768,7 +771,7 @@ void k_vsd(VsdArgs a) {
     far_bits = back_bits;
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
-      const int i = tid + j * kVsdThreads;
+      const int i = tid + j * NTH;
       if ((back_bits >> j) & 1u) {
         const float qhi = s_qhi[ebase + i >= nm];
         const float cf = floorf(64.0f * (__log2f(qhi) - __log2f(qbv[j])) - 0.05f);
@@ -789,7 +792,7 @@ void k_vsd(VsdArgs a) {
   // cover mode: est / gt silhouette bboxes (x0, y0, x1, y1), empty = (INT_MAX, INT_MAX, -1, -1)
   int bb[8] = {INT32_MAX, INT32_MAX, -1, -1, INT32_MAX, INT32_MAX, -1, -1};
   // step cost: two 16-bit per-tau counters per register (a lane evaluates at
-  // most kTileW * kTileH / kVsdThreads pixels per tile, <= kVsdMaxTiles tiles)
+  // most kTileW * kTileH / NTH pixels per tile, <= kVsdMaxTiles tiles)
   uint32_t c_tau[(NT + 1) / 2];
   double lin[kMaxTaus];
 #pragma unroll
@@ -813,7 +816,7 @@ void k_vsd(VsdArgs a) {
       for (int j = 0; j < kR; ++j) {
         short4 rc;
         if constexpr (kStream) {  // recomputed (round e0, entry e0 + tid + 512 j)
-          const int i = e0 + tid + j * kVsdThreads;
+          const int i = e0 + tid + j * NTH;
           rc = make_short4(1, 1, 0, 0);
           if (i < 2 * nm && !((COST == kCostGtInfo || COST == kCostRender) && i < nm)) {
             const int r = i >= nm, m = i - r * nm;
@@ -827,7 +830,7 @@ void k_vsd(VsdArgs a) {
         if (rc.x <= lx1 && rc.z >= lx0 && rc.y <= ly1 && rc.w >= ly0 && rc.x <= rc.z &&
             rc.y <= rc.w) {
           const uint32_t far = (far_bits >> j) & 1u;
-          ListT word = (ListT)(tid + j * kVsdThreads);
+          ListT word = (ListT)(tid + j * NTH);
           if constexpr (kCull) {
             const uint32_t x0 = (uint32_t)(max((int)rc.x, lx0) - lx0) >> 1;
             const uint32_t x1 = (uint32_t)(min((int)rc.z, lx1) - lx0) >> 1;
@@ -848,10 +851,11 @@ void k_vsd(VsdArgs a) {
         }
       }
     };
-    for (int t = sp, it = 0; t < ntx * nty; t += S, ++it) {
+    // 2b. one tile's raster into the q tile pair D, claims from queue qb
+    auto raster_tile = [&](const int t, const int it, const int qb,
+                           uint32_t(*const D)[kTileStride * kTileH]) {
       const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
       const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
-      const int qb = kAhead ? (it & 1) : 0;  // this tile's queue
       VSD_WAVE(11, 1);
       ListT* const s_list = s_lists[qb];
       int* const p_nlist = &s_nlists[qb];
@@ -867,7 +871,7 @@ void k_vsd(VsdArgs a) {
         if (tid == 0) {
           *p_nlist = 0;
           *p_nsmall = 0;
-          *p_next = kVsdFirstClaim;
+          *p_next = (NW * kGroup);
         }
         __syncthreads();
       }
@@ -895,7 +899,7 @@ void k_vsd(VsdArgs a) {
         VSD_STAMP(12);
         VSD_WAVE(0, 1);
         if (base >= nl) break;
-        if (base + kGroup * kVsdWaves >= nl) __builtin_amdgcn_s_setprio(kVsdPrio);
+        if (base + kGroup * NW >= nl) __builtin_amdgcn_s_setprio(kVsdPrio);
         f32x3 v[kGroup];
         uint32_t pk[kGroup];
         int pose[kGroup];
@@ -933,7 +937,7 @@ void k_vsd(VsdArgs a) {
                 const float qbd = s_qhi[pose[g]] *
                                   __builtin_amdgcn_exp2f(-(float)s_qb[ent[g]] * (1.0f / 64.0f));
                 const Region rg = make_region(word[g], tx1 - tx0 + 1, ty1 - ty0 + 1);
-                if (region_covered(s_dep[pose[g]], rg, 0, __float_as_uint(qbd), lane)) {
+                if (region_covered(D[pose[g]], rg, 0, __float_as_uint(qbd), lane)) {
                   dead |= 1u << g;
                   if (VSD_DIAG(4) && lane == 0) atomicAdd(&g_vsd_stats[9], 1ull);
                 }
@@ -964,7 +968,7 @@ void k_vsd(VsdArgs a) {
           if constexpr (kCull) {
             test[g] = (a.cull == 1 || a.cull == 2) && ((word[g] >> 11) & 1u) && base + g < nl;
             if (test[g])
-              qmin[g] = region_min8(s_dep[pose[g]],
+              qmin[g] = region_min8(D[pose[g]],
                                     make_region(word[g], tx1 - tx0 + 1, ty1 - ty0 + 1), 0, lane);
           }
         }
@@ -995,7 +999,7 @@ void k_vsd(VsdArgs a) {
               if (__builtin_amdgcn_ballot_w64(qmin[g] < qb) == 0) {
                 // first 8 blocks covered; a larger region continues from block 8
                 const Region rg = make_region(word[g], tx1 - tx0 + 1, ty1 - ty0 + 1);
-                if (rg.nb <= 8 || region_covered(s_dep[pose[g]], rg, 8, qb, lane)) {
+                if (rg.nb <= 8 || region_covered(D[pose[g]], rg, 8, qb, lane)) {
                   if (a.cull == 1) pk[g] = 0xFFFFFFFFu;  // no triangle of it can change the tile
                   if (VSD_DIAG(4) && lane == 0) atomicAdd(&g_vsd_stats[9], 1ull);
                 }
@@ -1071,7 +1075,7 @@ void k_vsd(VsdArgs a) {
 #endif
           }
           if (ok && !fast) {
-            uint32_t* dep = s_dep[r];
+            uint32_t* dep = D[r];
             r_raster(T, cc0, cc1, rr0, rr1, [&](int col, int row, float q) {
               if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], 1ull);
               atomicMax(&dep[(row - ty0) * kTileStride + (col - tx0)], __float_as_uint(q));
@@ -1136,9 +1140,9 @@ void k_vsd(VsdArgs a) {
                 }
                 const int fr =
                     VSD_DIAG(16) ? r_walk_row_max<true, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
-                                                        s_dep[(rec.meta >> 18) & 1u])
+                                                        D[(rec.meta >> 18) & 1u])
                                  : r_walk_row_max<false, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
-                                                  s_dep[(rec.meta >> 18) & 1u]);
+                                                  D[(rec.meta >> 18) & 1u]);
                 if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
               }
             }
@@ -1149,26 +1153,29 @@ void k_vsd(VsdArgs a) {
         wave_lds_sync();  // the staging area is rewritten by the next group
       }
       }  // rounds (kStream)
-      // list-ahead: this wave's share of the next tile's queue, while the other
-      // waves finish rasterising (the raster-end barrier below publishes it)
-      if constexpr (kAhead) {
-        if (t + S < ntx * nty) list_tile(t + S, qb ^ 1, 0);
-      }
+    };
+    auto touch_rows = [&](const int t) -> float {
       // Touch the test-depth lines of this wave's pixel rows (w, w + 8, ...)
       // while it waits for the other waves at the raster-end barrier: the
       // pixel pass then reads them from L2 instead of HBM. The empty asm below
       // consumes the value (the only wait for these loads).
-      // test depth of this tile: wave-uniform base, offsets < 64 rows x IW x 4 B
+      const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
+      const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
       const gptr<const float> tframe = frame + ((int64_t)ty0 * IW + tx0);
       float touch = 0.0f;
       if constexpr (COST == 0 || COST == 1) {
-        if (lane < 3 * (kTileH / kVsdWaves)) {
-          const int row = ty0 + wave + kVsdWaves * (lane / 3), k = lane % 3;
+        if (lane < 3 * (kTileH / NW)) {
+          const int row = ty0 + wave + NW * (lane / 3), k = lane % 3;
           const int col = k == 0 ? tx0 : (k == 1 ? min(tx0 + 32, tx1) : tx1);
           if (row <= ty1)
             touch = ld_off(tframe, (uint32_t)(__mul24(row - ty0, IW) + (col - tx0)) * 4u);
         }
       }
+      (void)ty1;
+      return touch;
+    };
+    auto coeffs = [&](const int t) {
+      const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
       // float64 distance coefficients of the tile's columns / rows (misc.py:137-138),
       // per wave into its scratch (its staging area is dead until the next
       // tile), computed before the raster-end barrier while other waves finish
@@ -1182,25 +1189,18 @@ void k_vsd(VsdArgs a) {
         w_pY[i] = pY;
         if constexpr (COST == 0) w_fB[i] = filt_b(pY);
       }
-      VSD_STAMP(2);
-      __syncthreads();
-      __builtin_amdgcn_s_setprio(0);
-      // every wave has read the queue counters (after the list barrier) and is
-      // done with s_next: reset them for the next tile (ordered by the
-      // pixel-end barrier)
-      if (kAhead && tid == 0) {
-        *p_nlist = 0;
-        *p_nsmall = 0;
-        *p_next = kVsdFirstClaim;
-      }
-      asm volatile("" ::"v"(touch));
-      VSD_STAMP(3);
+    };
+    // 3. one tile's pixel pass over the q tile pair D (this wave's rows)
+    auto pixel_tile = [&](const int t, uint32_t(*const D)[kTileStride * kTileH]) {
+      const int tx0 = rx0 + (t % ntx) * kTileW, ty0 = ry0 + (t / ntx) * kTileH;
+      const int tx1 = min(tx0 + kTileW - 1, rx1), ty1 = min(ty0 + kTileH - 1, ry1);
+      const gptr<const float> tframe = frame + ((int64_t)ty0 * IW + tx0);
       // 3. per-pixel distances, visibility masks, counters. Each wave first
       // compacts its covered pixels (rows wave, wave + 8, ...) into its own
       // list (ballot rank; the raster records are dead here), then evaluates
       // the list with full lanes. Wave-private: no block barrier, and the
       // pixel -> lane assignment is fixed (deterministic float64 sums).
-      uint16_t* pix = reinterpret_cast<uint16_t*>(&s_rec[0][0]) + wave * kPixPerWave;
+      uint16_t* pix = reinterpret_cast<uint16_t*>(&s_rec[0][0]) + wave * kPixPW;
       int npix = 0;
       {
         // lane = column, one wave-uniform tile row per step (rows w, w + 8, ...)
@@ -1210,11 +1210,11 @@ void k_vsd(VsdArgs a) {
         // column right of a tile cut by the ROI: the row walk may have written
         // it (r_walk_row_max); cleared here (wave-private rows, raster done)
         const int cut = tx1 - tx0 + 1;
-        VSD_WAVE(5, nrow > wave ? (nrow - wave + kVsdWaves - 1) / kVsdWaves : 0);
-        for (int r = wave; r < nrow; r += kVsdWaves) {
-          if (cut < kTileW && lane < 2) s_dep[lane][r * kTileStride + cut] = 0u;
+        VSD_WAVE(5, nrow > wave ? (nrow - wave + NW - 1) / NW : 0);
+        for (int r = wave; r < nrow; r += NW) {
+          if (cut < kTileW && lane < 2) D[lane][r * kTileStride + cut] = 0u;
           const int ps = r * kTileStride + lane;
-          const bool cov = col_in & ((s_dep[0][ps] | s_dep[1][ps]) != 0u);
+          const bool cov = col_in & ((D[0][ps] | D[1][ps]) != 0u);
           const unsigned long long bal = __ballot(cov);
           if constexpr (COST == kCostRender) {  // the row's covered column span
             if (bal != 0ull && lane == 0) {
@@ -1314,9 +1314,9 @@ void k_vsd(VsdArgs a) {
         const int p = pix[i];
         const int row = ty0 + p / kTileW, col = tx0 + p % kTileW;
         const int ps = (p / kTileW) * kTileStride + p % kTileW;
-        const uint32_t qe = s_dep[0][ps], qg = s_dep[1][ps];
-        s_dep[0][ps] = 0u;  // clean for the next tile (rows are wave-private here)
-        s_dep[1][ps] = 0u;
+        const uint32_t qe = D[0][ps], qg = D[1][ps];
+        D[0][ps] = 0u;  // clean for the next tile (rows are wave-private here)
+        D[1][ps] = 0u;
         if VSD_DIAG(4) atomicAdd(&g_vsd_stats[6], 1ull);
         if constexpr (COST == kCostRender) {  // the pose's q into its ROI buffer
           a.qbuf[a.qoff[b] + (int64_t)(row - ry0) * (rx1 - rx0 + 1) + (col - rx0)] = qg;
@@ -1367,6 +1367,38 @@ void k_vsd(VsdArgs a) {
         }
         if constexpr (COST == 0 || COST == 1) vsd_px(p, qe, qg, dt_of(p));
       }
+    };
+    for (int t = sp, it = 0; t < ntx * nty; t += S, ++it) {
+      const int qb = kAhead ? (it & 1) : 0;  // this tile's queue
+      raster_tile(t, it, qb, s_dep);
+      // list-ahead: this wave's share of the next tile's queue, while the other
+      // waves finish rasterising (the raster-end barrier below publishes it)
+      if constexpr (kAhead) {
+        if (t + S < ntx * nty) list_tile(t + S, qb ^ 1, 0);
+      }
+      // Touch the test-depth lines of this wave's pixel rows while it waits for
+      // the other waves at the raster-end barrier: the pixel pass then reads
+      // them from L2 instead of HBM. The empty asm below consumes the value
+      // (the only wait for these loads).
+      const float touch = touch_rows(t);
+      // float64 distance coefficients of the tile's columns / rows, per wave
+      // into its scratch (its staging area is dead until the next tile),
+      // computed before the raster-end barrier while other waves finish
+      coeffs(t);
+      VSD_STAMP(2);
+      __syncthreads();
+      __builtin_amdgcn_s_setprio(0);
+      // every wave has read the queue counters (after the list barrier) and is
+      // done with s_next: reset them for the next tile (ordered by the
+      // pixel-end barrier)
+      if (kAhead && tid == 0) {
+        s_nlists[qb] = 0;
+        s_nsmalls[qb] = 0;
+        s_nexts[qb] = NW * kGroup;
+      }
+      asm volatile("" ::"v"(touch));
+      VSD_STAMP(3);
+      pixel_tile(t, s_dep);
       VSD_STAMP(4);
       __syncthreads();
       VSD_STAMP(5);
@@ -1416,7 +1448,7 @@ void k_vsd(VsdArgs a) {
     for (int k = 0; k < 16; ++k) atomicAdd(&g_vsd_time[k], ph[k]);
   if (tid == 0) {
     uint64_t un = 0, in = 0;
-    for (int w = 0; w < kVsdWaves; ++w) {
+    for (int w = 0; w < NW; ++w) {
       un += s_cnt[w][0];
       in += s_cnt[w][1];
     }
@@ -1429,12 +1461,12 @@ void k_vsd(VsdArgs a) {
       out[1] = (double)in;
       if (COST == kCostGtInfo) {
         uint64_t valid = 0;
-        for (int w = 0; w < kVsdWaves; ++w) valid += s_cnt[w][10];
+        for (int w = 0; w < NW; ++w) valid += s_cnt[w][10];
         out[10] = (double)valid;
       }
       for (int k = 0; k < 8; ++k) {
         int v = (int)s_cnt[0][2 + k];
-        for (int w = 1; w < kVsdWaves; ++w) {
+        for (int w = 1; w < NW; ++w) {
           const int o = (int)s_cnt[w][2 + k];
           v = (k & 2) ? max(v, o) : min(v, o);
         }
@@ -1453,7 +1485,7 @@ void k_vsd(VsdArgs a) {
       for (int k = 0; k < a.n_tau; ++k) {
         uint64_t cnt = 0;
         double sum = 0.0;
-        for (int w = 0; w < kVsdWaves; ++w) {
+        for (int w = 0; w < NW; ++w) {
           cnt += s_cnt[w][2 + k];
           sum += s_lin[w][k];
         }
@@ -1470,11 +1502,11 @@ void k_vsd(VsdArgs a) {
         out[k] = 1.0;
       } else if (COST == 0) {
         uint64_t cnt = 0;
-        for (int w = 0; w < kVsdWaves; ++w) cnt += s_cnt[w][2 + k];
+        for (int w = 0; w < NW; ++w) cnt += s_cnt[w][2 + k];
         out[k] = (double)(cnt + (un - in)) / (double)un;
       } else {
         double sum = 0.0;
-        for (int w = 0; w < kVsdWaves; ++w) sum += s_lin[w][k];
+        for (int w = 0; w < NW; ++w) sum += s_lin[w][k];
         out[k] = (sum + (double)(un - in)) / (double)un;
       }
       if (over) out[k] = __builtin_nan("");  // capacity guard (above)

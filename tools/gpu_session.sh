@@ -7,9 +7,10 @@
 #   BENCH=1      bench.py $BENCH_ARGS -> gpurun_out/bench_$TAG.json
 #   PROFILE=1    rocprofv3 --kernel-trace --stats of the bench (no oracle legs)
 #   PMC=1        the PMC passes of tools/pmc.sh -> gpurun_out/${TAG}_pmc.json
-#   AB="a b .."  interleaved A/B of libraries (paths relative to the repo) on
-#                bench.py $AB_ARGS, REPS rounds -> gpurun_out/ab_$TAG.txt
-#   EXTRA="cmd"  one more command (its own limit: EXTRA_LIMIT seconds)
+#   EXTRA="cmd"  one more command (its own limit: EXTRA_LIMIT seconds), before AB
+#   AB="a b .."  interleaved A/B of libraries (paths relative to the repo; an
+#                arm LIB:VAR=VAL,.. also sets that environment) on bench.py
+#                $AB_ARGS, REPS rounds -> gpurun_out/ab_$TAG.txt
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${TAG:-r06}
@@ -34,17 +35,20 @@ if [ -n "$PMC" ]; then
   TAG=$TAG bash tools/pmc.sh "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" > gpurun_out/pmc_$TAG.log 2>&1 || fail pmc gpurun_out/pmc_$TAG.log
   tail -5 gpurun_out/pmc_$TAG.log
 fi
-if [ -n "$AB" ]; then
-  : > gpurun_out/ab_$TAG.txt
-  for rep in $(seq ${REPS:-3}); do
-    for lib in $AB; do
-      BOPX_LIB=$PWD/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --e2e-images 0 ${AB_ARGS:---steps 5 --warmup 1} > gpurun_out/ab_one.json 2> gpurun_out/ab_one.err || fail "ab $lib" gpurun_out/ab_one.err
-      python -c "import json,sys;d=json.load(open('gpurun_out/ab_one.json'));k=d['kernels'];print('%-40s rep %s %s value %.0f'%(sys.argv[1],sys.argv[2],' '.join('%s %.3f'%(n,v['ms']) for n,v in k.items() if isinstance(v,dict) and 'ms' in v),d['value']))" $lib $rep | tee -a gpurun_out/ab_$TAG.txt
-    done
-  done
-fi
 if [ -n "$EXTRA" ]; then
   timeout -k 10 ${EXTRA_LIMIT:-600} bash -c "$EXTRA" > gpurun_out/extra_$TAG.log 2>&1 || fail extra gpurun_out/extra_$TAG.log
   tail -20 gpurun_out/extra_$TAG.log
+fi
+if [ -n "$AB" ]; then
+  : > gpurun_out/ab_$TAG.txt
+  for rep in $(seq ${REPS:-3}); do
+    for arm in $AB; do
+      # an arm: LIB or LIB:VAR=VALUE[,VAR=VALUE...] (environment of that arm)
+      lib=${arm%%:*}; envs=""
+      [ "$arm" != "$lib" ] && envs=$(echo "${arm#*:}" | tr ',' ' ')
+      env $envs BOPX_LIB=$PWD/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --e2e-images 0 ${AB_ARGS:---steps 5 --warmup 1} > gpurun_out/ab_one.json 2> gpurun_out/ab_one.err || fail "ab $arm" gpurun_out/ab_one.err
+      python -c "import json,sys;d=json.load(open('gpurun_out/ab_one.json'));k=d['kernels'];print('%-50s rep %s %s value %.0f'%(sys.argv[1],sys.argv[2],' '.join('%s %.3f'%(n,v['ms']) for n,v in k.items() if isinstance(v,dict) and 'ms' in v),d['value']))" $arm $rep | tee -a gpurun_out/ab_$TAG.txt
+    done
+  done
 fi
 echo "session $TAG done"
