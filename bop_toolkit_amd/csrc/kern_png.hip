@@ -384,43 +384,26 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
       if (nb <= 32 && !refill_word()) return kErr;  // nb in (32, 64]
       const int lim = min(nb, 63);  // chain offsets stay lane indices
       const uint32_t ev = S.lit[(uint32_t)(bb >> lane) & ((1 << kLitRoot) - 1)];
-      // The chain from offset 0 by pointer jumping (round 6), in VALU and
-      // ds_bpermute instead of a serial v_readlane walk in SALU (the inflate is
-      // bound by scalar issue, one scalar unit per CU for its 16 streams):
-      // J0[l] = the offset after the step at l (l itself where the chain stops:
-      // no literal step, or one whose codes end past the valid bits), J(i+1) =
-      // Ji o Ji; lane k then finds the k-th chain offset pos_k = J0^k(0) from
-      // the binary digits of k (chains are at most 63 steps: a step takes a bit
-      // at least). Offsets only grow until the stop, a fixed point, so the steps
-      // are the lanes k with pos_k != pos_63 = off.
-      // (digit i of k and the doubling J(i+1) both need only Ji: their two
-      // ds_bpermute go out together, seven round trips in all)
-      const int st = (int)((ev >> 24) & kStop);
-      int j = st == (int)kStop || lane + st > lim ? lane : lane + st;  // J0
-      int pos = 0;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const int t = __builtin_amdgcn_ds_bpermute(pos << 2, j);        // Ji(pos)
-        const int jj = i < 5 ? __builtin_amdgcn_ds_bpermute(j << 2, j) : 0;  // J(i+1)
-        pos = (lane >> i) & 1 ? t : pos;
-        j = jj;
+      int off = 0;
+      uint64_t run = 0;  // bit l: a chain step (one or two literals) starts at offset l
+      int e = __builtin_amdgcn_readlane((int)ev, 0);
+      for (int nxt = (e >> 24) & (int)kStop; nxt <= lim; nxt = off + ((e >> 24) & (int)kStop)) {
+        run |= 1ull << off;
+        off = nxt;
+        e = __builtin_amdgcn_readlane((int)ev, off);
       }
-      const int off = __builtin_amdgcn_readlane(pos, 63);
-      int e = __builtin_amdgcn_readlane((int)ev, off);  // the entry the chain stops at
-      const uint64_t steps = __builtin_amdgcn_ballot_w64(pos != off);  // lanes 0 .. K - 1
-      if (steps) {
-        // step k's entry (one literal, or two: bit 31)
-        const uint32_t ek = (uint32_t)__builtin_amdgcn_ds_bpermute(pos << 2, (int)ev);
-        const bool on = (steps >> lane) & 1;
-        const uint64_t two = __builtin_amdgcn_ballot_w64(on && (int)ek < 0);
-        const int nlit = __popcll(steps) + __popcll(two);
+      if (run) {
+        const bool on = (run >> lane) & 1;
+        // chain steps with two literals (entries with bit 31 set, on the chain)
+        const uint64_t run2 = run & __builtin_amdgcn_ballot_w64((int)ev < 0);
+        const int nlit = __popcll(run) + __popcll(run2);
         if (nlit > out_n - p) return kErr;
         bb >>= off;  // off <= 63
         nb -= off;
         if (on) {
-          const int q = p + lane + popc_lt(two);
-          S.ring[q & kRingMask] = (uint8_t)(ek >> 4);
-          if ((int)ek < 0) S.ring[(q + 1) & kRingMask] = (uint8_t)(ek >> 16);
+          const int q = p + popc_lt(run) + popc_lt(run2);
+          S.ring[q & kRingMask] = (uint8_t)(ev >> 4);
+          if ((int)ev < 0) S.ring[(q + 1) & kRingMask] = (uint8_t)(ev >> 16);
         }
         p += nlit;
         while (p - flushed >= kFlush) {
