@@ -372,6 +372,8 @@ def launch_ranks(cmd, n, base_env=None, poll=0.2):
         live.remove(p)
         if r != 0 and rc == 0:
           rc = r if r > 0 else 128 - r
+          print("bench.py: rank %d exited with status %d; stopping the other %d rank(s)" %
+                (procs.index(p), r, len(live)), file=sys.stderr, flush=True)
           for q in live:
             q.terminate()
   finally:
@@ -717,10 +719,14 @@ def main():
     local %= torch.cuda.device_count()
   torch.cuda.set_device(local)
   if world > 1:
+    # a rank that dies leaves the others in a collective: bounded, so they fail
+    # loudly (RCCL / gloo timeout error) instead of hanging to the caller's limit
+    from datetime import timedelta
+    tmo = timedelta(seconds=float(os.environ.get("BOPX_DIST_TIMEOUT_S", "300")))
     if backend == "nccl":
-      dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+      dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
     else:
-      dist.init_process_group(backend)
+      dist.init_process_group(backend, timeout=tmo)
   from bop_toolkit_amd import shard
   from bop_toolkit_amd.batch import BatchEvaluator
   ev = BatchEvaluator(local)

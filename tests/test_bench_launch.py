@@ -52,6 +52,15 @@ def test_launch_ranks_failure_stops_the_others(tmp_path):
   assert rc == 3
 
 
+def test_launch_ranks_failure_is_reported(tmp_path, capfd):
+  """A failing rank is named on stderr with its status."""
+  code = ("import os, sys, time\nif os.environ['RANK'] == '2': sys.exit(5)\ntime.sleep(60)")
+  rc = bench.launch_ranks([sys.executable, "-c", code], 3, poll=0.02)
+  assert rc == 5
+  err = capfd.readouterr().err
+  assert "rank 2 exited with status 5; stopping the other 2 rank(s)" in err
+
+
 def test_gloo_bench_flow_two_ranks_launch(tmp_path):
   """The launcher path of main(): --gpus 2 without WORLD_SIZE starts two
   processes of the same command (here with a stub for the rank body)."""
