@@ -484,7 +484,13 @@ def cpu_baseline(objs, d, n, seconds, gpu=None):
     t1, (ov, om, op) = run(m)
   out = {"value": m / t1, "unit": "tuples/s", "cores": threads, "kind": "port",
          "sample": "%d tuples (first %d of this rank's workload), BOP19 set, %.1f s wall; "
-                   "oracle/bopx_oracle.c, reference per-tuple algorithm in C" % (m, m, t1)}
+                   "oracle/bopx_oracle.c, reference per-tuple algorithm in C" % (m, m, t1),
+         # the reference itself cannot travel to the GPU box; its own NumPy path was
+         # timed in the survey container
+         "reference_survey": {"value": 79.0, "unit": "tuples/s/core",
+                              "note": "reference NumPy path (pose_error.py), full BOP19 tuple "
+                                      "V=5k S=8 excluding the raster (no OpenGL offline), 1 "
+                                      "Xeon core of the survey container, BASELINE.md §2"}}
   if gpu is not None:
     gv, gm, gp = (t[:m].cpu().numpy() for t in gpu)
 
