@@ -566,88 +566,34 @@ def parity_leg(args, torch, skip=(), png_frames=None):
   for bit, with no frame left to the host decoder. `skip`: configurations
   already checked by this run (cpu_baseline.check)."""
   global W, H
-  import copy
-
   from bop_toolkit_amd import synth
   from bop_toolkit_amd.batch import BatchEvaluator
   from oracle import oracle
   t_all = time.perf_counter()
   keep_wh = (W, H)
   res, ok = {}, True
+  png_src = [png_frames]
   try:
     for c in sorted(PARITY_TUPLES):
       if c in skip:
         continue
-      t0 = time.perf_counter()
-      cfg = CONFIGS[c]
-      a = copy.copy(args)
-      a.config, a.cfg, a.tuples, a.axes_scale = c, cfg, PARITY_TUPLES[c], 1.0
-      a.objects, a.n_lat, a.n_lon = cfg["objects"], cfg["n_lat"], cfg["n_lon"]
-      a.seed = 20250220 + 4
-      W, H = cfg["W"], cfg["H"]
-      ev = BatchEvaluator(0)
-      objs = build_objects(ev, a, torch, dia_device=ev.device)
-      multi = "multi" in cfg
-      n, d = (build_workload_multi if multi else build_workload)(ev, objs, a, 0, 1, torch)
-      h = d["host"]
-      errs = cfg["errors"]
-      got = {}
-      if "vsd" in errs:
-        rd = d.get("renders")
-        got["vsd"] = (ev.vsd_shared(rd["slots"], rd["pose"], rd["frame_idx"], rd["est"], rd["gt"],
-                                    d["frames"], d["cam"], DELTA, TAUS, d["diameters"]) if multi
-                      else ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"],
-                                  d["frames"], d["cam"], DELTA, TAUS, d["diameters"]))
-      if "mssd" in errs:
-        got["mssd"] = ev.mssd(d["slots"], d["pose_est"], d["pose_gt"])
-        got["mspd"] = ev.mspd(d["slots"], d["pose_est"], d["pose_gt"], d["K"])
-      if "add" in errs:
-        got["add"] = ev.add(d["slots"], d["pose_est"], d["pose_gt"])
-        got["adi"] = ev.adi(d["slots"], d["pose_est"], d["pose_gt"])
-      torch.cuda.synchronize()
-      got = {k: v.cpu().numpy() for k, v in got.items()}
-      t_gpu = time.perf_counter() - t0
-      want = {}
-      K = getattr(synth, cfg["K"])
-      if "vsd" in errs:
-        frames = d["frames"].cpu().numpy()
-        want["vsd"], mssd_o, mspd_o = oracle.bop19_batch(
-            objs, h["obj"], h["pe"], h["pg"], h["frame_idx"], frames, h["cam"], DELTA, TAUS,
-            np.array([objs[o]["diameter"] for o in h["obj"]]))
-        if "mssd" in errs:
-          want["mssd"], want["mspd"] = mssd_o, mspd_o
-        if c == 3 and png_frames is None:
-          png_frames = frames[:24]
-      elif "mssd" in errs:
-        want["mssd"] = np.array([oracle.mssd(objs[o]["pts"], objs[o]["syms"], h["pe"][i],
-                                             h["pg"][i]) for i, o in enumerate(h["obj"])])
-        want["mspd"] = np.array([oracle.mspd(objs[o]["pts"], objs[o]["syms"], h["pe"][i],
-                                             h["pg"][i], K) for i, o in enumerate(h["obj"])])
-      if "add" in errs:
-        want["add"] = np.array([oracle.add(objs[o]["pts"], h["pe"][i], h["pg"][i])
-                                for i, o in enumerate(h["obj"])])
-        want["adi"] = np.array([oracle.adi(objs[o]["pts"], h["pe"][i], h["pg"][i])
-                                for i, o in enumerate(h["obj"])])
-      row = {"tuples": int(n), "W": W, "H": H}
-      for k in got:
-        if k == "vsd":
-          same = int((got[k] == want[k]).all(1).sum())
-          row["vsd_rows_bit_identical"] = same
-          ok &= same == n
-        else:
-          mab, mrel = _max_diff(got[k], want[k])
-          row[k] = {"max_abs": mab, "max_rel": mrel}
-          ok &= mab < PARITY_TOL
-      row["s"] = round(time.perf_counter() - t0, 2)
-      row["gpu_s"] = round(t_gpu, 2)
-      res[str(c)] = row
-      del ev, d
+      try:
+        ok &= parity_config(c, args, torch, oracle, synth, BatchEvaluator, res, png_src)
+      except Exception as e:  # noqa: BLE001 - reported in the line, the bench line still prints
+        res[str(c)] = {"error": repr(e)[:300]}
+        ok = False
+      torch.cuda.empty_cache()
   finally:
     W, H = keep_wh
+  png_frames = png_src[0]
   png = None
   if png_frames is not None:
-    png = png_check(png_frames, torch)
-    ok &= png["bit_identical"] == png["frames"] and png["device_decoded"] == png["frames"]
+    try:
+      png = png_check(png_frames, torch)
+      ok &= png["bit_identical"] == png["frames"] and png["device_decoded"] == png["frames"]
+    except Exception as e:  # noqa: BLE001
+      png = {"error": repr(e)[:300]}
+      ok = False
   torch.cuda.empty_cache()
   return {"configs": res, "png": png, "all_ok": bool(ok), "tol": PARITY_TOL,
           "s": round(time.perf_counter() - t_all, 2),
@@ -656,6 +602,80 @@ def parity_leg(args, torch, skip=(), png_frames=None):
                   "multi-instance shared-render variant); VSD rows compared bit for bit, point "
                   "errors by max abs / rel with matching infinities; png: kern_png.hip vs "
                   "Pillow on 16-bit PNGs of configs[3] test depth"}
+
+
+def parity_config(c, args, torch, oracle, synth, BatchEvaluator, res, png_src):
+  """One configuration of the parity leg (parity_leg); records its row in res
+  and returns whether it passed (png_src: [frames or None], filled from
+  configs[3] when the caller has no test depth for the PNG check)."""
+  global W, H
+  import copy
+  t0 = time.perf_counter()
+  ok = True
+  cfg = CONFIGS[c]
+  a = copy.copy(args)
+  a.config, a.cfg, a.tuples, a.axes_scale = c, cfg, PARITY_TUPLES[c], 1.0
+  a.objects, a.n_lat, a.n_lon = cfg["objects"], cfg["n_lat"], cfg["n_lon"]
+  a.seed = 20250220 + 4
+  W, H = cfg["W"], cfg["H"]
+  ev = BatchEvaluator(0)
+  objs = build_objects(ev, a, torch, dia_device=ev.device)
+  multi = "multi" in cfg
+  n, d = (build_workload_multi if multi else build_workload)(ev, objs, a, 0, 1, torch)
+  h = d["host"]
+  errs = cfg["errors"]
+  got = {}
+  if "vsd" in errs:
+    rd = d.get("renders")
+    got["vsd"] = (ev.vsd_shared(rd["slots"], rd["pose"], rd["frame_idx"], rd["est"], rd["gt"],
+                                d["frames"], d["cam"], DELTA, TAUS, d["diameters"]) if multi
+                  else ev.vsd(d["slots"], d["pose_est"], d["pose_gt"], d["frame_idx"],
+                              d["frames"], d["cam"], DELTA, TAUS, d["diameters"]))
+  if "mssd" in errs:
+    got["mssd"] = ev.mssd(d["slots"], d["pose_est"], d["pose_gt"])
+    got["mspd"] = ev.mspd(d["slots"], d["pose_est"], d["pose_gt"], d["K"])
+  if "add" in errs:
+    got["add"] = ev.add(d["slots"], d["pose_est"], d["pose_gt"])
+    got["adi"] = ev.adi(d["slots"], d["pose_est"], d["pose_gt"])
+  torch.cuda.synchronize()
+  got = {k: v.cpu().numpy() for k, v in got.items()}
+  t_gpu = time.perf_counter() - t0
+  want = {}
+  K = getattr(synth, cfg["K"])
+  if "vsd" in errs:
+    frames = d["frames"].cpu().numpy()
+    want["vsd"], mssd_o, mspd_o = oracle.bop19_batch(
+        objs, h["obj"], h["pe"], h["pg"], h["frame_idx"], frames, h["cam"], DELTA, TAUS,
+        np.array([objs[o]["diameter"] for o in h["obj"]]))
+    if "mssd" in errs:
+      want["mssd"], want["mspd"] = mssd_o, mspd_o
+    if c == 3 and png_src[0] is None:
+      png_src[0] = frames[:24]
+  elif "mssd" in errs:
+    want["mssd"] = np.array([oracle.mssd(objs[o]["pts"], objs[o]["syms"], h["pe"][i],
+                                         h["pg"][i]) for i, o in enumerate(h["obj"])])
+    want["mspd"] = np.array([oracle.mspd(objs[o]["pts"], objs[o]["syms"], h["pe"][i],
+                                         h["pg"][i], K) for i, o in enumerate(h["obj"])])
+  if "add" in errs:
+    want["add"] = np.array([oracle.add(objs[o]["pts"], h["pe"][i], h["pg"][i])
+                            for i, o in enumerate(h["obj"])])
+    want["adi"] = np.array([oracle.adi(objs[o]["pts"], h["pe"][i], h["pg"][i])
+                            for i, o in enumerate(h["obj"])])
+  row = {"tuples": int(n), "W": W, "H": H}
+  for k in got:
+    if k == "vsd":
+      same = int((got[k] == want[k]).all(1).sum())
+      row["vsd_rows_bit_identical"] = same
+      ok &= same == n
+    else:
+      mab, mrel = _max_diff(got[k], want[k])
+      row[k] = {"max_abs": mab, "max_rel": mrel}
+      ok &= mab < PARITY_TOL
+  row["s"] = round(time.perf_counter() - t0, 2)
+  row["gpu_s"] = round(t_gpu, 2)
+  res[str(c)] = row
+  del ev, d
+  return ok
 
 
 def png_check(frames, torch):

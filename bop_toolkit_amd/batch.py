@@ -51,8 +51,10 @@ def _join_preload(t, box):
 
 @atexit.register
 def _join_preloads():
+  # bounded: loading code objects takes milliseconds; a preload that does not
+  # return is left to the daemon thread rather than holding the exit
   for t in list(_PRELOADS):
-    t.join()
+    t.join(timeout=60)
 
 
 class BatchEvaluator:

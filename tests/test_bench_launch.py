@@ -140,3 +140,23 @@ def test_parity_max_diff():
   assert abs(a - 1e-6) < 1e-12 and abs(r - 2.5e-7) < 1e-12
   assert set(bench.PARITY_TUPLES) == {0, 1, 2, 3, 4, 5}
   assert all(c in bench.CONFIGS for c in bench.PARITY_TUPLES)
+
+
+def test_parity_leg_survives_a_failing_configuration(monkeypatch):
+  """A configuration whose parity run raises is reported in its row and turns
+  all_ok off; the other configurations still run and the line still prints."""
+  import torch
+  calls = []
+
+  def fake(c, args, torch_, oracle, synth, ev_cls, res, png_src):
+    calls.append(c)
+    if c == 2:
+      raise RuntimeError("boom")
+    res[str(c)] = {"tuples": 1}
+    return True
+  monkeypatch.setattr(bench, "parity_config", fake)
+  monkeypatch.setattr(torch.cuda, "empty_cache", lambda: None)
+  out = bench.parity_leg(object(), torch, skip=(3,))
+  assert calls == [0, 1, 2, 4, 5]
+  assert out["all_ok"] is False and "boom" in out["configs"]["2"]["error"]
+  assert out["configs"]["4"] == {"tuples": 1} and out["png"] is None
