@@ -772,6 +772,7 @@ static int replace_symmetries(bopx_ctx* c, int n, const int* slots, const int64_
     if (hipMalloc((void**)&fresh[(size_t)i], count * sizeof(double)) != hipSuccess) {
       (void)hipGetLastError();
       fresh[(size_t)i] = nullptr;
+      (void)hipStreamSynchronize(c->stream);  // earlier copies into `fresh` have landed
       drop();
       return fail(c, BOPX_E_OOM, "symmetry set allocation failed");
     }
