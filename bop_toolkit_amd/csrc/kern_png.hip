@@ -203,30 +203,34 @@ __device__ __forceinline__ int slow_index(uint64_t bb, int lim, int base, int la
 // 1024)). Returns 0 or kErr; *adler = the stream's Adler-32 field.
 __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, int in_n, uint8_t* __restrict__ out,
                               int out_n, InfLds& S, int lane, uint32_t* adler) {
-  // input: 1 KB chunks, words [base, base + 256) in four VGPRs, lane l
-  // holding words base + l + 64 k in component k (four coalesced dword loads),
-  // read with v_readlane from `cw`, the component of the current 64 words (a
-  // copy every 64 words instead of a four-way branch per word). The next chunk
-  // is loaded when the current one is used up (one load latency per KB of
-  // input; a prefetch into a loop-carried register makes the compiler copy it,
-  // and the copy waits for the load anyway)
+  // input: 1 KB chunks, words [256 (seg >> 2), + 256) in four VGPRs, lane l
+  // holding word 64 k + l of the chunk in component k (four coalesced dword
+  // loads), read with v_readlane from `cw`, the component of the current 64
+  // words (segment seg; a copy every 64 words instead of a four-way branch per
+  // word). The next chunk is loaded when the current one is used up (one load
+  // latency per KB of input; a prefetch into a loop-carried register makes the
+  // compiler copy it, and the copy waits for the load anyway). The next word
+  // is 64 seg + li. Reads past the stream are caught once per segment (the
+  // readable padding is 2048 bytes) and exactly by the final check: a stream
+  // whose bits end inside its bytes never loads a word past in_n + 8 (the bit
+  // buffer holds <= 64 bits).
   const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
   const int in_chunks = (in_n + 2048) >> 10;  // 1 KB chunks inside the readable bytes
   uint32_t c0 = in32[lane], c1 = in32[64 + lane], c2 = in32[128 + lane], c3 = in32[192 + lane];
   uint32_t cw = c0;
-  int base = 0;
-  int wi = 0;  // next input word
+  int seg = 0, li = 0;
   uint64_t bb = 0;
   int nb = 0;
   int p = 0, flushed = 0;
 
   auto refill_word = [&]() __attribute__((always_inline)) -> bool {
-    int i = wi - base;
-    if (__builtin_expect((i & 63) == 0 && i != 0, 0)) {  // the next 64 words
-      if (i >= 256) {
-        base += 256;
-        i = 0;
-        const int ch = min(base >> 8, max(in_chunks - 1, 0));
+    if (__builtin_expect(li == 64, 0)) {  // the next 64 words
+      ++seg;
+      li = 0;
+      if (seg * 256 > in_n + 8) return false;  // past the stream
+      const int sc = seg & 3;
+      if (sc == 0) {
+        const int ch = min(seg >> 2, max(in_chunks - 1, 0));
         const uint32_t* w32 = in32 + ch * 256;
         c0 = w32[lane];
         c1 = w32[64 + lane];
@@ -237,14 +241,14 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
         // values, not lvalues: a conditional over the captured variables would
         // select their addresses and put them in scratch
         const uint32_t v1 = c1, v2 = c2, v3 = c3;
-        cw = i == 64 ? v1 : (i == 128 ? v2 : v3);
+        cw = sc == 1 ? v1 : (sc == 2 ? v2 : v3);
       }
     }
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cw, i & 63);
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cw, li);
     bb |= (uint64_t)w << nb;
     nb += 32;
-    ++wi;
-    return wi * 4 <= in_n + 8;
+    ++li;
+    return true;
   };
   auto refill = [&]() __attribute__((always_inline)) -> bool { return nb > 32 || refill_word(); };
   auto flush_block = [&](int f) __attribute__((always_inline)) {
@@ -505,7 +509,7 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
     if (!refill()) return kErr;
     *adler = __builtin_bswap32((uint32_t)bb);
     nb -= 32;
-    if (wi * 4 - nb / 8 > in_n) return kErr;  // the stream ran past its bytes
+    if ((64 * seg + li) * 4 - nb / 8 > in_n) return kErr;  // the stream ran past its bytes
   }
   return 0;
 }
