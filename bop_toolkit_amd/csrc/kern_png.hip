@@ -60,7 +60,7 @@ struct InfLds {
   uint16_t dist[1 << kDistRoot];
   uint16_t sorted[288 + 32];      // symbols by code: literal/length, then distance
   uint8_t lens[288 + 32];         // code lengths: literal/length, then distance
-  alignas(16) uint8_t ring[kRing];  // the latest kRing output bytes
+  alignas(16) uint8_t ring[kRing + 64];  // the latest kRing output bytes; a spare byte per lane
 };
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -392,7 +392,7 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
       uint64_t run = 0;  // bit l: a chain step (one or two literals) starts at offset l
       int e = __builtin_amdgcn_readlane((int)ev, 0);
       for (int nxt = (e >> 24) & (int)kStop; nxt <= lim; nxt = off + ((e >> 24) & (int)kStop)) {
-        run |= 1ull << off;
+        asm("s_bitset1_b64 %0, %1" : "+s"(run) : "s"(off));  // run |= 1 << off, one instruction
         off = nxt;
         e = __builtin_amdgcn_readlane((int)ev, off);
       }
@@ -401,15 +401,15 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
         // chain steps with two literals (entries with bit 31 set, on the chain)
         const uint64_t run2 = run & __builtin_amdgcn_ballot_w64((int)ev < 0);
         const int nlit = __popcll(run) + __popcll(run2);
-        if (nlit > out_n - p) return kErr;
         bb >>= off;  // off <= 63
         nb -= off;
-        if (on) {
-          const int q = p + popc_lt(run) + popc_lt(run2);
-          S.ring[q & kRingMask] = (uint8_t)(ev >> 4);
-          if ((int)ev < 0) S.ring[(q + 1) & kRingMask] = (uint8_t)(ev >> 16);
-        }
+        // every lane stores (no exec mask to set up): the lanes off the chain,
+        // and the second byte of one-literal steps, into the lane's spare byte
+        const int q = p + popc_lt(run) + popc_lt(run2);
+        S.ring[on ? q & kRingMask : kRing + lane] = (uint8_t)(ev >> 4);
+        S.ring[on && (int)ev < 0 ? (q + 1) & kRingMask : kRing + lane] = (uint8_t)(ev >> 16);
         p += nlit;
+        if (p > out_n) return kErr;
         while (p - flushed >= kFlush) {
           flush_block(flushed);
           flushed += kFlush;
