@@ -223,11 +223,15 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
   int nb = 0;
   int p = 0, flushed = 0;
 
+  // over: a segment past the stream was entered. Sticky, and checked where a
+  // loop iteration makes no output (block headers, the slow symbol path) and
+  // at the end, so the literal windows carry no exit for it.
+  bool over = false;
   auto refill_word = [&]() __attribute__((always_inline)) -> bool {
     if (__builtin_expect(li == 64, 0)) {  // the next 64 words
       ++seg;
       li = 0;
-      if (seg * 256 > in_n + 8) return false;  // past the stream
+      over |= seg * 256 > in_n + 8;  // past the stream
       const int sc = seg & 3;
       if (sc == 0) {
         const int ch = min(seg >> 2, max(in_chunks - 1, 0));
@@ -248,9 +252,12 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
     bb |= (uint64_t)w << nb;
     nb += 32;
     ++li;
-    return true;
+    return !over;
   };
-  auto refill = [&]() __attribute__((always_inline)) -> bool { return nb > 32 || refill_word(); };
+  auto refill = [&]() __attribute__((always_inline)) -> bool {
+    if (nb <= 32) refill_word();
+    return !over;
+  };
   auto flush_block = [&](int f) __attribute__((always_inline)) {
     wave_sync();
     const uint4 v = reinterpret_cast<const uint4*>(S.ring)[((f & kRingMask) >> 4) + lane];
@@ -384,8 +391,10 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
       // is taken while its code(s) end inside the buffer's nb valid bits: the
       // bits above nb are zero, and a code that reaches past them cannot match
       // a shorter entry (prefix-free), so its entry's step ends past nb too.
-      if (nb <= 32 && !refill_word()) return kErr;
-      if (nb <= 32 && !refill_word()) return kErr;  // nb in (32, 64]
+      if (nb <= 32) {  // to nb in (32, 64]; a read past the stream is caught below
+        refill_word();
+        if (nb <= 32) refill_word();
+      }
       const int lim = min(nb, 63);  // chain offsets stay lane indices
       const uint32_t ev = S.lit[(uint32_t)(bb >> lane) & ((1 << kLitRoot) - 1)];
       int off = 0;
@@ -418,7 +427,8 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
       if (((e >> 24) & (int)kStop) != (int)kStop) continue;  // a literal past the window
       // not a literal with a short code: its entry again, from valid bits (a
       // long code plus length extra bits need up to 20)
-      if (nb <= 32 && !refill_word()) return kErr;
+      if (nb <= 32) refill_word();
+      if (over) return kErr;
       e = uni((int)(S.lit[(uint32_t)bb & ((1 << kLitRoot) - 1)] & 0xFFFFu));
       int L = e & 15, sym = e >> 4;
       if (e == kNoCode) {
@@ -509,7 +519,7 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
     if (!refill()) return kErr;
     *adler = __builtin_bswap32((uint32_t)bb);
     nb -= 32;
-    if ((64 * seg + li) * 4 - nb / 8 > in_n) return kErr;  // the stream ran past its bytes
+    if (over || (64 * seg + li) * 4 - nb / 8 > in_n) return kErr;  // the stream ran past its bytes
   }
   return 0;
 }
