@@ -396,7 +396,8 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
         if (nb <= 32) refill_word();
       }
       const int lim = min(nb, 63);  // chain offsets stay lane indices
-      const uint32_t ev = S.lit[(uint32_t)(bb >> lane) & ((1 << kLitRoot) - 1)];
+      const uint32_t bits = (uint32_t)(bb >> lane);
+      uint32_t ev = S.lit[bits & ((1 << kLitRoot) - 1)];
       int off = 0;
       uint64_t run = 0;  // bit l: a chain step (one or two literals) starts at offset l
       int e = __builtin_amdgcn_readlane((int)ev, 0);
@@ -405,18 +406,49 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
         off = nxt;
         e = __builtin_amdgcn_readlane((int)ev, off);
       }
+      if (__builtin_expect((e & 0xFFFF) == (int)kNoCode, 0) && off + 15 <= nb) {
+        // The chain stopped at a code longer than the root: decode the long
+        // codes at every offset with 15 valid bits lane-parallel (canonical,
+        // from the per-length limits of lanes 11-15, then `sorted`), make the
+        // literals among them chain steps, and follow the chain on.
+        const int m11 = __builtin_amdgcn_readlane(lit_lim, 11), m12 = __builtin_amdgcn_readlane(lit_lim, 12),
+                  m13 = __builtin_amdgcn_readlane(lit_lim, 13), m14 = __builtin_amdgcn_readlane(lit_lim, 14),
+                  m15 = __builtin_amdgcn_readlane(lit_lim, 15);
+        const int b11 = __builtin_amdgcn_readlane(lit_base, 11), b12 = __builtin_amdgcn_readlane(lit_base, 12),
+                  b13 = __builtin_amdgcn_readlane(lit_base, 13), b14 = __builtin_amdgcn_readlane(lit_base, 14),
+                  b15 = __builtin_amdgcn_readlane(lit_base, 15);
+        const int r15 = (int)(__builtin_bitreverse32(bits) >> 17);
+        const int L = 11 + (r15 >= m11) + (r15 >= m12) + (r15 >= m13) + (r15 >= m14) + (r15 >= m15);
+        const int bs = L <= 12 ? (L == 11 ? b11 : b12) : L <= 14 ? (L == 13 ? b13 : b14) : b15;
+        const bool cand = (ev & 0xFFFFu) == kNoCode && lane + 15 <= nb && L <= 15;
+        const int sym = S.sorted[cand ? bs + (r15 >> (15 - L)) : 0];
+        if (cand && sym < 256) ev = (uint32_t)L << 24 | (uint32_t)sym << 4 | (uint32_t)L;
+        e = __builtin_amdgcn_readlane((int)ev, off);
+        for (int nxt = off + ((e >> 24) & (int)kStop); nxt <= lim;
+             nxt = off + ((e >> 24) & (int)kStop)) {
+          asm("s_bitset1_b64 %0, %1" : "+s"(run) : "s"(off));
+          off = nxt;
+          e = __builtin_amdgcn_readlane((int)ev, off);
+        }
+      }
       if (run) {
-        const bool on = (run >> lane) & 1;
         // chain steps with two literals (entries with bit 31 set, on the chain)
         const uint64_t run2 = run & __builtin_amdgcn_ballot_w64((int)ev < 0);
         const int nlit = __popcll(run) + __popcll(run2);
         bb >>= off;  // off <= 63
         nb -= off;
         // every lane stores (no exec mask to set up): the lanes off the chain,
-        // and the second byte of one-literal steps, into the lane's spare byte
+        // and the second byte of one-literal steps, into the lane's spare byte;
+        // the step masks pick the address per lane as v_cndmask conditions
         const int q = p + popc_lt(run) + popc_lt(run2);
-        S.ring[on ? q & kRingMask : kRing + lane] = (uint8_t)(ev >> 4);
-        S.ring[on && (int)ev < 0 ? (q + 1) & kRingMask : kRing + lane] = (uint8_t)(ev >> 16);
+        const uint32_t spare = (uint32_t)(kRing + lane);
+        uint32_t a1, a2;
+        asm("v_cndmask_b32_e64 %0, %1, %2, %3"
+            : "=v"(a1) : "v"(spare), "v"((uint32_t)(q & kRingMask)), "s"(run));
+        asm("v_cndmask_b32_e64 %0, %1, %2, %3"
+            : "=v"(a2) : "v"(spare), "v"((uint32_t)((q + 1) & kRingMask)), "s"(run2));
+        S.ring[a1] = (uint8_t)(ev >> 4);
+        S.ring[a2] = (uint8_t)(ev >> 16);
         p += nlit;
         if (p > out_n) return kErr;
         while (p - flushed >= kFlush) {
@@ -425,6 +457,9 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
         }
       }
       if (((e >> 24) & (int)kStop) != (int)kStop) continue;  // a literal past the window
+      // a long code too close to the window's end: the next window starts at it
+      // (one with 15 valid bits is a length / end-of-block code or none)
+      if ((e & 0xFFFF) == (int)kNoCode && off + 15 > nb) continue;
       // not a literal with a short code: its entry again, from valid bits (a
       // long code plus length extra bits need up to 20)
       if (nb <= 32) refill_word();
