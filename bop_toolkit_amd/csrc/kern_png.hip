@@ -383,6 +383,9 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
     if (dst < 0) return kErr;
     const bool no_dist = dst == 1;
 
+    // errors leave the symbol loop by the same exit as the end-of-block code
+    // (one exit besides the back edges: no per-window exit dispatch)
+    bool err = false;
     for (;;) {  // symbols of this block
       // Literal runs, a bit-buffer window at a time: lane l looks the table up
       // at bit offset l (one LDS gather), the chain of short literal codes
@@ -450,7 +453,7 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
         S.ring[a1] = (uint8_t)(ev >> 4);
         S.ring[a2] = (uint8_t)(ev >> 16);
         p += nlit;
-        if (p > out_n) return kErr;
+        if (p > out_n) { err = true; break; }
         while (p - flushed >= kFlush) {
           flush_block(flushed);
           flushed += kFlush;
@@ -463,23 +466,23 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
       // not a literal with a short code: its entry again, from valid bits (a
       // long code plus length extra bits need up to 20)
       if (nb <= 32) refill_word();
-      if (over) return kErr;
+      if (over) { err = true; break; }
       e = uni((int)(S.lit[(uint32_t)bb & ((1 << kLitRoot) - 1)] & 0xFFFFu));
       int L = e & 15, sym = e >> 4;
       if (e == kNoCode) {
         const int idx = slow_index<kLitRoot>(bb, lit_lim, lit_base, lane, L);
-        if (idx < 0) return kErr;
+        if (idx < 0) { err = true; break; }
         sym = uni(S.sorted[idx]);
       }
       bb >>= L;
       nb -= L;
       if (sym < 256) {
-        if (p >= out_n) return kErr;
+        if (p >= out_n) { err = true; break; }
         put(sym);
         continue;
       }
       if (sym == 256) break;
-      if (sym > 285 || no_dist) return kErr;
+      if (sym > 285 || no_dist) { err = true; break; }
       // length: base and extra bits of RFC 1951 3.2.5 in closed form
       const int ls = sym - 257;
       const int lx = ls < 8 || ls == 28 ? 0 : (ls >> 2) - 1;
@@ -487,24 +490,24 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
       const int len = lbase + (int)(bb & ((1u << lx) - 1));
       bb >>= lx;
       nb -= lx;
-      if (!refill()) return kErr;
+      if (!refill()) { err = true; break; }
       e = uni(S.dist[bb & ((1 << kDistRoot) - 1)]);
       L = e & 15;
       int ds = e >> 4;
       if (e == kNoCode) {
         const int idx = slow_index<kDistRoot>(bb, dist_lim, dist_base, lane, L);
-        if (idx < 0) return kErr;
+        if (idx < 0) { err = true; break; }
         ds = uni(S.sorted[288 + idx]);
       }
       bb >>= L;
       nb -= L;
-      if (ds >= 30) return kErr;
+      if (ds >= 30) { err = true; break; }
       const int dx = ds < 4 ? 0 : (ds >> 1) - 1;
       const int dbase = ds < 4 ? ds + 1 : ((2 + (ds & 1)) << dx) + 1;
       const int dist = dbase + (int)(bb & ((1u << dx) - 1));
       bb >>= dx;
       nb -= dx;
-      if (dist > p || len > out_n - p) return kErr;
+      if (dist > p || len > out_n - p) { err = true; break; }
       // copy: byte i of the match = out[p - dist + i % dist]; sources all lie
       // before p, so each 64-byte round reads, then writes. Rounds before r0
       // wrote ring slots p .. p + r0 - 1, which hold the sources q with
@@ -544,6 +547,7 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
         flushed += kFlush;
       }
     }
+    if (err) return kErr;
   }
   if (p != out_n) return kErr;
   if (p > flushed) flush_block(flushed);  // the tail (the buffer is padded to 1 KB)
