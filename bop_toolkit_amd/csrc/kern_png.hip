@@ -403,12 +403,15 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
       uint32_t ev = S.lit[bits & ((1 << kLitRoot) - 1)];
       int off = 0;
       uint64_t run = 0;  // bit l: a chain step (one or two literals) starts at offset l
-      int e = __builtin_amdgcn_readlane((int)ev, 0);
-      for (int nxt = (e >> 24) & (int)kStop; nxt <= lim; nxt = off + ((e >> 24) & (int)kStop)) {
+      // lane l: the offset after the step that starts at l (> 63 at a stop),
+      // so a chain step is one v_readlane and one compare
+      int jv = lane + (int)((ev >> 24) & kStop);
+      for (int nxt = __builtin_amdgcn_readlane(jv, 0); nxt <= lim;
+           nxt = __builtin_amdgcn_readlane(jv, off)) {
         asm("s_bitset1_b64 %0, %1" : "+s"(run) : "s"(off));  // run |= 1 << off, one instruction
         off = nxt;
-        e = __builtin_amdgcn_readlane((int)ev, off);
       }
+      int e = __builtin_amdgcn_readlane((int)ev, off);
       if (__builtin_expect((e & 0xFFFF) == (int)kNoCode, 0) && off + 15 <= nb) {
         // The chain stopped at a code longer than the root: decode the long
         // codes at every offset with 15 valid bits lane-parallel (canonical,
@@ -425,14 +428,16 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
         const int bs = L <= 12 ? (L == 11 ? b11 : b12) : L <= 14 ? (L == 13 ? b13 : b14) : b15;
         const bool cand = (ev & 0xFFFFu) == kNoCode && lane + 15 <= nb && L <= 15;
         const int sym = S.sorted[cand ? bs + (r15 >> (15 - L)) : 0];
-        if (cand && sym < 256) ev = (uint32_t)L << 24 | (uint32_t)sym << 4 | (uint32_t)L;
-        e = __builtin_amdgcn_readlane((int)ev, off);
-        for (int nxt = off + ((e >> 24) & (int)kStop); nxt <= lim;
-             nxt = off + ((e >> 24) & (int)kStop)) {
+        if (cand && sym < 256) {
+          ev = (uint32_t)L << 24 | (uint32_t)sym << 4 | (uint32_t)L;
+          jv = lane + L;
+        }
+        for (int nxt = __builtin_amdgcn_readlane(jv, off); nxt <= lim;
+             nxt = __builtin_amdgcn_readlane(jv, off)) {
           asm("s_bitset1_b64 %0, %1" : "+s"(run) : "s"(off));
           off = nxt;
-          e = __builtin_amdgcn_readlane((int)ev, off);
         }
+        e = __builtin_amdgcn_readlane((int)ev, off);
       }
       if (run) {
         // chain steps with two literals (entries with bit 31 set, on the chain)
