@@ -11,13 +11,19 @@
 // the wave decodes it with wave-uniform control (bit buffer, positions and
 // table entries in SGPRs via readfirstlane) and uses its lanes where the work
 // is parallel: building the Huffman tables, back-reference copies (64 bytes a
-// round), flushing the output ring. Per wave LDS: a 1024-entry literal/length
-// table and a 256-entry distance table (16-bit entries: symbol | length << 9;
-// longer codes take a canonical slow path from SGPR limits), the symbols
-// sorted by code, the code lengths, and a 4 KB ring of the latest output.
-// The input is read 1 KB at a time into four VGPRs per lane (v_readlane per
-// 32 bits), so one load latency per KB of input is on the chain. The ring is flushed to HBM every
-// 1 KB; distances beyond the ring read the flushed bytes back from L2.
+// round), flushing the output ring, and literal runs a 64-bit window at a time
+// (lane l looks the table up at bit offset l; the chain of steps through the
+// window is followed with v_readlane, long codes in the window are decoded
+// lane-parallel). Per wave LDS: a 1024-entry literal/length table (32-bit
+// entries: symbol << 4 | length, and the entry's chain step with a second
+// literal), a 256-entry distance table (16-bit; longer codes take a canonical
+// path from the per-length limits), the symbols sorted by code, the code
+// lengths, and a 4 KB ring of the latest output. The input is read 1 KB at a
+// time into four VGPRs per lane (v_readlane per 32 bits), so one load latency
+// per KB of input is on the chain. The ring is flushed to HBM every 1 KB;
+// distances beyond the ring read the flushed bytes back from L2. At the
+// callers' batch sizes a launch lasts one stream's instruction stream, so the
+// window's instruction count is what the kernel is tuned on.
 //
 // k_png_unfilter: one wave per frame, 64 rows in flight (lane = row), lane k
 // working on pixel t - 2k at step t: the pixels a filter needs from the row
@@ -222,6 +228,7 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
   uint64_t bb = 0;
   int nb = 0;
   int p = 0, flushed = 0;
+  int nfe = min(kFlush, out_n + 1);  // next flush point, or the first position past the frame
 
   // over: a segment past the stream was entered. Sticky, and checked where a
   // loop iteration makes no output (block headers, the slow symbol path) and
@@ -271,6 +278,7 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
     if ((p & (kFlush - 1)) == 0) {
       flush_block(flushed);
       flushed += kFlush;
+      nfe = min(flushed + kFlush, out_n + 1);
     }
   };
 
@@ -458,10 +466,13 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
         S.ring[a1] = (uint8_t)(ev >> 4);
         S.ring[a2] = (uint8_t)(ev >> 16);
         p += nlit;
-        if (p > out_n) { err = true; break; }
-        while (p - flushed >= kFlush) {
-          flush_block(flushed);
-          flushed += kFlush;
+        if (p >= nfe) {  // a flush is due, or the output ran past the frame (one compare)
+          if (p > out_n) { err = true; break; }
+          do {
+            flush_block(flushed);
+            flushed += kFlush;
+          } while (p - flushed >= kFlush);
+          nfe = min(flushed + kFlush, out_n + 1);
         }
       }
       if (((e >> 24) & (int)kStop) != (int)kStop) continue;  // a literal past the window
@@ -551,6 +562,7 @@ __device__ __forceinline__ int inflate_stream(const uint8_t* __restrict__ in, in
         flush_block(flushed);
         flushed += kFlush;
       }
+      nfe = min(flushed + kFlush, out_n + 1);
     }
     if (err) return kErr;
   }
