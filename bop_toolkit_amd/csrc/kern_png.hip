@@ -643,6 +643,11 @@ __global__ __launch_bounds__(64 * kUnfWaves) void k_png_unfilter(
   uint16_t(*slot)[4] = s_slot[wave];
   uint64_t A = 0, B = 0;
   bool bad = false;
+  // a 16-bit pixel hi << 8 | lo as the pair hi << 16 | lo (and the raw pair
+  // x = lo << 8 | hi alike), so both bytes of a step are filtered at once
+  auto wide = [](uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0C010C00u); };   // lo, 0, hi, 0
+  auto wide_raw = [](uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0C000C01u); };  // hi, 0, lo, 0 from x
+  auto narrow = [](uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0C0C0200u); };   // hi << 8 | lo
   for (int r0 = 0; r0 < H; r0 += 64) {
     const int row = r0 + lane;
     const bool act = row < H;
@@ -654,6 +659,10 @@ __global__ __launch_bounds__(64 * kUnfWaves) void k_png_unfilter(
       B += (N - rb) * f;
       bad |= f > 4;
     }
+    // the filter types present in the pass (wave-uniform): a step computes
+    // only those, and Paeth (rare in depth images) per byte
+    const bool has1 = __any(f == 1), has2 = __any(f == 2), has3 = __any(f == 3),
+               has4 = __any(f == 4);
     // lane k works on pixel c = t - 2k at step t; steps go in groups of 8, whose
     // 16 bytes start at rb + 1 + 16 g - 4 k (the same alignment for every group)
     const int64_t g0 = rb + 1 - 4 * lane;
@@ -665,30 +674,59 @@ __global__ __launch_bounds__(64 * kUnfWaves) void k_png_unfilter(
       for (int i = 0; i < 5; ++i) w[i] = fr32[d + i];
     };
     uint32_t left = 0, upl = 0;  // this row's previous pixel, the row above's previous pixel
-    auto step = [&](uint32_t x, int c) {
-      if (act && c >= 0 && c < W) {
-        const uint32_t xh = x & 255, xl = (x >> 8) & 255;
-        const uint32_t up = row == 0 ? 0u : lane == 0 ? carry[c] : slot[lane - 1][c & 3];
-        const uint32_t hi = unfilter_byte(f, xh, left >> 8, up >> 8, upl >> 8);
-        const uint32_t lo = unfilter_byte(f, xl, left & 255, up & 255, upl & 255);
-        const uint32_t px = hi << 8 | lo;
-        slot[lane][c & 3] = (uint16_t)px;
-        if (lane == 63) carry[c] = (uint16_t)px;
-        out[(int64_t)row * W + c] = (float)px * scale;
-        const uint64_t bi = (uint64_t)(rb + 1 + 2 * c);
-        A += xh + xl;
-        B += (N - bi) * xh + (N - bi - 1) * xl;
-        left = px;
-        upl = up;
-      }
-      wave_sync();
-    };
+    // Adler-32 of the row's bytes: their sum and sum of (byte index in the row) x
+    // byte, 32-bit within a group of 8 steps, 64-bit per group
+    uint32_t rowA = 0;
+    uint64_t rowS = 0;
+    float* orow = out + (int64_t)(act ? row : 0) * W;
     auto group = [&](const uint32_t(&w)[5], int g) {
       uint32_t pl[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) pl[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+      const int c0 = 8 * g - 2 * lane;
+      float fv[8];
+      uint32_t gA = 0, gS = 0, gL = 0;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) step(pl[u >> 1] >> (16 * (u & 1)), 8 * g + u - 2 * lane);
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t x = (pl[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
+        const int c = c0 + u;
+        const bool valid = act && c >= 0 && c < W;
+        if (valid) {
+          const uint32_t up = row == 0 ? 0u : lane == 0 ? carry[c] : slot[lane - 1][c & 3];
+          const uint32_t wx = wide_raw(x), wa = wide(left), wb = wide(up);
+          uint32_t r = wx;
+          if (has1 && f == 1) r = wx + wa;
+          if (has2 && f == 2) r = wx + wb;
+          if (has3 && f == 3) r = wx + ((wa + wb) >> 1);
+          uint32_t px = narrow(r & 0x00FF00FFu);
+          if (has4 && f == 4) {
+            const uint32_t xh = x & 255, xl = x >> 8;
+            px = unfilter_byte(4, xh, left >> 8, up >> 8, upl >> 8) << 8 |
+                 unfilter_byte(4, xl, left & 255, up & 255, upl & 255);
+          }
+          slot[lane][c & 3] = (uint16_t)px;
+          if (lane == 63) carry[c] = (uint16_t)px;
+          fv[u] = (float)px * scale;
+          const uint32_t xh = x & 255, xl = x >> 8, sb = xh + xl;
+          gA += sb;
+          gS += (uint32_t)c * sb;  // byte 2c is xh, 2c + 1 is xl: 2 c (xh + xl) + xl
+          gL += xl;
+          left = px;
+          upl = up;
+        }
+        wave_sync();
+      }
+      rowA += gA;
+      rowS += 2 * (uint64_t)gS + gL;
+      if (act && c0 >= 0 && c0 + 7 < W && (W & 1) == 0) {  // 8 pixels: four aligned 8-byte stores
+        float2* o2 = reinterpret_cast<float2*>(orow + c0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o2[i] = make_float2(fv[2 * i], fv[2 * i + 1]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (act && c0 + u >= 0 && c0 + u < W) orow[c0 + u] = fv[u];
+      }
     };
     const int nsteps = W + 2 * min(63, H - 1 - r0);
     const int ng = (nsteps + 7) >> 3;
@@ -700,6 +738,10 @@ __global__ __launch_bounds__(64 * kUnfWaves) void k_png_unfilter(
       if (g + 1 >= ng) break;
       load(wa, g + 2);
       group(wb, g + 1);
+    }
+    if (act) {  // byte j of the row is byte rb + 1 + j of the stream
+      A += rowA;
+      B += (N - (uint64_t)rb - 1) * rowA - rowS;
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
