@@ -668,10 +668,14 @@ __global__ __launch_bounds__(64 * kUnfWaves) void k_png_unfilter(
     const int64_t g0 = rb + 1 - 4 * lane;
     const int sh = (int)(g0 & 3);
     const int64_t d0 = (g0 - sh) >> 2;
+    // (each word index clamped on its own: with 1-pixel rows (3 bytes) the
+    // window of a lane's first groups starts before the frame, and clamping
+    // the window would shift its alignment; the words before the frame only
+    // feed steps with c < 0)
     auto load = [&](uint32_t(&w)[5], int g) {
-      const int64_t d = min(max(d0 + 4 * (int64_t)g, (int64_t)0), last_word);
+      const int64_t d = min(d0 + 4 * (int64_t)g, last_word);
 #pragma unroll
-      for (int i = 0; i < 5; ++i) w[i] = fr32[d + i];
+      for (int i = 0; i < 5; ++i) w[i] = fr32[max(d + i, (int64_t)0)];
     };
     uint32_t left = 0, upl = 0;  // this row's previous pixel, the row above's previous pixel
     // Adler-32 of the row's bytes: their sum and sum of (byte index in the row) x
