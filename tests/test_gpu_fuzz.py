@@ -10,7 +10,8 @@ delta, taus, normalisation and cost. Step cost bit for bit, tlinear within
 and the foreign-renderer entry (bopx_vsd_from_depths) on the oracle's depth maps.
 
 BOPX_FUZZ_CASES scales the run (default 12 scenes x 8 tuples: ~20 s on the
-card, most of it the oracle's full-frame renders).
+card, most of it the oracle's full-frame renders); BOPX_FUZZ_OFFSET starts the
+seeds elsewhere (default 0).
 """
 import os
 
@@ -20,6 +21,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 CASES = int(os.environ.get("BOPX_FUZZ_CASES", "12"))
+OFFSET = int(os.environ.get("BOPX_FUZZ_OFFSET", "0"))  # first seed (fresh draws past earlier runs)
 SIZES = [(320, 240), (640, 480), (720, 540), (1280, 960)]
 
 
@@ -150,7 +152,7 @@ def _case(oracle_mod, seed):
     ctx.close()
 
 
-@pytest.mark.parametrize("seed", range(CASES))
+@pytest.mark.parametrize("seed", range(OFFSET, OFFSET + CASES))
 def test_fuzz_vsd_vs_oracle(oracle_mod, seed):
   _case(oracle_mod, seed)
 
@@ -220,7 +222,7 @@ def _point_case(oracle_mod, seed):
     assert abs(got["adi"][j] - v) <= 1e-9 * abs(v), (seed, i, "adi", got["adi"][j], v)
 
 
-@pytest.mark.parametrize("seed", range(max(1, CASES // 3)))
+@pytest.mark.parametrize("seed", range(OFFSET, OFFSET + max(1, CASES // 3)))
 def test_fuzz_point_errors_vs_oracle(oracle_mod, seed):
   _point_case(oracle_mod, seed)
 
@@ -297,6 +299,6 @@ def _gt_info_case(oracle_mod, seed):
     assert np.array_equal(mk[i, 1], np.where(visib_m, 255, 0).astype(np.uint8)), (seed, i)
 
 
-@pytest.mark.parametrize("seed", range(max(1, CASES // 3)))
+@pytest.mark.parametrize("seed", range(OFFSET, OFFSET + max(1, CASES // 3)))
 def test_fuzz_gt_info_vs_oracle(oracle_mod, seed):
   _gt_info_case(oracle_mod, seed)
