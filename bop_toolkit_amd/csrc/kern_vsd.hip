@@ -447,6 +447,9 @@ __device__ __forceinline__ T ld_off(gptr<const T> base, uint32_t byte_off) {
 }
 
 constexpr int kVsdWaves = kVsdThreads / 64;
+#ifndef BOPX_VSD_WALK_UNMASKED  // A/B switch: the unmasked walk for every class
+#define BOPX_VSD_WALK_UNMASKED 0
+#endif
 constexpr int kRowWin = 256;  // row items numbered per window (start flags)
 // covered-pixel list of a wave: its rows w, w + kVsdWaves, ... of the tile
 constexpr int kPixPerWave = (kTileH + kVsdWaves - 1) / kVsdWaves * kTileW;
@@ -533,7 +536,7 @@ void k_vsd(VsdArgs a) {
   // entry indices, no occlusion test (the list would not fit the LDS budget).
   // row-walk atomics (raster.h r_walk_row_max): unmasked for the 1-rectangle
   // objects, masked above (round 2: -0.9 % / -1.2 % on the two classes)
-  constexpr bool kWalkMasked = RPT != 1;
+  constexpr bool kWalkMasked = RPT != 1 && !BOPX_VSD_WALK_UNMASKED;
   constexpr bool kStream = RPT == 0;
   constexpr int kR = kStream ? 4 : RPT;  // rectangles per thread and round
   constexpr bool kCull = RPT >= 1 && RPT <= 2;

@@ -312,7 +312,7 @@ __device__ __forceinline__ void r_raster(const RTri& t, int cc0, int cc1, int rr
 // Balancing rows instead of whole triangles bounds a lane's walk by the widest
 // row in the batch instead of the largest bounding box.
 struct __attribute__((aligned(16))) RRow {
-  uint32_t er[3];      // edge values (+ top-left bias) at (cc0, rr0)
+  uint32_t er[3];      // edge values (+ top-left bias - 1) at (cc0, rr0)
   uint32_t duv[3];     // dU | dV << 16 (int16 each: small triangles)
   int32_t px0u, py0v;  // 256*cc0 + 128 - U0, 256*rr0 + 128 - V0
   float iz0, ga, gb;   // 1/Z plane
@@ -327,8 +327,10 @@ __device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int 
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     // |dU|, |dV|, |p0 - vertex| < 2^15 -> exact 24-bit multiplies
+    // biased by -1: a centre is inside iff every walked edge value is >= 0, so
+    // the walk reads coverage off the sign bits (no wrap: |E| < 2^31, tl - 1 <= 0)
     r.er[k] = (uint32_t)(__mul24(t.dU[k], py0 - t.Vs[k]) - __mul24(t.dV[k], px0 - t.Us[k]) +
-                         t.tl[k]);
+                         (t.tl[k] - 1));
     r.duv[k] = ((uint32_t)t.dU[k] & 0xFFFFu) | ((uint32_t)t.dV[k] << 16);
   }
   r.px0u = px0 - t.U0;
@@ -341,11 +343,14 @@ __device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int 
 }
 
 // Walk row j of a record into the LDS z-buffer, branch-free: every column issues one
-// signed atomicMax, with 0 (a no-op on the 0-initialised buffer) where the pixel
-// centre is outside the triangle. Records are regular small triangles only, so q
-// is finite (never NaN): a q <= 0 (including -0.0) has a sign bit or is +0 and
-// loses the signed max against 0, which is exactly the spec's "fragments with
-// q <= 0 are dropped" without a compare. No exec-mask branches in the loop body.
+// signed atomicMax of q's bits OR'd with the sign bit of the column's smallest
+// (biased) edge value, i.e. a negative no-op on the buffer (0-initialised, only
+// ever non-negative) where the pixel centre is outside the triangle: one
+// v_and_or_b32 instead of a compare and a select per column. Records are regular
+// small triangles only, so q is finite (never NaN): a q <= 0 (including -0.0) has
+// a sign bit or is +0 and loses the signed max against the buffer, which is
+// exactly the spec's "fragments with q <= 0 are dropped" without a compare. No
+// exec-mask branches in the loop body.
 // dep: the pose's q tile (row pitch kTileStride). Returns the fragment count
 // (diagnostics).
 // MASKED: only covered centres issue their atomicMax (exec-masked; fewer bank
@@ -388,15 +393,15 @@ __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* de
     const int32_t m1 = min((int32_t)f0, min((int32_t)f1, (int32_t)f2));
     const f32x2 q = __builtin_elementwise_fma(ga2, fdx, qrow2);
     const float q0 = q.x, q1 = q.y;
-    frags += (m0 > 0) + ((i + 1 < w) & (m1 > 0));  // diagnostics (dead in the product build)
+    frags += (m0 >= 0) + ((i + 1 < w) & (m1 >= 0));  // diagnostics (dead in the product build)
     if constexpr (kNoAtomics) {
-      asm volatile("" ::"v"(m0 > 0 ? q0 : 0.0f), "v"(m1 > 0 ? q1 : 0.0f), "v"(d + i));
+      asm volatile("" ::"v"(m0 >= 0 ? q0 : 0.0f), "v"(m1 >= 0 ? q1 : 0.0f), "v"(d + i));
     } else if constexpr (MASKED) {
-      if (m0 > 0) atomicMax(d + i, __float_as_int(q0));
-      if (m1 > 0) atomicMax(d + i + 1, __float_as_int(q1));
+      if (m0 >= 0) atomicMax(d + i, __float_as_int(q0));
+      if (m1 >= 0) atomicMax(d + i + 1, __float_as_int(q1));
     } else {
-      atomicMax(d + i, m0 > 0 ? __float_as_int(q0) : 0);
-      atomicMax(d + i + 1, m1 > 0 ? __float_as_int(q1) : 0);
+      atomicMax(d + i, __float_as_int(q0) | (m0 & INT32_MIN));
+      atomicMax(d + i + 1, __float_as_int(q1) | (m1 & INT32_MIN));
     }
     e[0] = f0 + sx[0];
     e[1] = f1 + sx[1];
