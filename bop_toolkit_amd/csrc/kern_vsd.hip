@@ -1097,7 +1097,7 @@ void k_vsd(VsdArgs a) {
             r_make_row(T, cc0, cc1, rr0, tx0, ty0, r, first,
                        s_rec[wave][__builtin_amdgcn_mbcnt_hi(
                            (uint32_t)(rbal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rbal, 0u))]);
-          int rec_base = 0;  // records started before the current pass
+          int rec_last = -1;  // the last record started before the current pass
           for (int wb = 0; wb < (VSD_DIAG(32) ? 0 : nrow); wb += kRowWin) {
             VSD_WAVE(2, 1);
             wave_lds_sync();  // records written / previous window's owners consumed
@@ -1116,16 +1116,18 @@ void k_vsd(VsdArgs a) {
             for (int p0 = 0; p0 < wn; p0 += 64) {
               const int p = p0 + lane;
               const bool valid = p < wn;
-              const uint64_t M =
-                  __builtin_amdgcn_ballot_w64(valid && ((fl4 >> (p0 >> 3)) & 0xFFu) != 0u);
-              const int owner = rec_base - 1 + (int)((M >> lane) & 1u) +
-                                (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
-              rec_base += __popcll(M);
+              const uint64_t M = __builtin_amdgcn_ballot_w64(((fl4 >> (p0 >> 3)) & 0xFFu) != 0u) &
+                                 __builtin_amdgcn_ballot_w64(valid);
+              // flags at or below the lane: bit 0 (scalar) + those of M >> 1 below it
+              const uint64_t Mh = M >> 1;
+              const int owner = rec_last + (int)(M & 1u) +
+                                (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(Mh >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)Mh, 0u));
+              rec_last += __popcll(M);
               VSD_WAVE(3, 1);
 #if BOPX_VSD_DIAG
               if VSD_DIAG(4) {
-                const int wl = valid ? (int)((s_rec[wave][owner].meta >> 12) & 63u) + 1 : 0;
+                const int wl = valid ? (int)((s_rec[wave][owner].meta >> 16) & 63u) + 1 : 0;
                 VSD_WAVE(4, diag_wave_max((wl + 1) >> 1));
               }
 #endif
@@ -1142,10 +1144,10 @@ void k_vsd(VsdArgs a) {
                   dst[2] = r2;
                 }
                 const int fr =
-                    VSD_DIAG(16) ? r_walk_row_max<true, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
-                                                        D[(rec.meta >> 18) & 1u])
-                                 : r_walk_row_max<false, kWalkMasked>(rec, wb + p - (int)(rec.meta >> 19),
-                                                  D[(rec.meta >> 18) & 1u]);
+                    VSD_DIAG(16) ? r_walk_row_max<true, kWalkMasked>(rec, wb + p - (int)(rec.pyf & 0xFFFFu),
+                                                        D[0])
+                                 : r_walk_row_max<false, kWalkMasked>(rec, wb + p - (int)(rec.pyf & 0xFFFFu),
+                                                  D[0]);
                 if VSD_DIAG(4) atomicAdd(&g_vsd_stats[5], (unsigned long long)fr);
               }
             }

@@ -314,13 +314,19 @@ __device__ __forceinline__ void r_raster(const RTri& t, int cc0, int cc1, int rr
 struct __attribute__((aligned(16))) RRow {
   uint32_t er[3];      // edge values (+ top-left bias - 1) at (cc0, rr0)
   uint32_t duv[3];     // dU | dV << 16 (int16 each: small triangles)
-  int32_t px0u, py0v;  // 256*cc0 + 128 - U0, 256*rr0 + 128 - V0
+  float px0u;          // 256*cc0 + 128 - U0 (an integer, |.| < 2^15: exact)
+  uint32_t pyf;        // first item | (256*rr0 + 128 - V0) << 16 (|.| < 2^15: small triangles)
   float iz0, ga, gb;   // 1/Z plane
-  uint32_t meta;       // cc0-x0 | (rr0-y0) << 6 | (w-1) << 12 | pose << 18 | first item << 19
+  uint32_t meta;       // byte offset of (cc0, rr0) in the q-tile pair | (w-1) << 16
 };
 static_assert(sizeof(RRow) == 48, "RRow is a 48-B LDS record");
 
 // Small triangles only; [cc0,cc1] x [rr0,rr1] inside the 64x64 tile at (x0, y0).
+// The row walk's tile address and row start are precomputed here, once per
+// triangle, instead of once per walked row: 256*rr0 + 128 - V0 lies between
+// minV - maxV and maxV - minV (rr0 within the bbox rows), an int16 for a small
+// triangle; the byte offset (pose's tile of the pair, row, column) is < 2^16.
+static_assert(2 * kTileStride * kTileH * 4 <= 65536, "q-tile pair byte offsets are 16-bit");
 __device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int rr0, int x0,
                                            int y0, int pose, int first, RRow& r) {
   const int32_t px0 = 256 * cc0 + 128, py0 = 256 * rr0 + 128;
@@ -333,13 +339,13 @@ __device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int 
                          (t.tl[k] - 1));
     r.duv[k] = ((uint32_t)t.dU[k] & 0xFFFFu) | ((uint32_t)t.dV[k] << 16);
   }
-  r.px0u = px0 - t.U0;
-  r.py0v = py0 - t.V0;
+  r.px0u = (float)(px0 - t.U0);
+  r.pyf = (uint32_t)first | ((uint32_t)(py0 - t.V0) << 16);
   r.iz0 = t.iz0;
   r.ga = t.ga;
   r.gb = t.gb;
-  r.meta = (uint32_t)(cc0 - x0) | ((uint32_t)(rr0 - y0) << 6) | ((uint32_t)(cc1 - cc0) << 12) |
-           ((uint32_t)pose << 18) | ((uint32_t)first << 19);
+  r.meta = (uint32_t)(4 * ((pose * kTileH + rr0 - y0) * kTileStride + cc0 - x0)) |
+           ((uint32_t)(cc1 - cc0) << 16);
 }
 
 // Walk row j of a record into the LDS z-buffer, branch-free: every column issues one
@@ -351,8 +357,8 @@ __device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int 
 // a sign bit or is +0 and loses the signed max against the buffer, which is
 // exactly the spec's "fragments with q <= 0 are dropped" without a compare. No
 // exec-mask branches in the loop body.
-// dep: the pose's q tile (row pitch kTileStride). Returns the fragment count
-// (diagnostics).
+// dep: the q-tile pair (row pitch kTileStride); the record's offset picks the pose's
+// tile. Returns the fragment count (diagnostics).
 // MASKED: only covered centres issue their atomicMax (exec-masked; fewer bank
 // conflicts on scattered rows) instead of every column (0 where the centre is
 // outside: no exec-mask save / restore). Round 2, same box: unmasked 0.9 %
@@ -360,11 +366,10 @@ __device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int 
 // class; skipping a column no lane covers (ballot) was 1.9 % slower.
 template <bool kNoAtomics = false, bool MASKED = true>  // kNoAtomics: timing ablation (diag builds)
 __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* dep) {
-  // j < 64 and the tile row tr < 64 always; the masks (no-ops) tell the
-  // compiler so, which keeps every multiply below on the full-rate 24-bit path.
+  // j < 64 always; the mask (a no-op) tells the compiler so, which keeps every
+  // multiply below on the full-rate 24-bit path.
   j &= 63;
-  const int tc0 = r.meta & 63u, tr = ((int)((r.meta >> 6) & 63u) + j) & 63;
-  const int w = (int)((r.meta >> 12) & 63u) + 1;
+  const int w = (int)((r.meta >> 16) & 63u) + 1;
   uint32_t e[3], sx[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -374,13 +379,14 @@ __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* de
     sx[k] = (uint32_t)__mul24(-256, dV);
   }
   // spec v5: q = fma(ga, dx, fma(gb, dy, iz0)); the row term once per row
-  const float qrow = __builtin_fmaf(r.gb, (float)(r.py0v + (j << 8)), r.iz0);
+  const float qrow = __builtin_fmaf(r.gb, (float)(((int32_t)r.pyf >> 16) + (j << 8)), r.iz0);
   // the column pair's dx (integers below 2^24: += 512 is exact), packed so the
   // two fmas and the step are one v_pk_fma_f32 / v_pk_add_f32 each
   typedef float f32x2 __attribute__((ext_vector_type(2)));
-  f32x2 fdx = {(float)r.px0u, (float)r.px0u + 256.0f};
+  f32x2 fdx = {r.px0u, r.px0u + 256.0f};
   const f32x2 ga2 = {r.ga, r.ga}, qrow2 = {qrow, qrow}, step2 = {512.0f, 512.0f};
-  int* d = reinterpret_cast<int*>(dep) + __mul24(tr, kTileStride) + tc0;
+  int* d = reinterpret_cast<int*>(reinterpret_cast<char*>(dep) + (r.meta & 0xFFFFu) +
+                                 __mul24(j, 4 * kTileStride));
   int frags = 0;
   // Two columns per iteration (independent chains). The second column of the
   // last pair may be one past the rectangle and is not masked: past the
