@@ -1127,7 +1127,7 @@ void k_vsd(VsdArgs a) {
               VSD_WAVE(3, 1);
 #if BOPX_VSD_DIAG
               if VSD_DIAG(4) {
-                const int wl = valid ? (int)((s_rec[wave][owner].meta >> 16) & 63u) + 1 : 0;
+                const int wl = valid ? (int)(s_rec[wave][owner].meta >> 25) + 1 : 0;
                 VSD_WAVE(4, diag_wave_max((wl + 1) >> 1));
               }
 #endif

@@ -316,8 +316,8 @@ struct __attribute__((aligned(16))) RRow {
   uint32_t duv[3];     // dU | dV << 16 (int16 each: small triangles)
   float px0u;          // 256*cc0 + 128 - U0 (an integer, |.| < 2^15: exact)
   uint32_t pyf;        // first item | (256*rr0 + 128 - V0) << 16 (|.| < 2^15: small triangles)
-  float iz0, ga, gb;   // 1/Z plane
-  uint32_t meta;       // byte offset of (cc0, rr0) in the q-tile pair | (w-1) << 16
+  float ga, iz0, gb;   // 1/Z plane (ga first: an even register of the 16-B read)
+  uint32_t meta;       // byte offset of (cc0, rr0) in the q-tile pair | (w-1) << 25
 };
 static_assert(sizeof(RRow) == 48, "RRow is a 48-B LDS record");
 
@@ -345,7 +345,7 @@ __device__ __forceinline__ void r_make_row(const RTri& t, int cc0, int cc1, int 
   r.ga = t.ga;
   r.gb = t.gb;
   r.meta = (uint32_t)(4 * ((pose * kTileH + rr0 - y0) * kTileStride + cc0 - x0)) |
-           ((uint32_t)(cc1 - cc0) << 16);
+           ((uint32_t)(cc1 - cc0) << 25);
 }
 
 // Walk row j of a record into the LDS z-buffer, branch-free: every column issues one
@@ -369,7 +369,7 @@ __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* de
   // j < 64 always; the mask (a no-op) tells the compiler so, which keeps every
   // multiply below on the full-rate 24-bit path.
   j &= 63;
-  const int w = (int)((r.meta >> 16) & 63u) + 1;
+  const int w = (int)(r.meta >> 25) + 1;
   uint32_t e[3], sx[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -384,7 +384,11 @@ __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* de
   // two fmas and the step are one v_pk_fma_f32 / v_pk_add_f32 each
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   f32x2 fdx = {r.px0u, r.px0u + 256.0f};
-  const f32x2 ga2 = {r.ga, r.ga}, qrow2 = {qrow, qrow}, step2 = {512.0f, 512.0f};
+  // ga and qrow in the low halves only: the packed fma reads each low half for
+  // both columns (op_sel_hi), so neither is copied into a register pair
+  const f32x2 ga_ = {r.ga, r.iz0}, step2 = {512.0f, 512.0f};
+  f32x2 qrow_;  // the high half is never read
+  qrow_.x = qrow;
   int* d = reinterpret_cast<int*>(reinterpret_cast<char*>(dep) + (r.meta & 0xFFFFu) +
                                  __mul24(j, 4 * kTileStride));
   int frags = 0;
@@ -393,11 +397,13 @@ __device__ __forceinline__ int r_walk_row_max(const RRow& r, int j, uint32_t* de
   // triangle's own bbox no pixel centre is inside it; past a tile clip it lands
   // in the padding column (tc0 + w = 64 < kTileStride) or, for a tile cut by
   // the ROI, in the column right of it, which the pixel compaction clears.
-  for (int i = 0; i < w; i += 2, fdx += step2) {
+  // i < w  <=>  i << 25 <= meta (the offset below bit 25; i <= 64: no wrap)
+  for (int i = 0; ((uint32_t)i << 25) <= r.meta; i += 2, fdx += step2) {
     const uint32_t f0 = e[0] + sx[0], f1 = e[1] + sx[1], f2 = e[2] + sx[2];
     const int32_t m0 = min((int32_t)e[0], min((int32_t)e[1], (int32_t)e[2]));
     const int32_t m1 = min((int32_t)f0, min((int32_t)f1, (int32_t)f2));
-    const f32x2 q = __builtin_elementwise_fma(ga2, fdx, qrow2);
+    f32x2 q;  // {fma(ga, fdx.x, qrow), fma(ga, fdx.y, qrow)}
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(q) : "v"(ga_), "v"(fdx), "v"(qrow_));
     const float q0 = q.x, q1 = q.y;
     frags += (m0 >= 0) + ((i + 1 < w) & (m1 >= 0));  // diagnostics (dead in the product build)
     if constexpr (kNoAtomics) {

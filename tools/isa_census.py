@@ -47,6 +47,8 @@ FUNCS = {  # device function -> phase
     "wave_sum_u32": "epilogue", "wave_sum_f64": "epilogue",
 }
 REGIONS = [  # (start, stop, phase) inside k_vsd
+    ("auto raster_tile = [&]", "for (int claimed = 0;; claimed = 1)", "tile_loop"),
+    ("for (int t = sp, it = 0;", "if constexpr (COST == kCostRender) return;", "tile_loop"),
     ("auto step_exact = [&]", "auto vsd_px = [&]", "exact"),
     ("if (unc) {  // undo", "} else {  // tlinear", "exact"),
     ("for (int wb = 0; wb <", "VSD_STAMP(11);", "walk"),
@@ -56,7 +58,6 @@ REGIONS = [  # (start, stop, phase) inside k_vsd
     ("for (int claimed = 0;; claimed = 1)", "int cnt = 0;", "staging"),
     ("auto list_tile = [&]", "for (int t = sp, it = 0;", "list"),
     ("}  // rounds (kStream)", "// Touch the test-depth lines", "list"),
-    ("for (int t = sp, it = 0;", "for (int claimed = 0;; claimed = 1)", "tile_loop"),
     ("// Touch the test-depth lines", "// 3. per-pixel distances", "coeffs_touch"),
     ("// 3. per-pixel distances", "// step cost: the certified", "pixel_compaction"),
     ("// step cost: the certified", "// 4. workgroup reduction", "pixel"),
@@ -72,7 +73,7 @@ LOOP_REGIONS = [
     ("for (int wb = 0; wb <", "for (int p0 = 0; p0 < wn", "row_windows"),
     ("for (int c0 = 0; c0 <", "for (int wb = 0; wb <", "setup_chunks"),
     ("for (int claimed = 0;; claimed = 1)", "int cnt = 0;", "claim_iters"),
-    ("for (int t = sp, it = 0;", "for (int claimed = 0;; claimed = 1)", "tile_iters"),
+    ("for (int t = sp, it = 0;", "if constexpr (COST == kCostRender) return;", "tile_iters"),
     ("// 3. per-pixel distances", "// step cost: the certified", "pix_compact_rows"),
     ("for (int i = lane; i < npix; i += 64)", "VSD_STAMP(4);", "pix_iters"),
     ("func", "r_raster", "slow"),
