@@ -554,6 +554,7 @@ void k_vsd(VsdArgs a) {
   __shared__ float s_zr[2][2];  // per pose: depth range of the meshlet corners (min, max)
   __shared__ int s_nexts[kQueues];
   __shared__ __attribute__((aligned(16))) float s_pose[2][12];
+  __shared__ __attribute__((aligned(16))) float s_pose_pk[2][12];  // r_vertex_pk order
   __shared__ int s_roi[4];
   __shared__ int s_nlists[kQueues];
   __shared__ int s_nsmalls[kQueues];
@@ -614,8 +615,13 @@ void k_vsd(VsdArgs a) {
   c32.cx = (float)(cx + (double)ox);  // the renderer receives cx + offset (float64)
   c32.cy = (float)(cy + (double)oy);
   if (tid < 12) {
-    s_pose[0][tid] = (float)a.pose_est[12 * b + tid];
-    s_pose[1][tid] = (float)a.pose_gt[12 * b + tid];
+    const float pe = (float)a.pose_est[12 * b + tid], pg = (float)a.pose_gt[12 * b + tid];
+    s_pose[0][tid] = pe;
+    s_pose[1][tid] = pg;
+    // pair order {R0,R3, R1,R4, R2,R5, t0,t1, R6,R7,R8, t2}: element tid's slot
+    const int d = (int)((0xb76a98531420ull >> (4 * tid)) & 15u);
+    s_pose_pk[0][d] = pe;
+    s_pose_pk[1][d] = pg;
   }
   const double diam = COST == 0 && a.normalized ? a.diameters[b] : 1.0;
   // Step cost: per-pixel dd >= T_k. Normalised by a finite diameter > 0 with
@@ -982,11 +988,8 @@ void k_vsd(VsdArgs a) {
         float izl[kGroup];  // this lane's vertex 1/Z (0 for an invalid vertex)
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
-          const float4* P = reinterpret_cast<const float4*>(&s_pose[pose[g]][0]);
-          const float4 p0 = P[0], p1 = P[1], p2 = P[2];  // 3 x ds_read_b128
-          const float Rf[12] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y,
-                                p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
-          const RVtx rv = r_vertex(Rf, c32, v[g].x, v[g].y, v[g].z);
+          // 3 x ds_read_b128 of the pose in pair order (X and Y in packed ops)
+          const RVtx rv = r_vertex_pk(&s_pose_pk[pose[g]][0], c32, v[g].x, v[g].y, v[g].z);
           w_stage[g * kMeshletVerts + lane] = rv;
           izl[g] = rv.iz;
         }

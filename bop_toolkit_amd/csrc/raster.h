@@ -77,6 +77,36 @@ __device__ __forceinline__ RVtx r_vertex(const float* __restrict__ Rf, const Cam
   return o;
 }
 
+// r_vertex with X and Y computed as the two halves of packed float32 ops
+// (v_pk_mul_f32 / v_pk_add_f32: the same IEEE operations in the same order,
+// no contraction, so the same bits). P: the pose in pair order
+// {R0,R3, R1,R4, R2,R5, t0,t1, R6,R7,R8, t2} (16-B aligned).
+__device__ __forceinline__ RVtx r_vertex_pk(const float* __restrict__ P, const Cam32& c, float x,
+                                            float y, float z) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const float4 p0 = reinterpret_cast<const float4*>(P)[0];
+  const float4 p1 = reinterpret_cast<const float4*>(P)[1];
+  const float4 p2 = reinterpret_cast<const float4*>(P)[2];
+  const f32x2 r03 = {p0.x, p0.y}, r14 = {p0.z, p0.w}, r25 = {p1.x, p1.y}, t01 = {p1.z, p1.w};
+  const f32x2 xx = {x, x}, yy = {y, y}, zz = {z, z};
+  const f32x2 XY = ((r03 * xx + r14 * yy) + r25 * zz) + t01;
+  // Z in scalar ops: the empty asm keeps the SLP vectoriser from pairing its
+  // products (the pairs would cost more register copies than they save)
+  float zx = p2.x * x, zy = p2.y * y, zz1 = p2.z * z;
+  asm("" : "+v"(zx), "+v"(zy), "+v"(zz1));
+  const float Z = ((zx + zy) + zz1) + p2.w;
+  const float iz = rcp_rn(Z);
+  const f32x2 f = {c.fx, c.fy}, cc = {c.cx, c.cy}, izz = {iz, iz};
+  const f32x2 uv = (f * XY) * izz + cc;
+  const f32x2 uv256 = uv * (f32x2){256.0f, 256.0f};
+  RVtx o;
+  const bool ok = (int)(Z > 0.0f) & (int)(fabsf(uv.x) <= kGuardBand) & (int)(fabsf(uv.y) <= kGuardBand);
+  o.U = ok ? (int32_t)__builtin_rintf(ok ? uv256.x : 0.0f) : INT32_MIN;
+  o.V = ok ? (int32_t)__builtin_rintf(ok ? uv256.y : 0.0f) : 0;
+  o.iz = ok ? iz : 0.0f;
+  return o;
+}
+
 __device__ __forceinline__ int64_t r_floor_div256(int64_t a) {
   return a >= 0 ? a / 256 : -((-a + 255) / 256);
 }
