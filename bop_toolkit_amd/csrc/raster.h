@@ -266,8 +266,10 @@ __device__ __forceinline__ bool r_touches(RVtx a, RVtx b, RVtx c, int x0, int x1
                                           int y1) {
   const int32_t minU = min(a.U, min(b.U, c.U)), maxU = max(a.U, max(b.U, c.U));
   const int32_t minV = min(a.V, min(b.V, c.V)), maxV = max(a.V, max(b.V, c.V));
-  return a.ok() && b.ok() && c.ok() && max((minU + 127) >> 8, x0) <= min((maxU - 128) >> 8, x1) &&
-         max((minV + 127) >> 8, y0) <= min((maxV - 128) >> 8, y1);
+  // branch-free: an invalid vertex (U = INT32_MIN, V = 0) is the minimum U, so one
+  // compare covers the three validity tests, and no term can overflow
+  return (int)(minU != INT32_MIN) & (int)(max((minU + 127) >> 8, x0) <= min((maxU - 128) >> 8, x1)) &
+         (int)(max((minV + 127) >> 8, y0) <= min((maxV - 128) >> 8, y1));
 }
 
 // Spec v5 fragment value: fused plane evaluation, clamped to izmax for an
