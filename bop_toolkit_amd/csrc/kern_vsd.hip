@@ -1017,12 +1017,13 @@ void k_vsd(VsdArgs a) {
         int cnt = 0;
 #pragma unroll
         for (int g = 0; g < kGroup; ++g) {
-          bool hit = false;
-          if (pk[g] != 0xFFFFFFFFu) {
-            const RVtx* sg = &w_stage[g * kMeshletVerts];
-            hit = r_touches(sg[pk[g] & 255u], sg[(pk[g] >> 8) & 255u], sg[(pk[g] >> 16) & 255u],
-                            tx0, tx1, ty0, ty1);
-          }
+          // branch-free: a lane without a triangle (pk = ~0) tests vertex 0 three
+          // times and is masked out, so the hit mask feeds the ballot directly
+          const bool has = pk[g] != 0xFFFFFFFFu;
+          const uint32_t pkg = has ? pk[g] : 0u;
+          const RVtx* sg = &w_stage[g * kMeshletVerts];
+          const bool hit = has & r_touches(sg[pkg & 255u], sg[(pkg >> 8) & 255u],
+                                           sg[(pkg >> 16) & 255u], tx0, tx1, ty0, ty1);
           const unsigned long long bal = __ballot(hit);
           if (hit)
             w_tri[cnt + __popcll(bal & ((1ull << lane) - 1ull))] =
